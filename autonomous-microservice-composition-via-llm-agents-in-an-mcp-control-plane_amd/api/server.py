@@ -1,0 +1,130 @@
+"""FastAPI surface.
+
+Same routes and request/response field names as the reference
+(control_plane.py:39-43, 79-85, 140-151):
+
+* ``POST /plan``             {intent} -> {graph}
+* ``POST /execute``          {graph, payload} -> {results, errors}
+* ``POST /plan_and_execute`` {intent} -> {results, errors}  (payload ``{}``,
+  control_plane.py:151)
+
+plus ``GET /metrics`` (Prometheus text, README.md:43-44) and ``GET /healthz``.
+
+Differences by design: the app is built by a factory (no import-time DB
+connection), the HTTP client is lifespan-managed (D14) and the
+planner is awaited instead of blocking the event loop (D9).  Error semantics
+are kept: a planner reply that is not a JSON object -> 500, missing
+``intent`` -> 422, a failed node without fallback -> 502 (T7, T8).
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+from typing import Optional
+
+import httpx
+from fastapi import FastAPI
+from fastapi.responses import PlainTextResponse
+from pydantic import BaseModel
+
+from ..config import Settings
+from ..orchestrator import Orchestrator
+from ..planner.base import Planner, StubPlanner
+from ..registry import BaseRegistry, make_registry
+from ..utils.metrics import METRICS
+
+logging.basicConfig(level=logging.INFO)
+
+
+class PlanRequest(BaseModel):
+    intent: str
+
+
+class PlanResponse(BaseModel):
+    graph: dict
+
+
+class ExecuteRequest(BaseModel):
+    graph: dict
+    payload: dict
+
+
+class ExecuteResponse(BaseModel):
+    results: dict
+    errors: dict
+
+
+def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegistry] = None,
+               planner: Optional[Planner] = None,
+               transport: Optional[httpx.AsyncBaseTransport] = None) -> FastAPI:
+    settings = settings or Settings.from_env()
+    registry = registry if registry is not None else make_registry(settings.redis_url,
+                                                                   settings.services_prefix)
+    state = {}
+
+    def _make_planner() -> Planner:
+        if planner is not None:
+            return planner
+        if settings.planner_backend == "local":
+            from ..planner.local import LocalPlanner
+            return LocalPlanner.from_settings(settings, registry)
+        return StubPlanner(registry)
+
+    @contextlib.asynccontextmanager
+    async def lifespan(app: FastAPI):
+        client = httpx.AsyncClient(transport=transport) if transport is not None else httpx.AsyncClient()
+        state["orch"] = Orchestrator(client=client, timeout=settings.exec_timeout,
+                                     retries=settings.retries,
+                                     concurrent_generations=settings.concurrent_generations,
+                                     registry=registry,
+                                     use_registry_fallback=settings.use_registry_fallback,
+                                     telemetry_to_registry=settings.telemetry_to_registry)
+        state["planner"] = _make_planner()
+        try:
+            yield
+        finally:
+            await state["planner"].aclose()
+            await client.aclose()
+
+    app = FastAPI(lifespan=lifespan)
+    app.state.registry = registry
+    app.state.settings = settings
+    app.state.components = state
+
+    @app.post("/plan", response_model=PlanResponse)
+    async def plan_intent(req: PlanRequest):
+        return PlanResponse(graph=await state["planner"].plan(req.intent))
+
+    @app.post("/execute", response_model=ExecuteResponse)
+    async def run_graph(req: ExecuteRequest):
+        return ExecuteResponse(**await state["orch"].execute(req.graph, req.payload))
+
+    @app.post("/plan_and_execute", response_model=ExecuteResponse)
+    async def plan_and_run(req: PlanRequest):
+        graph = PlanResponse(graph=await state["planner"].plan(req.intent)).graph
+        return ExecuteResponse(**await state["orch"].execute(graph, {}))
+
+    @app.get("/metrics", response_class=PlainTextResponse)
+    async def metrics():
+        return METRICS.render()
+
+    @app.get("/healthz")
+    async def healthz():
+        return {"ok": True, "services": len(registry.list_services())}
+
+    return app
+
+
+def main():  # pragma: no cover - CLI entry (reference :155-157)
+    import argparse
+
+    import uvicorn
+    ap = argparse.ArgumentParser(description="MI355X MCP control plane")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8000)
+    args = ap.parse_args()
+    uvicorn.run(create_app(), host=args.host, port=args.port)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main()

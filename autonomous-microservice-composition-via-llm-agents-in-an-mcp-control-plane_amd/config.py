@@ -1,0 +1,78 @@
+"""Typed settings.
+
+The reference reads three environment variables (control_plane.py:17-19) and
+hard-codes everything else (key prefix :20, model/temperature :70-72, timeout
+:109/:123, host/port :157).  We keep the env var names ``REDIS_URL`` and
+``POSTGRES_DSN`` (the latter is accepted but unused: the schema-embedding store
+lives in HBM, see ``retrieval``) and expose the rest as ``MCP_*`` variables.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import Optional
+
+SERVICES_PREFIX = "mcp:service:"
+TELEMETRY_PREFIX = "mcp:telemetry:"
+
+
+def _env(name: str, default, cast=str):
+    raw = os.getenv(name)
+    if raw is None or raw == "":
+        return default
+    if cast is bool:
+        return raw.strip().lower() in ("1", "true", "yes", "on")
+    return cast(raw)
+
+
+@dataclasses.dataclass
+class Settings:
+    # registry
+    redis_url: Optional[str] = None          # None -> in-memory registry
+    postgres_dsn: Optional[str] = None       # accepted for parity, unused
+    services_prefix: str = SERVICES_PREFIX
+    # planner
+    planner_backend: str = "stub"            # stub | local
+    model: str = "llama3-8b"                 # llama3-8b | llama3-70b | tiny
+    tp: int = 1
+    replicas: int = 1
+    max_batch: int = 256
+    max_step_tokens: int = 8192
+    kv_blocks: int = 0                       # 0 -> size from free HBM
+    temperature: float = 0.2                 # control_plane.py:72
+    max_nodes: int = 6
+    topk: int = 32                           # schema retrieval: services kept in prompt
+    retrieval_threshold: int = 48            # prune only when registry is larger
+    embed_dim: int = 1024
+    seed: int = 0
+    # orchestrator
+    exec_timeout: float = 5.0                # control_plane.py:109,123
+    retries: int = 0                         # parity default (reference has none)
+    concurrent_generations: bool = False     # parity default: strictly serial
+    use_registry_fallback: bool = False      # parity default: edge fallback only
+    telemetry_to_registry: bool = False
+
+    @classmethod
+    def from_env(cls) -> "Settings":
+        return cls(
+            redis_url=_env("REDIS_URL", None),
+            postgres_dsn=_env("POSTGRES_DSN", None),
+            planner_backend=_env("MCP_PLANNER_BACKEND", "stub"),
+            model=_env("MCP_MODEL", "llama3-8b"),
+            tp=_env("MCP_TP", 1, int),
+            replicas=_env("MCP_REPLICAS", 1, int),
+            max_batch=_env("MCP_MAX_BATCH", 256, int),
+            max_step_tokens=_env("MCP_MAX_STEP_TOKENS", 8192, int),
+            kv_blocks=_env("MCP_KV_BLOCKS", 0, int),
+            temperature=_env("MCP_TEMPERATURE", 0.2, float),
+            max_nodes=_env("MCP_MAX_NODES", 6, int),
+            topk=_env("MCP_TOPK", 32, int),
+            retrieval_threshold=_env("MCP_RETRIEVAL_THRESHOLD", 48, int),
+            embed_dim=_env("MCP_EMBED_DIM", 1024, int),
+            seed=_env("MCP_SEED", 0, int),
+            exec_timeout=_env("MCP_EXEC_TIMEOUT", 5.0, float),
+            retries=_env("MCP_RETRIES", 0, int),
+            concurrent_generations=_env("MCP_CONCURRENT_GENERATIONS", False, bool),
+            use_registry_fallback=_env("MCP_USE_REGISTRY_FALLBACK", False, bool),
+            telemetry_to_registry=_env("MCP_TELEMETRY_TO_REGISTRY", False, bool),
+        )
