@@ -1,0 +1,232 @@
+// K5/K6: unified paged, causal, GQA attention for ragged batches (prefill,
+// extend/jump-forward chunks and single-token decode in ONE kernel family).
+//
+// Layouts
+//   q       [T, Hq, D]            rotated queries (rope_kv output)
+//   k/v     [num_blocks, Hkv, 64, D]  paged cache, block = one 64-key tile
+//   out     [T, Hq, D]
+// Work item = (sequence, q-tile of QT tokens) x kv-head.  All G = Hq/Hkv query
+// heads that share a kv head are processed together, so each K/V tile is read
+// once per group (GQA), and the 16 MFMA rows of a wave are (16/G tokens) x G heads.
+//
+// Math per wave (D = 128, v_mfma_f32_16x16x32_bf16):
+//   S^T[key][qrow] = K . Q^T  (K from LDS as the A operand, Q in registers as B)
+//   -> every lane owns one query row (lane&15): the online-softmax rescale of O
+//      is a per-lane scalar, row max/sum need two xor-shuffles (16, 32);
+//   O^T[d][qrow] += V^T . P^T with P^T taken straight from the S^T accumulators
+//      (key order permuted identically in both operands,
+//      cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's
+//      operand") and V^T read with ds_read_b64_tr_b16 (T10).
+// K/V tiles: global_load_lds_dwordx4 into a double-buffered LDS ring with the
+// 256-B-row XOR swizzle chunk ^= row&15 on source and read (tools/lds_banks.py).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int D = 128;
+constexpr int KT = 64;                        // keys per tile == cache block size
+constexpr int TILE = KT * D;                  // bf16 elements per K or V tile (16 KiB)
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+DEV bf16x4 tr_read(const bf16* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+template <int NW, int G>
+__global__ __launch_bounds__(NW * 64) void attn_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    bf16* __restrict__ out, const int* __restrict__ q_start, const int* __restrict__ q_len,
+    const int* __restrict__ ctx_len, const int* __restrict__ block_table, int max_blocks,
+    const int* __restrict__ work_seq, const int* __restrict__ work_q0, int Hq, int Hkv,
+    float scale_log2) {
+  constexpr int TPW = 16 / G;                 // tokens per wave
+  constexpr int QT = NW * TPW;                // tokens per work item
+  constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
+  static_assert(PIECES % NW == 0, "pieces split evenly");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];   // [buf][K|V][64][128]
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kvh = blockIdx.y;
+  const int s = work_seq[blockIdx.x];
+  const int q0 = work_q0[blockIdx.x];
+  const int qs = q_start[s], ql = q_len[s], cl = ctx_len[s];
+  const int* bt = block_table + (size_t)s * max_blocks;
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // this lane's query row
+  const int tok = q0 + wave * TPW + fr / G;   // index inside the sequence's query span
+  const int head = kvh * G + fr % G;
+  const bool qvalid = tok < ql;
+  const int qpos = cl - ql + tok;             // absolute position (causal bound)
+
+  // last position any row of this work item needs
+  const int last_tok = min(q0 + QT, ql) - 1;
+  const int kv_end = cl - ql + last_tok + 1;
+  const int ntiles = (kv_end + KT - 1) / KT;
+
+  // Q fragments (B operand): lane holds Q[row fr][d = 32ks + 8fq + j]
+  bf16x8 qf[4];
+  {
+    const bf16* qp = q + ((size_t)(qs + (qvalid ? tok : 0)) * Hq + head) * D + 8 * fq;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 32 * ks);
+      if (!qvalid) qf[ks] = bf16x8{};
+    }
+  }
+
+  // staging: piece p covers rows 4p..4p+3 of the K (p<16) or V (p>=16) tile
+  const int srow = lane >> 4;
+  auto stage = [&](int kt, int buf) {
+    const size_t blk = (size_t)bt[kt];
+    const bf16* kb = kc + (blk * Hkv + kvh) * (size_t)TILE;
+    const bf16* vb = vc + (blk * Hkv + kvh) * (size_t)TILE;
+    bf16* base = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < PIECES / NW; ++i) {
+      const int p = wave * (PIECES / NW) + i;
+      const int tile = p >> 4, pr = p & 15;
+      const int row = pr * 4 + srow;
+      const int chunk = (lane & 15) ^ (row & 15);
+      const bf16* src = (tile ? vb : kb) + row * D + chunk * 8;
+      glds16(src, base + tile * TILE + pr * 512);
+    }
+  };
+
+  f32x4 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_part = 0.f;
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
+    const bf16* Kl = smem + cur * 2 * TILE;
+    const bf16* Vl = Kl + TILE;
+
+    // ---- S^T = K Q^T : 4 key sub-tiles x 4 d-steps
+    f32x4 sacc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sacc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int row = nt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c = ks * 4 + fq;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * D + ((c ^ (row & 15)) << 3));
+        sacc[nt] = mfma16x16x32(kf, qf[ks], sacc[nt]);
+      }
+    }
+    // ---- mask + online softmax (this lane: query row fr, keys 16nt + 4fq + r)
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * KT + nt * 16 + fq * 4 + r;
+        float v = sacc[nt][r] * scale_log2;
+        v = (key <= qpos && key < cl) ? v : -INFINITY;
+        sacc[nt][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    m_run = m_new;
+    float psum = 0.f;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sacc[nt][r] - m_use);
+        psum += p;
+        pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
+      }
+    l_part = l_part * alpha + psum;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+
+    // ---- O^T += V^T P^T  (V^T via transposed LDS reads, permuted key order)
+    const int tq = (lane & 15) >> 2, tp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int col = dt * 16 + tp * 4;
+      const int chunk = col >> 3, half = (col & 7);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int key0 = k2 * 32 + fq * 4 + tq;
+        const int key1 = key0 + 16;
+        const bf16x4 v0 = tr_read(Vl + key0 * D + ((chunk ^ (key0 & 15)) << 3) + half);
+        const bf16x4 v1 = tr_read(Vl + key1 * D + ((chunk ^ (key1 & 15)) << 3) + half);
+        const bf16x8 vf = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        o[dt] = mfma16x16x32(vf, pf[k2], o[dt]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + r]
+  float l_tot = l_part + __shfl_xor(l_part, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (!qvalid) return;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  bf16* op = out + ((size_t)(qs + tok) * Hq + head) * D + 4 * fq;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    bf16x4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv);
+    *reinterpret_cast<bf16x4*>(op + dt * 16) = w;
+  }
+}
+
+template <int G>
+void attn_dispatch(int nw, const bf16* q, const bf16* kc, const bf16* vc, bf16* out,
+                   const int* q_start, const int* q_len, const int* ctx_len, const int* bt,
+                   int max_blocks, const int* ws, const int* wq, int nwork, int Hq, int Hkv,
+                   float sl2, hipStream_t s) {
+  const dim3 grid(nwork, Hkv);
+  if (nw == 1)
+    attn_kernel<1, G><<<grid, 64, 0, s>>>(q, kc, vc, out, q_start, q_len, ctx_len, bt, max_blocks,
+                                          ws, wq, Hq, Hkv, sl2);
+  else
+    attn_kernel<4, G><<<grid, 256, 0, s>>>(q, kc, vc, out, q_start, q_len, ctx_len, bt,
+                                           max_blocks, ws, wq, Hq, Hkv, sl2);
+}
+
+}  // namespace
+
+int attn_tokens_per_item(int nw, int group) { return nw * (16 / group); }
+
+int launch_paged_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
+                           const int* q_start, const int* q_len, const int* ctx_len,
+                           const int* block_table, int max_blocks, const int* work_seq,
+                           const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
+                           float scale, hipStream_t s) {
+  if (head_dim != D) return 1;
+  if (nw != 1 && nw != 4) return 2;
+  if (nwork <= 0) return 0;
+  const float sl2 = scale * 1.4426950408889634f;
+  const int G = Hq / Hkv;
+  auto qq = (const bf16*)q;
+  auto kk = (const bf16*)k_cache;
+  auto vv = (const bf16*)v_cache;
+  auto oo = (bf16*)out;
+  switch (G) {
+    case 1: attn_dispatch<1>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
+    case 2: attn_dispatch<2>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
+    case 4: attn_dispatch<4>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
+    case 8: attn_dispatch<8>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
+    case 16: attn_dispatch<16>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
+    default: return 3;
+  }
+  return 0;
+}

@@ -1,0 +1,161 @@
+// PyTorch bindings of the gfx950 kernel library (pybind11 + ATen).
+// Shape / dtype / device checks live here so the .hip launchers stay raw and
+// graph-capturable; every op runs on the current HIP stream of the tensor's
+// device.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include "kernels.h"
+
+namespace {
+
+inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_BF16_TENSOR(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_BF16(t)
+#define CHECK_I32_TENSOR(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_I32(t)
+
+void rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, double eps) {
+  CHECK_BF16_TENSOR(x); CHECK_BF16_TENSOR(w); CHECK_BF16_TENSOR(out);
+  const int H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0 && w.numel() == H && out.sizes() == x.sizes(), "rmsnorm shapes");
+  launch_rmsnorm(x.data_ptr(), w.data_ptr(), out.data_ptr(), x.numel() / H, H, (float)eps, stream());
+}
+
+void add_rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& out,
+                 double eps) {
+  CHECK_BF16_TENSOR(x); CHECK_BF16_TENSOR(residual); CHECK_BF16_TENSOR(w); CHECK_BF16_TENSOR(out);
+  const int H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0 && w.numel() == H && residual.sizes() == x.sizes() &&
+              out.sizes() == x.sizes(), "add_rmsnorm shapes");
+  launch_add_rmsnorm(x.data_ptr(), residual.data_ptr(), w.data_ptr(), out.data_ptr(),
+                     x.numel() / H, H, (float)eps, stream());
+}
+
+void silu_mul(const at::Tensor& x, at::Tensor& y) {
+  CHECK_BF16_TENSOR(x); CHECK_BF16_TENSOR(y);
+  const int F = y.size(-1);
+  TORCH_CHECK(F % 8 == 0 && x.size(-1) == 2 * F && x.numel() == 2 * y.numel(), "silu_mul shapes");
+  launch_silu_mul(x.data_ptr(), y.data_ptr(), y.numel() / F, F, stream());
+}
+
+void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
+  CHECK_I32_TENSOR(ids); CHECK_BF16_TENSOR(table); CHECK_BF16_TENSOR(out);
+  const int H = table.size(1);
+  TORCH_CHECK(H % 8 == 0 && out.size(-1) == H && out.numel() == ids.numel() * H, "embedding shapes");
+  launch_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), H, stream());
+}
+
+void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slots,
+             const at::Tensor& cos_sin, at::Tensor& q_out, at::Tensor& k_cache,
+             at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D) {
+  CHECK_BF16_TENSOR(qkv); CHECK_I32_TENSOR(pos); CHECK_I32_TENSOR(slots);
+  CHECK_BF16_TENSOR(q_out); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache);
+  CHECK_DEV(cos_sin); CHECK_CONTIG(cos_sin);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 3 &&
+              cos_sin.size(1) == D / 2 && cos_sin.size(2) == 2, "cos_sin [P, D/2, 2] f32");
+  const int T = pos.numel();
+  TORCH_CHECK(qkv.numel() == (int64_t)T * (Hq + 2 * Hkv) * D, "qkv shape");
+  TORCH_CHECK(q_out.numel() == (int64_t)T * Hq * D, "q_out shape");
+  TORCH_CHECK(slots.numel() == T, "slots shape");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "cache [nb, Hkv, BS, D]");
+  TORCH_CHECK(D == 128 || D == 64, "head_dim must be 64 or 128");
+  launch_rope_kv(qkv.data_ptr(), pos.data_ptr<int>(), slots.data_ptr<int>(), cos_sin.data_ptr(),
+                 q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D,
+                 k_cache.size(2), stream());
+}
+
+void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::optional<at::Tensor>& R) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
+  const int K = X.size(-1);
+  const int M = X.numel() / K;
+  const int N = W.size(0);
+  TORCH_CHECK(W.dim() == 2 && W.size(1) == K, "W must be [N, K]");
+  TORCH_CHECK(Y.numel() == (int64_t)M * N && Y.size(-1) == N, "Y must be [M, N]");
+  const int rc = gemm_tn_check(M, N, K);
+  TORCH_CHECK(rc == 0, "gemm: unsupported shape M=", M, " N=", N, " K=", K, " (code ", rc, ")");
+  const void* rp = nullptr;
+  if (R.has_value()) {
+    CHECK_BF16_TENSOR((*R));
+    TORCH_CHECK(R->numel() == Y.numel(), "R shape");
+    rp = R->data_ptr();
+  }
+  launch_gemm_tn(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, stream());
+}
+
+void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                     at::Tensor& out, const at::Tensor& q_start, const at::Tensor& q_len,
+                     const at::Tensor& ctx_len, const at::Tensor& block_table,
+                     const at::Tensor& work_seq, const at::Tensor& work_q0, int64_t nw,
+                     double scale) {
+  CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
+  CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
+  CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq); CHECK_I32_TENSOR(work_q0);
+  TORCH_CHECK(q.dim() == 3, "q must be [T, Hq, D]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64, "cache block size must be 64");
+  const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
+  TORCH_CHECK(block_table.dim() == 2, "block_table [S, max_blocks]");
+  TORCH_CHECK(work_seq.numel() == work_q0.numel(), "work list");
+  const int rc = launch_paged_attention(
+      q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
+      q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
+      block_table.size(1), work_seq.data_ptr<int>(), work_q0.data_ptr<int>(), work_seq.numel(), nw,
+      Hq, Hkv, D, (float)scale, stream());
+  TORCH_CHECK(rc == 0, "paged_attention: unsupported config (code ", rc, ")");
+}
+
+void sample_allowed(const at::Tensor& hidden, const at::Tensor& W, const at::Tensor& allow_ptr,
+                    const at::Tensor& allow_ids, const at::Tensor& ctr, double temperature,
+                    int64_t seed, at::Tensor& out_tok, const c10::optional<at::Tensor>& out_logit) {
+  CHECK_BF16_TENSOR(hidden); CHECK_BF16_TENSOR(W);
+  CHECK_I32_TENSOR(allow_ptr); CHECK_I32_TENSOR(allow_ids); CHECK_I32_TENSOR(out_tok);
+  CHECK_DEV(ctr); TORCH_CHECK(ctr.scalar_type() == at::kLong, "ctr int64");
+  const int S = hidden.size(0), H = hidden.size(1);
+  TORCH_CHECK(W.size(1) == H && H % 8 == 0, "W [V, H]");
+  TORCH_CHECK(allow_ptr.numel() == S + 1 && out_tok.numel() == S && ctr.numel() == S, "sample shapes");
+  float* lp = nullptr;
+  if (out_logit.has_value()) lp = out_logit->data_ptr<float>();
+  launch_sample_allowed(hidden.data_ptr(), W.data_ptr(), allow_ptr.data_ptr<int>(),
+                        allow_ids.data_ptr<int>(), (const long long*)ctr.data_ptr<int64_t>(),
+                        (float)temperature, (unsigned long long)seed, S, H,
+                        out_tok.data_ptr<int>(), lp, stream());
+}
+
+void sample_dense(const at::Tensor& logits, const at::Tensor& ctr, double temperature,
+                  int64_t seed, at::Tensor& out_tok) {
+  CHECK_BF16_TENSOR(logits); CHECK_I32_TENSOR(out_tok);
+  TORCH_CHECK(ctr.scalar_type() == at::kLong, "ctr int64");
+  launch_sample_dense(logits.data_ptr(), logits.size(0), logits.size(1),
+                      (const long long*)ctr.data_ptr<int64_t>(), (float)temperature,
+                      (unsigned long long)seed, out_tok.data_ptr<int>(), stream());
+}
+
+void add_inplace(at::Tensor& y, const at::Tensor& x) {
+  CHECK_BF16_TENSOR(y); CHECK_BF16_TENSOR(x);
+  TORCH_CHECK(y.numel() == x.numel() && y.numel() % 8 == 0, "add_inplace shapes");
+  launch_add_inplace(y.data_ptr(), x.data_ptr(), y.numel(), stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels for the MCP planner engine";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("add_rmsnorm", &add_rmsnorm);
+  m.def("silu_mul", &silu_mul);
+  m.def("embedding", &embedding);
+  m.def("rope_kv", &rope_kv);
+  m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none());
+  m.def("paged_attention", &paged_attention);
+  m.def("attn_tokens_per_item", &attn_tokens_per_item);
+  m.def("sample_allowed", &sample_allowed, py::arg("hidden"), py::arg("W"), py::arg("allow_ptr"),
+        py::arg("allow_ids"), py::arg("ctr"), py::arg("temperature"), py::arg("seed"),
+        py::arg("out_tok"), py::arg("out_logit") = py::none());
+  m.def("sample_dense", &sample_dense);
+  m.def("add_inplace", &add_inplace);
+}

@@ -1,0 +1,148 @@
+// K1/K2: bf16 "TN" GEMM on MFMA for every Llama projection.
+//   Y[M,N] = X[M,K] · W[N,K]^T   (+ R[M,N] when RESID: fused residual add)
+// X = activations (row-major, K contiguous), W = nn.Linear weight (out x in,
+// K contiguous), fp32 accumulation, bf16 out.
+//
+// Structure (cdna_hip_programming.md §5, "Minimum 2-phase" T3+T4 recipe):
+//  * 128x128 block tile, BK = 64, 256 threads = 4 waves in a 2x2 grid, each wave
+//    64x64 = 4x4 v_mfma_f32_16x16x32_bf16 tiles.
+//  * global -> LDS with global_load_lds_dwordx4 (one 1 KiB wave-instruction = 8
+//    rows x 128 B), double-buffered: tile k+1 is in flight while tile k is read.
+//  * LDS image is lane-linear; the XOR swizzle chunk ^= row&7 is applied on the
+//    SOURCE address and on the ds_read_b128 address (rule 21) -> conflict-free
+//    (tools/lds_banks.py).
+//  * operands swapped in the MFMA (W as A, X as B) so each lane ends with 4
+//    consecutive output columns of one row -> 8-byte bf16 stores.
+//  * XCD-aware bijective block remap + grouped tile order for L2 reuse (T1).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_ELEMS = 128 * BK;          // one operand tile, bf16 elements (16 KiB)
+
+template <bool RESID>
+__global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X,
+                                                      const bf16* __restrict__ W,
+                                                      bf16* __restrict__ Y,
+                                                      const bf16* __restrict__ R, int M, int N,
+                                                      int K) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE_ELEMS];   // [buf][A|B][128][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const int nwg = nm * nn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  // grouped ordering: GROUP m-tiles share each W panel
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * nn;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP;
+  const int gsz = min(nm - first_m, GROUP);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging addresses: wave w stages pieces 4w..4w+3 of each operand
+  const int lrow = lane >> 3;                  // row inside the 8-row piece
+  const int lchunk = (lane & 7) ^ lrow;        // inverse swizzle on the source
+  const bf16* srcA[4];
+  const bf16* srcB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 8 + lrow;
+    const int ra = min(m0 + row, M - 1);
+    const int rb = min(n0 + row, N - 1);
+    srcA[i] = X + (size_t)ra * K + lchunk * 8;
+    srcB[i] = W + (size_t)rb * K + lchunk * 8;
+  }
+  auto stage = [&](int kt, int buf) {
+    bf16* la = smem + (buf * 2 + 0) * TILE_ELEMS;
+    bf16* lb = smem + (buf * 2 + 1) * TILE_ELEMS;
+    const int koff = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(srcA[i] + koff, la + (wave * 4 + i) * 512);
+      glds16(srcB[i] + koff, lb + (wave * 4 + i) * 512);
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage(0, 0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const bf16* la = smem + (cur * 2 + 0) * TILE_ELEMS;
+    const bf16* lb = smem + (cur * 2 + 1) * TILE_ELEMS;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int ra = wm * 64 + t * 16 + fr;
+        const int rb = wn * 64 + t * 16 + fr;
+        af[t] = *reinterpret_cast<const bf16x8*>(la + ra * BK + ((c ^ (ra & 7)) << 3));
+        bfr[t] = *reinterpret_cast<const bf16x8*>(lb + rb * BK + ((c ^ (rb & 7)) << 3));
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(bfr[nt], af[mt], acc[mt][nt]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds Y[m][n..n+3]
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int m = m0 + wm * 64 + mt * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int n = n0 + wn * 64 + nt * 16 + fq * 4;
+      if (n >= N) continue;
+      f32x4 v = acc[mt][nt];
+      if (RESID) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+      *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+    }
+  }
+}
+
+}  // namespace
+
+int gemm_tn_check(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 1;
+  if (K % 64) return 2;
+  if (N % 4) return 3;
+  return 0;
+}
+
+void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                    hipStream_t s) {
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const dim3 grid(nm * nn);
+  if (R)
+    gemm_tn_128<true><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                           (const bf16*)R, M, N, K);
+  else
+    gemm_tn_128<false><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M,
+                                            N, K);
+}

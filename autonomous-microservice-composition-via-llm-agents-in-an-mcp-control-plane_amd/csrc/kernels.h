@@ -1,0 +1,39 @@
+// Host-side launch API of the gfx950 kernel library.  Every launcher takes raw
+// device pointers and a HIP stream, performs no allocation and no host sync,
+// so all of them are safe inside hipGraph stream capture.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+// elementwise.hip
+void launch_rmsnorm(const void* x, const void* w, void* out, int T, int H, float eps,
+                    hipStream_t s);
+void launch_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int H,
+                        float eps, hipStream_t s);
+void launch_silu_mul(const void* x, void* y, int T, int F, hipStream_t s);
+void launch_embedding(const int* ids, const void* table, void* out, int T, int H, hipStream_t s);
+void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const void* cos_sin,
+                    void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
+                    int BS, hipStream_t s);
+void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
+
+// gemm.hip
+int gemm_tn_check(int M, int N, int K);
+void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                    hipStream_t s);
+
+// attention.hip
+int attn_tokens_per_item(int nw, int group);
+int launch_paged_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
+                           const int* q_start, const int* q_len, const int* ctx_len,
+                           const int* block_table, int max_blocks, const int* work_seq,
+                           const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
+                           float scale, hipStream_t s);
+
+// sampling.hip
+void launch_sample_allowed(const void* hidden, const void* W, const int* allow_ptr,
+                           const int* allow_ids, const long long* ctr, float temperature,
+                           unsigned long long seed, int S, int H, int* out_tok, float* out_logit,
+                           hipStream_t s);
+void launch_sample_dense(const void* logits, int S, int V, const long long* ctr, float temperature,
+                         unsigned long long seed, int* out_tok, hipStream_t s);

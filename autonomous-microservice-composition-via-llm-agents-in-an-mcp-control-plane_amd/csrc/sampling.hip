@@ -1,0 +1,112 @@
+// K9: LM head + grammar mask + temperature sampling, fused.
+//
+// Constrained decoding only ever samples from a small allowed set per sequence
+// (the DAG grammar's choice points, planner/grammar.py).  Masking the full
+// 128,256-entry softmax to that set is mathematically identical to a softmax
+// over the allowed tokens only, so this kernel computes the logits of the
+// allowed rows of the LM head (one 8 KiB row dot-product per allowed token)
+// and draws with Gumbel-max:  argmax_i (logit_i / T + g_i),  g_i ~ Gumbel(0,1)
+// from a counter-based hash RNG (reproducible per (seed, sequence counter, token)).
+// T <= 0 selects greedy decoding.
+#include "common.h"
+#include "kernels.h"
+
+__global__ __launch_bounds__(256) void sample_allowed_kernel(
+    const bf16* __restrict__ hidden, const bf16* __restrict__ W, const int* __restrict__ allow_ptr,
+    const int* __restrict__ allow_ids, const long long* __restrict__ ctr, float inv_temp,
+    unsigned long long seed, int H, int* __restrict__ out_tok, float* __restrict__ out_logit) {
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int a0 = allow_ptr[s], a1 = allow_ptr[s + 1];
+  const bf16* h = hidden + (size_t)s * H;
+  const int nvec = H >> 3;
+  float best = -INFINITY, best_logit = 0.f;
+  int best_tok = -1;
+  for (int a = a0 + wave; a < a1; a += 4) {
+    const int tok = allow_ids[a];
+    const bf16* w = W + (size_t)tok * H;
+    float acc = 0.f;
+    for (int c = lane; c < nvec; c += 64) {
+      const bf16x8 x = reinterpret_cast<const bf16x8*>(h)[c];
+      const bf16x8 y = reinterpret_cast<const bf16x8*>(w)[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += (float)x[j] * (float)y[j];
+    }
+    acc = wave_sum(acc);
+    float score = acc;
+    if (inv_temp > 0.f) {
+      const float u = uniform01(seed, (unsigned long long)ctr[s], (unsigned long long)tok);
+      score = acc * inv_temp - __logf(-__logf(u));
+    }
+    if (score > best) {
+      best = score;
+      best_tok = tok;
+      best_logit = acc;
+    }
+  }
+  __shared__ float sb[4], sl[4];
+  __shared__ int st[4];
+  if (lane == 0) {
+    sb[wave] = best;
+    st[wave] = best_tok;
+    sl[wave] = best_logit;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int bi = 0;
+    for (int i = 1; i < 4; ++i)
+      if (st[i] >= 0 && (st[bi] < 0 || sb[i] > sb[bi])) bi = i;
+    out_tok[s] = st[bi];
+    if (out_logit) out_logit[s] = sl[bi];
+  }
+}
+
+void launch_sample_allowed(const void* hidden, const void* W, const int* allow_ptr,
+                           const int* allow_ids, const long long* ctr, float temperature,
+                           unsigned long long seed, int S, int H, int* out_tok, float* out_logit,
+                           hipStream_t s) {
+  if (S <= 0) return;
+  const float inv_t = temperature > 0.f ? 1.f / temperature : 0.f;
+  sample_allowed_kernel<<<S, 256, 0, s>>>((const bf16*)hidden, (const bf16*)W, allow_ptr,
+                                          allow_ids, ctr, inv_t, seed, H, out_tok, out_logit);
+}
+
+// Dense variant: logits [S, V] (fp32 or bf16 via the GEMM), optional -inf mask
+// folded in by the caller.  One block per row, Gumbel-max over the full vocab.
+__global__ __launch_bounds__(256) void sample_dense_kernel(const bf16* __restrict__ logits, int V,
+                                                           const long long* __restrict__ ctr,
+                                                           float inv_temp,
+                                                           unsigned long long seed,
+                                                           int* __restrict__ out_tok) {
+  const int s = blockIdx.x;
+  const bf16* row = logits + (size_t)s * V;
+  float best = -INFINITY;
+  int bt = 0;
+  for (int i = threadIdx.x; i < V; i += 256) {
+    const float l = (float)row[i];
+    float sc = l;
+    if (inv_temp > 0.f) sc = l * inv_temp - __logf(-__logf(uniform01(seed, (unsigned long long)ctr[s], (unsigned long long)i)));
+    if (sc > best) { best = sc; bt = i; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int ot = __shfl_xor(bt, o, 64);
+    if (ob > best || (ob == best && ot < bt)) { best = ob; bt = ot; }
+  }
+  __shared__ float sb[4];
+  __shared__ int st[4];
+  if ((threadIdx.x & 63) == 0) { sb[threadIdx.x >> 6] = best; st[threadIdx.x >> 6] = bt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int bi = 0;
+    for (int i = 1; i < 4; ++i) if (sb[i] > sb[bi]) bi = i;
+    out_tok[s] = st[bi];
+  }
+}
+
+void launch_sample_dense(const void* logits, int S, int V, const long long* ctr, float temperature,
+                         unsigned long long seed, int* out_tok, hipStream_t s) {
+  if (S <= 0) return;
+  const float inv_t = temperature > 0.f ? 1.f / temperature : 0.f;
+  sample_dense_kernel<<<S, 256, 0, s>>>((const bf16*)logits, V, ctr, inv_t, seed, out_tok);
+}

@@ -1,0 +1,110 @@
+"""Per-step batch metadata (host side) for the ragged, paged forward pass.
+
+One engine step feeds a ragged batch: sequence ``s`` contributes ``q_len[s]``
+new tokens (1 for decode, a chunk for prefill / grammar jump-forward) whose KV
+lands in the paged cache, and attends causally to ``ctx_len[s]`` keys.
+
+All int32 metadata of a step is packed into ONE host buffer and moved with ONE
+host->device copy (``pack``); the attention work lists are derived here too:
+sequences with few new tokens go to the 1-wave kernel variant, longer ones to
+the 4-wave variant (csrc/attention.hip).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+BLOCK_SIZE = 64
+
+
+def tokens_per_item(nw: int, group: int) -> int:
+    return nw * (16 // group)
+
+
+@dataclasses.dataclass
+class AttnMeta:
+    q_start: torch.Tensor      # [S] int32
+    q_len: torch.Tensor        # [S]
+    ctx_len: torch.Tensor      # [S]
+    block_table: torch.Tensor  # [S, max_blocks]
+    work: List[tuple]          # [(nw, work_seq[int32], work_q0[int32]), ...]
+
+    def work_lists(self):
+        return self.work
+
+
+def build_work(q_len: Sequence[int], group: int, small_cutoff: Optional[int] = None):
+    """Split each sequence's query span into work items.
+
+    Returns {nw: (seq_ids, q0s)} with nw in {1, 4}."""
+    t1 = tokens_per_item(1, group)
+    t4 = tokens_per_item(4, group)
+    cutoff = t1 * 2 if small_cutoff is None else small_cutoff
+    out = {1: ([], []), 4: ([], [])}
+    for s, ql in enumerate(q_len):
+        if ql <= 0:
+            continue
+        nw, qt = (1, t1) if ql <= cutoff else (4, t4)
+        for q0 in range(0, ql, qt):
+            out[nw][0].append(s)
+            out[nw][1].append(q0)
+    return out
+
+
+@dataclasses.dataclass
+class StepInputs:
+    """Host-side description of one forward step."""
+    token_ids: np.ndarray      # [T] int32
+    positions: np.ndarray      # [T] int32
+    slots: np.ndarray          # [T] int32 (physical KV slot, -1 = skip)
+    q_start: np.ndarray        # [S]
+    q_len: np.ndarray          # [S]
+    ctx_len: np.ndarray        # [S]
+    block_table: np.ndarray    # [S, max_blocks]
+    logit_rows: np.ndarray     # [R] token row whose hidden feeds sampling
+
+    @property
+    def num_tokens(self) -> int:
+        return int(self.token_ids.shape[0])
+
+
+@dataclasses.dataclass
+class DeviceStep:
+    token_ids: torch.Tensor
+    positions: torch.Tensor
+    slots: torch.Tensor
+    logit_rows: torch.Tensor
+    attn: AttnMeta
+
+
+def pack(step: StepInputs, group: int, device, pin: bool = True) -> DeviceStep:
+    """Pack all int32 arrays into one buffer -> one H2D copy -> views."""
+    work = build_work(step.q_len.tolist(), group)
+    parts = [step.token_ids, step.positions, step.slots, step.logit_rows, step.q_start,
+             step.q_len, step.ctx_len, step.block_table.reshape(-1)]
+    for nw in (1, 4):
+        parts += [np.asarray(work[nw][0], np.int32), np.asarray(work[nw][1], np.int32)]
+    sizes = [int(p.size) for p in parts]
+    host = np.concatenate([np.asarray(p, dtype=np.int32).reshape(-1) for p in parts])
+    t = torch.from_numpy(host)
+    if device is not None and torch.device(device).type == "cuda":
+        if pin:
+            t = t.pin_memory()
+        t = t.to(device, non_blocking=True)
+    views, off = [], 0
+    for n in sizes:
+        views.append(t[off:off + n])
+        off += n
+    S = step.q_len.shape[0]
+    bt = views[7].view(S, -1) if S else views[7].view(0, 1)
+    work_l = []
+    for i, nw in enumerate((1, 4)):
+        ws, wq = views[8 + 2 * i], views[9 + 2 * i]
+        if ws.numel():
+            work_l.append((nw, ws, wq))
+    meta = AttnMeta(q_start=views[4], q_len=views[5], ctx_len=views[6], block_table=bt, work=work_l)
+    return DeviceStep(token_ids=views[0], positions=views[1], slots=views[2], logit_rows=views[3],
+                      attn=meta)

@@ -1,0 +1,157 @@
+"""Python entry points of the gfx950 kernel library.
+
+GPU tensors always run the hand-written HIP kernels from the in-tree
+``_kernels*.so`` (built by ``csrc/build.py``); if that library is missing on a
+GPU box the first GPU op raises — there is no silent eager fallback.  CPU
+tensors run the fp32 references in ``ops.reference`` (CPU test tier only).
+"""
+from __future__ import annotations
+
+import glob
+import importlib.machinery
+import importlib.util
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_LIB = None
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class KernelLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the HIP kernel extension module."""
+    global _LIB
+    if _LIB is None:
+        cands = sorted(glob.glob(os.path.join(_HERE, "_kernels*.so")))
+        if not cands:
+            raise KernelLibraryMissing(
+                "HIP kernel library not built: run `python csrc/build.py` "
+                "(or __graft_entry__.build()) before using GPU tensors")
+        loader = importlib.machinery.ExtensionFileLoader("_kernels", cands[0])
+        spec = importlib.util.spec_from_file_location("_kernels", cands[0], loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _LIB = mod
+    return _LIB
+
+
+def library_path() -> Optional[str]:
+    c = sorted(glob.glob(os.path.join(_HERE, "_kernels*.so")))
+    return c[0] if c else None
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (KernelLibraryMissing, ImportError, OSError):
+        return False
+
+
+# --------------------------------------------------------------------- ops
+def rmsnorm(x, w, eps, out=None):
+    if x.is_cuda:
+        out = torch.empty_like(x) if out is None else out
+        lib().rmsnorm(x, w, out, eps)
+        return out
+    r = ref.rmsnorm(x, w, eps)
+    return r if out is None else out.copy_(r)
+
+
+def add_rmsnorm(x, residual, w, eps, out=None):
+    """residual += x (in place, bf16); returns rmsnorm(residual) * w."""
+    if x.is_cuda:
+        out = torch.empty_like(x) if out is None else out
+        lib().add_rmsnorm(x, residual, w, out, eps)
+        return out
+    r = ref.add_rmsnorm(x, residual, w, eps)
+    return r if out is None else out.copy_(r)
+
+
+def silu_mul(x, out=None):
+    F = x.shape[-1] // 2
+    if x.is_cuda:
+        out = x.new_empty(*x.shape[:-1], F) if out is None else out
+        lib().silu_mul(x, out)
+        return out
+    r = ref.silu_mul(x)
+    return r if out is None else out.copy_(r)
+
+
+def embedding(ids, table, out=None):
+    if table.is_cuda:
+        out = table.new_empty(ids.numel(), table.shape[1]) if out is None else out
+        lib().embedding(ids, table, out)
+        return out
+    r = table[ids.long()]
+    return r if out is None else out.copy_(r)
+
+
+def gemm(X, W, R=None, out=None):
+    """Y = X @ W^T (+ R).  X [M, K], W [N, K]."""
+    if X.is_cuda:
+        out = X.new_empty(*X.shape[:-1], W.shape[0]) if out is None else out
+        lib().gemm(X, W, out, R)
+        return out
+    r = ref.gemm(X, W, R)
+    return r if out is None else out.copy_(r)
+
+
+def rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D):
+    if qkv.is_cuda:
+        lib().rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
+    else:
+        ref.rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
+    return q_out
+
+
+def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
+    """``meta`` is an ``AttnMeta`` (engine.batch) holding the per-sequence and
+    work-list int32 tensors."""
+    if q.is_cuda:
+        out = torch.empty_like(q) if out is None else out
+        L = lib()
+        for nw, ws, wq in meta.work_lists():
+            L.paged_attention(q, k_cache, v_cache, out, meta.q_start, meta.q_len, meta.ctx_len,
+                              meta.block_table, ws, wq, nw, scale)
+        return out
+    r = ref.paged_attention(q, k_cache, v_cache, meta.q_start, meta.q_len, meta.ctx_len,
+                            meta.block_table, scale)
+    return r if out is None else out.copy_(r)
+
+
+def sample_allowed(hidden, W, allow_ptr, allow_ids, ctr, temperature, seed, out_tok=None,
+                   out_logit=None):
+    if hidden.is_cuda:
+        out_tok = torch.empty(hidden.shape[0], dtype=torch.int32, device=hidden.device) \
+            if out_tok is None else out_tok
+        lib().sample_allowed(hidden, W, allow_ptr, allow_ids, ctr, temperature, seed, out_tok,
+                             out_logit)
+        return out_tok
+    # CPU: same Gumbel-max semantics with torch's RNG
+    toks = []
+    g = torch.Generator().manual_seed(int(seed))
+    for ids, logits in ref.sample_allowed_logits(hidden, W, allow_ptr, allow_ids):
+        if temperature > 0:
+            u = torch.rand(logits.shape, generator=g).clamp_(1e-7, 1 - 1e-7)
+            sc = logits / temperature - torch.log(-torch.log(u))
+        else:
+            sc = logits
+        toks.append(int(ids[int(torch.argmax(sc))]))
+    t = torch.tensor(toks, dtype=torch.int32)
+    return t if out_tok is None else out_tok.copy_(t)
+
+
+def add_inplace(y, x):
+    if y.is_cuda:
+        lib().add_inplace(y, x)
+    else:
+        y.add_(x)
+    return y

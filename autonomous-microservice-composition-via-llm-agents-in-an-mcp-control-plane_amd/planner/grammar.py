@@ -1,0 +1,253 @@
+"""DAG-JSON grammar -> token constraints.
+
+A random-init (or any) model's unconstrained output would rarely parse (the
+reference returns HTTP 500 on non-JSON, control_plane.py:74).  The
+planner therefore decodes under a grammar that can only produce a T2 DAG over
+registry services:
+
+    {"nodes":[{"name":"<svc>","endpoint":"<its endpoint>",
+               "inputs":{"<key>":"<payload field | earlier node>",...},
+               "retries":<0-3>}, ...],
+     "edges":[{"from":"<src>","to":"<dst>"[,"fallback":"<registry fallback>"]}, ...]}
+
+The model decides: which service comes next (or stop), the source of every
+input field, the retry count and whether each edge carries a fallback.  Every
+other character is forced.  Edges are derived from the chosen input sources
+(producer -> consumer), so the graph is acyclic and names are unique by
+construction.
+
+Decoding mechanics: a *choice* is a prefix-free set of alternative strings;
+each alternative is tokenised standalone and the choice becomes a token trie.
+At a trie node with one child the token is forced (no sampling); with several
+children the engine samples from exactly those children (``allowed``).  Forced
+text after a decision is appended as a jump-forward span: its tokens still run
+through the model (their KV is needed) but in a single batched forward.
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, List, Optional, Sequence, Tuple
+
+RETRY_CHOICES = ["0", "1", "2", "3"]
+
+
+class Trie:
+    __slots__ = ("children", "leaf", "mask")
+
+    def __init__(self):
+        self.children: Dict[int, "Trie"] = {}
+        self.leaf: int = -1        # alternative index ending here
+        self.mask: int = 0         # bitmask of alternatives below
+
+
+def build_trie(token_seqs: Sequence[Sequence[int]]) -> Trie:
+    root = Trie()
+    for i, seq in enumerate(token_seqs):
+        if not seq:
+            raise ValueError("empty alternative")
+        node = root
+        node.mask |= 1 << i
+        for t in seq:
+            node = node.children.setdefault(t, Trie())
+            node.mask |= 1 << i
+        if node.leaf >= 0 or node.children:
+            raise ValueError("alternatives are not prefix-free")
+        node.leaf = i
+    for n in _walk(root):
+        if n.leaf >= 0 and n.children:
+            raise ValueError("alternatives are not prefix-free")
+    return root
+
+
+def _walk(n: Trie):
+    yield n
+    for c in n.children.values():
+        yield from _walk(c)
+
+
+class GrammarSpec:
+    """Per-plan constants: candidate services, their token tries, caches."""
+
+    def __init__(self, services: Sequence[dict], tokenizer, max_nodes: int = 6,
+                 allow_retries: bool = True):
+        self.services = list(services)
+        self.tok = tokenizer
+        self.max_nodes = max(1, max_nodes)
+        self.allow_retries = allow_retries
+        self.names = [s["name"] for s in self.services]
+        self.keys = [self._input_keys(s) for s in self.services]
+        self._trie_cache: Dict[Tuple[str, ...], Trie] = {}
+        self.name_trie = self.trie(tuple(json.dumps(n) for n in self.names))
+
+    @staticmethod
+    def _input_keys(s) -> List[str]:
+        sch = s.get("input_schema") or {}
+        if isinstance(sch.get("properties"), dict):
+            return list(sch["properties"].keys())
+        return [k for k in sch.keys() if k not in ("type", "required", "$schema", "title")]
+
+    def encode(self, text: str) -> List[int]:
+        return self.tok.encode(text)
+
+    def trie(self, alts: Tuple[str, ...]) -> Trie:
+        t = self._trie_cache.get(alts)
+        if t is None:
+            t = build_trie([self.tok.encode(a) for a in alts])
+            self._trie_cache[alts] = t
+        return t
+
+
+class DagDecoder:
+    """Per-request grammar state machine.
+
+    Protocol with the engine::
+
+        toks = dec.advance()      # forced tokens to append (may be empty)
+        if dec.done: ...
+        allowed = dec.allowed()   # >=2 token ids: sample one
+        dec.feed(token)           # then advance() again
+    """
+
+    def __init__(self, spec: GrammarSpec):
+        self.spec = spec
+        self.text_parts: List[str] = []
+        self.done = False
+        self._gen = self._program()
+        self._choice: Optional[Tuple[Tuple[str, ...], Trie, int]] = None   # (alts, node, live mask)
+        self._node: Optional[Trie] = None
+        self._pending_tokens: List[int] = []
+        self._result_index: Optional[int] = None
+        self._step_gen(None)
+
+    # ------------------------------------------------------------- program
+    def _program(self):
+        sp = self.spec
+        yield ('{"nodes":[{"name":', None)
+        used_mask = 0
+        chosen: List[int] = []
+        node_inputs: List[Dict[str, str]] = []
+        while True:
+            live = ((1 << len(sp.names)) - 1) & ~used_mask
+            alts = tuple(json.dumps(n) for n in sp.names)
+            idx = yield (None, (alts, sp.name_trie, live))
+            used_mask |= 1 << idx
+            svc = sp.services[idx]
+            text = ',"endpoint":' + json.dumps(svc["endpoint"]) + ',"inputs":{'
+            yield (text, None)
+            inputs = {}
+            prev_names = [sp.names[j] for j in chosen]
+            for ki, key in enumerate(sp.keys[idx]):
+                yield (("," if ki else "") + json.dumps(key) + ":", None)
+                srcs = [key] + [n for n in prev_names if n != key]
+                alts_s = tuple(json.dumps(x) for x in srcs)
+                if len(alts_s) == 1:
+                    yield (alts_s[0], None)
+                    inputs[key] = srcs[0]
+                else:
+                    si = yield (None, (alts_s, sp.trie(alts_s), (1 << len(alts_s)) - 1))
+                    inputs[key] = srcs[si]
+            if sp.allow_retries:
+                yield ('},"retries":', None)
+                alts_r = tuple(RETRY_CHOICES)
+                yield (None, (alts_r, sp.trie(alts_r), (1 << len(alts_r)) - 1))
+                yield ("}", None)
+            else:
+                yield ("}}", None)
+            chosen.append(idx)
+            node_inputs.append(inputs)
+            can_more = len(chosen) < sp.max_nodes and used_mask != (1 << len(sp.names)) - 1
+            if not can_more:
+                break
+            alts_c = (',{"name":', '],"edges":[')
+            ci = yield (None, (alts_c, sp.trie(alts_c), 3))
+            if ci == 1:
+                break
+        if not (len(chosen) < sp.max_nodes and used_mask != (1 << len(sp.names)) - 1):
+            yield ('],"edges":[', None)
+        # edges: producer -> consumer for every node-valued input source
+        first = True
+        for j, idx in enumerate(chosen):
+            dst = sp.names[idx]
+            srcs = []
+            for v in node_inputs[j].values():
+                if v in sp.names and v != dst and v not in srcs and \
+                        sp.names.index(v) in chosen[:j]:
+                    srcs.append(v)
+            for src in srcs:
+                yield (("" if first else ",") + '{"from":' + json.dumps(src) + ',"to":'
+                       + json.dumps(dst), None)
+                first = False
+                fb = sp.services[idx].get("fallback")
+                if fb:
+                    alts_f = (',"fallback":' + json.dumps(fb) + "}", "}")
+                    yield (None, (alts_f, sp.trie(alts_f), 3))
+                else:
+                    yield ("}", None)
+        yield ("]}", None)
+
+    def _step_gen(self, send):
+        """Run the program until the next choice (or the end), collecting forced text."""
+        try:
+            item = self._gen.send(send) if send is not None or self._gen.gi_frame.f_lasti >= 0 \
+                else next(self._gen)
+        except StopIteration:
+            self.done = True
+            self._choice = None
+            return
+        while True:
+            text, choice = item
+            if text is not None:
+                self.text_parts.append(text)
+                self._pending_tokens += self.spec.encode(text)
+                try:
+                    item = next(self._gen)
+                except StopIteration:
+                    self.done = True
+                    self._choice = None
+                    return
+                continue
+            alts, trie, live = choice
+            self._choice = (alts, trie, live)
+            self._node = trie
+            return
+
+    # ------------------------------------------------------------ protocol
+    def _live_children(self):
+        alts, trie, live = self._choice
+        return [t for t, c in self._node.children.items() if c.mask & live]
+
+    def advance(self) -> List[int]:
+        """Return forced tokens (jump-forward), resolving single-child trie steps."""
+        while not self.done and self._choice is not None:
+            kids = self._live_children()
+            if len(kids) != 1:
+                break
+            self._take(kids[0])
+        out, self._pending_tokens = self._pending_tokens, []
+        return out
+
+    def allowed(self) -> List[int]:
+        return self._live_children()
+
+    def feed(self, token: int) -> None:
+        if token not in self._node.children or not (self._node.children[token].mask & self._choice[2]):
+            raise ValueError(f"token {token} not allowed by the grammar")
+        self._take(token)
+
+    def _take(self, token: int):
+        self._pending_tokens.append(token)
+        self._node = self._node.children[token]
+        if self._node.leaf >= 0:
+            alts = self._choice[0]
+            idx = self._node.leaf
+            self.text_parts.append(alts[idx])
+            self._choice = None
+            self._step_gen(idx)
+
+    # -------------------------------------------------------------- result
+    @property
+    def text(self) -> str:
+        return "".join(self.text_parts)
+
+    def result(self) -> dict:
+        return json.loads(self.text)

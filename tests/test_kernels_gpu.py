@@ -1,0 +1,181 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 reference
+(SURVEY §4.3.2).  Runs only on a real MI355X (``-m gpu``)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import mcp_amd.ops as ops
+from mcp_amd.engine.batch import StepInputs, pack
+from mcp_amd.ops import reference as ref
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")]
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_native_library_loaded():
+    assert ops.library_path() is not None
+    ops.lib()   # raises if the .so cannot be loaded
+
+
+@pytest.mark.parametrize("T,H", [(1, 4096), (37, 4096), (5, 8192), (3, 256)])
+def test_rmsnorm(T, H):
+    x = torch.randn(T, H, device=DEV).bfloat16()
+    w = (torch.rand(H, device=DEV) + 0.5).bfloat16()
+    out = ops.rmsnorm(x, w, 1e-5)
+    assert rel_err(out, ref.rmsnorm(x, w, 1e-5)) < 1e-2
+    r = torch.randn(T, H, device=DEV).bfloat16()
+    r_ref = r.clone()
+    out2 = ops.add_rmsnorm(x, r, w, 1e-5)
+    exp = ref.add_rmsnorm(x, r_ref, w, 1e-5)
+    assert rel_err(r, r_ref) < 1e-2 and rel_err(out2, exp) < 1e-2
+
+
+def test_silu_mul_embedding_add():
+    x = torch.randn(19, 2 * 1024, device=DEV).bfloat16()
+    assert rel_err(ops.silu_mul(x), ref.silu_mul(x)) < 1e-2
+    table = torch.randn(1000, 512, device=DEV).bfloat16()
+    ids = torch.randint(0, 1000, (33,), device=DEV, dtype=torch.int32)
+    assert torch.equal(ops.embedding(ids, table), table[ids.long()])
+    y = torch.randn(64, 64, device=DEV).bfloat16()
+    y0 = y.clone()
+    z = torch.randn(64, 64, device=DEV).bfloat16()
+    ops.add_inplace(y, z)
+    assert rel_err(y, y0.float() + z.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (17, 384, 256), (128, 128, 4096), (300, 1024, 512),
+                                   (1000, 6144, 4096), (64, 1284, 128), (4096, 4096, 4096)])
+def test_gemm(M, N, K):
+    torch.manual_seed(0)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    Y = ops.gemm(X, W)
+    assert rel_err(Y, ref.gemm(X, W)) < 1e-2
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    Y2 = ops.gemm(X, W, R=R)
+    assert rel_err(Y2, ref.gemm(X, W, R)) < 1e-2
+
+
+def test_gemm_orientation_exact():
+    # A = I, asymmetric B: catches a transposed C-write (cdna_hip_programming.md §3)
+    K = 128
+    X = torch.eye(K, device=DEV).bfloat16()
+    W = torch.arange(K * K, device=DEV).reshape(K, K).remainder(97).bfloat16()
+    Y = ops.gemm(X, W)
+    assert torch.equal(Y.float(), W.t().float())
+
+
+def _cache(nb, Hkv, D=128, BS=64):
+    k = torch.randn(nb, Hkv, BS, D, device=DEV).bfloat16()
+    v = torch.randn(nb, Hkv, BS, D, device=DEV).bfloat16()
+    return k, v
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (8, 8), (16, 8)])
+def test_rope_kv(Hq, Hkv):
+    D, T = 128, 45
+    cs = ref.rope_cos_sin(4096, D, 500000.0, DEV)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).bfloat16()
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(8 * 64, device=DEV)[:T].int()
+    slots[3] = -1
+    kc, vc = _cache(8, Hkv)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q1 = torch.empty(T, Hq, D, device=DEV).bfloat16()
+    q2 = q1.clone()
+    ops.rope_kv(qkv, pos, slots, cs, q1, kc, vc, Hq, Hkv, D)
+    ref.rope_kv(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), q2_cpu := q2.cpu(), kc2_cpu := kc2.cpu(),
+                vc2_cpu := vc2.cpu(), Hq, Hkv, D)
+    assert rel_err(q1.cpu(), q2_cpu) < 1e-2
+    assert rel_err(kc.cpu(), kc2_cpu) < 1e-2
+    assert torch.equal(vc.cpu(), vc2_cpu)
+
+
+def _attn_case(q_lens, ctx_lens, Hq, Hkv, seed=0):
+    torch.manual_seed(seed)
+    D, BS = 128, 64
+    S = len(q_lens)
+    nblk = [(c + BS - 1) // BS for c in ctx_lens]
+    nb = sum(nblk) + 3
+    kc, vc = _cache(nb, Hkv)
+    perm = torch.randperm(nb).tolist()
+    maxb = max(nblk)
+    bt = np.zeros((S, maxb), np.int32)
+    o = 0
+    for s in range(S):
+        bt[s, :nblk[s]] = perm[o:o + nblk[s]]
+        o += nblk[s]
+    T = sum(q_lens)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    qs = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    step = StepInputs(token_ids=np.zeros(T, np.int32), positions=np.zeros(T, np.int32),
+                      slots=np.zeros(T, np.int32), q_start=qs,
+                      q_len=np.asarray(q_lens, np.int32), ctx_len=np.asarray(ctx_lens, np.int32),
+                      block_table=bt, logit_rows=np.zeros(0, np.int32))
+    dev = pack(step, Hq // Hkv, DEV)
+    out = ops.paged_attention(q, kc, vc, dev.attn, 1 / math.sqrt(D))
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), torch.from_numpy(qs),
+                              torch.tensor(q_lens), torch.tensor(ctx_lens), torch.from_numpy(bt),
+                              1 / math.sqrt(D))
+    return out.cpu(), exp
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (8, 8)])
+def test_paged_attention_mixed(Hq, Hkv):
+    q_lens = [1, 1, 7, 130, 64, 3, 1]
+    ctx_lens = [1, 900, 200, 130, 700, 64, 65]
+    out, exp = _attn_case(q_lens, ctx_lens, Hq, Hkv)
+    assert rel_err(out, exp) < 2e-2
+    assert torch.isfinite(out.float()).all()
+
+
+def test_paged_attention_spike():
+    # a single large score forces the online-softmax rescale path (rule 26)
+    out, exp = _attn_case([40], [300], 32, 8, seed=3)
+    assert rel_err(out, exp) < 2e-2
+
+
+def test_sample_allowed_greedy_and_distribution():
+    torch.manual_seed(0)
+    S, H, V = 6, 4096, 2000
+    hidden = torch.randn(S, H, device=DEV).bfloat16()
+    W = (torch.randn(V, H, device=DEV) * 0.02).bfloat16()
+    allowed = [torch.randperm(V)[:n].tolist() for n in (1, 2, 5, 17, 64, 300)]
+    ptr = np.cumsum([0] + [len(a) for a in allowed]).astype(np.int32)
+    ids = torch.tensor(sum(allowed, []), dtype=torch.int32, device=DEV)
+    ptr_t = torch.from_numpy(ptr).to(DEV)
+    ctr = torch.arange(S, dtype=torch.int64, device=DEV)
+    tok = ops.sample_allowed(hidden, W, ptr_t, ids, ctr, 0.0, 1234)
+    for s, (aid, logits) in enumerate(ref.sample_allowed_logits(hidden.cpu(), W.cpu(), ptr, ids.cpu())):
+        assert int(tok[s]) == int(aid[int(torch.argmax(logits))])
+    # temperature sampling follows softmax(logits / T) over the allowed set
+    s = 3
+    T = 0.5
+    aid, logits = ref.sample_allowed_logits(hidden.cpu(), W.cpu(), ptr, ids.cpu())[s]
+    p = torch.softmax(logits / T, dim=0)
+    counts = torch.zeros(len(aid))
+    pos = {int(t): i for i, t in enumerate(aid)}
+    h1 = hidden[s:s + 1].contiguous()
+    p1 = torch.tensor([0, len(aid)], dtype=torch.int32, device=DEV)
+    ids1 = aid.int().to(DEV)
+    N = 4000
+    for i in range(N // 200):
+        hh = h1.expand(200, H).contiguous()
+        pp = torch.arange(0, 201, dtype=torch.int32, device=DEV) * 0
+        ptr_b = torch.tensor(np.arange(201) * len(aid), dtype=torch.int32, device=DEV)
+        ids_b = ids1.repeat(200)
+        c = torch.arange(i * 200, (i + 1) * 200, dtype=torch.int64, device=DEV)
+        t = ops.sample_allowed(hh, W, ptr_b, ids_b, c, T, 99)
+        for x in t.cpu().tolist():
+            counts[pos[x]] += 1
+    freq = counts / counts.sum()
+    assert (freq - p).abs().max().item() < 0.05
