@@ -86,6 +86,35 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
   launch_gemm_tn(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, stream());
 }
 
+void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
+  TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
+  const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && Y.numel() == (int64_t)M * N, "gemm_f32out shapes");
+  TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_f32out: unsupported shape");
+  launch_gemm_tn_f32out(X.data_ptr(), W.data_ptr(), Y.data_ptr<float>(), M, N, K, stream());
+}
+
+void l2norm_rows(at::Tensor& x) {
+  CHECK_BF16_TENSOR(x);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0, "l2norm_rows: [N, D], D % 8 == 0");
+  launch_l2norm_rows(x.data_ptr(), x.size(0), x.size(1), stream());
+}
+
+void segment_topk(const at::Tensor& vals, const c10::optional<at::Tensor>& idx, int64_t seg_len,
+                  int64_t k, at::Tensor& out_v, at::Tensor& out_i) {
+  CHECK_DEV(vals); CHECK_CONTIG(vals);
+  TORCH_CHECK(vals.scalar_type() == at::kFloat && vals.dim() == 2, "vals [B, L] f32");
+  const int B = vals.size(0), L = vals.size(1);
+  const int nseg = (L + seg_len - 1) / seg_len;
+  TORCH_CHECK(out_v.numel() == (int64_t)B * nseg * k && out_i.numel() == out_v.numel(), "topk out shapes");
+  const int* ip = nullptr;
+  if (idx.has_value()) { CHECK_I32_TENSOR((*idx)); TORCH_CHECK(idx->numel() == vals.numel(), "idx shape"); ip = idx->data_ptr<int>(); }
+  const int rc = launch_segment_topk(vals.data_ptr<float>(), ip, B, L, seg_len, k,
+                                     out_v.data_ptr<float>(), out_i.data_ptr<int>(), stream());
+  TORCH_CHECK(rc == 0, "segment_topk: seg_len <= 4096 and 0 < k <= seg_len");
+}
+
 void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                      at::Tensor& out, const at::Tensor& q_start, const at::Tensor& q_len,
                      const at::Tensor& ctx_len, const at::Tensor& block_table,
@@ -151,6 +180,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);
   m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none());
+  m.def("gemm_f32out", &gemm_f32out);
+  m.def("l2norm_rows", &l2norm_rows);
+  m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),
+        py::arg("k"), py::arg("out_v"), py::arg("out_i"));
   m.def("paged_attention", &paged_attention);
   m.def("attn_tokens_per_item", &attn_tokens_per_item);
   m.def("sample_allowed", &sample_allowed, py::arg("hidden"), py::arg("W"), py::arg("allow_ptr"),

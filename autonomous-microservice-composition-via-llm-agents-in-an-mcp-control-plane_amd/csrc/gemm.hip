@@ -22,10 +22,10 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_ELEMS = 128 * BK;          // one operand tile, bf16 elements (16 KiB)
 
-template <bool RESID>
+template <bool RESID, typename OutT = bf16>
 __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X,
                                                       const bf16* __restrict__ W,
-                                                      bf16* __restrict__ Y,
+                                                      OutT* __restrict__ Y,
                                                       const bf16* __restrict__ R, int M, int N,
                                                       int K) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE_ELEMS];   // [buf][A|B][128][64]
@@ -118,10 +118,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
       }
-      bf16x4 o;
+      if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<f32x4*>(Y + (size_t)m * N + n) = v;
+      } else {
+        bf16x4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-      *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+        *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+      }
     }
   }
 }
@@ -145,4 +149,12 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
   else
     gemm_tn_128<false><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M,
                                             N, K);
+}
+
+// fp32-output variant (retrieval scores: bf16 would tie near-equal cosines)
+void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N, int K,
+                           hipStream_t s) {
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  gemm_tn_128<false, float><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, Y,
+                                                          nullptr, M, N, K);
 }

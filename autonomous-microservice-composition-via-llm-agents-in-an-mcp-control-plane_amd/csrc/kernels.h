@@ -21,6 +21,13 @@ void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
 int gemm_tn_check(int M, int N, int K);
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s);
+void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N, int K,
+                           hipStream_t s);
+
+// topk.hip
+void launch_l2norm_rows(void* x, int N, int D, hipStream_t s);
+int launch_segment_topk(const float* vals, const int* idx_in, int B, int L, int seg_len, int k,
+                        float* out_v, int* out_i, hipStream_t s);
 
 // attention.hip
 int attn_tokens_per_item(int nw, int group);

@@ -1,0 +1,291 @@
+"""Continuous-batching, grammar-driven LLM engine (one per GPU / TP group).
+
+Replaces the remote LLM call of the reference planner (control_plane.py:69-73).
+One ``step()`` = one ragged forward over every runnable sequence:
+
+* a sequence contributes all its *pending* tokens: prompt chunks, the token
+  sampled last step, and grammar-forced spans (jump-forward: forced JSON text
+  is fed in the same forward instead of one decode step per token);
+* KV goes into the paged cache; the shared registry-prompt prefix is computed
+  once per batch and its full blocks are shared by every request
+  (prefix caching by reference-counted blocks);
+* sequences waiting on a grammar choice get their last hidden state
+  normalised and sampled by the fused allowed-set LM-head kernel (K9) at
+  temperature 0.2 (control_plane.py:72);
+* one host<->device round trip per step: packed int32 metadata in, sampled
+  token ids out.
+
+The scheduler is single-threaded and owns all GPU state; the
+async frontend (planner.local) talks to it through queues.
+"""
+from __future__ import annotations
+
+import dataclasses
+import itertools
+import time
+from typing import Callable, Dict, List, Optional, Sequence as Seq
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..utils.metrics import METRICS
+from .batch import BLOCK_SIZE, StepInputs, pack
+from .kv_cache import KVCache
+
+_uid = itertools.count(1)
+
+
+@dataclasses.dataclass
+class PrefixEntry:
+    tokens: tuple
+    blocks: List[int]
+    length: int                # tokens covered by the shared (full) blocks
+    computed: bool = False
+    refs: int = 0
+
+
+class Sequence:
+    def __init__(self, decoder, prompt_tokens: List[int], prefix: Optional[PrefixEntry] = None,
+                 on_done: Optional[Callable] = None):
+        self.uid = next(_uid)
+        self.decoder = decoder
+        self.prefix = prefix
+        self.blocks: List[int] = list(prefix.blocks) if prefix else []
+        self.num_cached = prefix.length if prefix else 0     # tokens with KV in cache
+        self.pending: List[int] = list(prompt_tokens)
+        self.n_samples = 0
+        self.done = False
+        self.result = None
+        self.error: Optional[str] = None
+        self.on_done = on_done
+        self.t_submit = time.perf_counter()
+        self.t_first = None
+        self.t_done = None
+        self.is_prefix_job = decoder is None
+        if decoder is not None:
+            self.pending += decoder.advance()
+
+    @property
+    def wants_sample(self) -> bool:
+        return self.decoder is not None and not self.decoder.done
+
+
+class LLMEngine:
+    def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
+                 max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
+                 seed: int = 0):
+        self.model = model
+        cfg = model.cfg
+        self.device = model.device
+        if num_blocks is not None:
+            self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
+        else:
+            self.kv = KVCache.sized_for(cfg.layers, model.hkv, cfg.head_dim, self.device,
+                                        budget_bytes=kv_budget_bytes)
+        self.alloc = self.kv.allocator
+        self.max_batch = max_batch
+        self.max_step_tokens = max_step_tokens
+        self.temperature = temperature
+        self.seed = seed
+        self.running: List[Sequence] = []
+        self.waiting: List[Sequence] = []
+        self.prefixes: Dict[tuple, PrefixEntry] = {}
+        self.steps = 0
+        self.stats = {"tokens": 0, "samples": 0, "forward_s": 0.0, "steps": 0}
+
+    # ------------------------------------------------------------- prefixes
+    def get_prefix(self, tokens: Seq[int]) -> Optional[PrefixEntry]:
+        """Shared prefix entry covering the full 64-token blocks of ``tokens``.
+
+        The first request creates a prefix job that computes those blocks; later
+        requests (same step or later) only reference them."""
+        tokens = tuple(tokens)
+        n_full = (len(tokens) // BLOCK_SIZE) * BLOCK_SIZE
+        if n_full == 0:
+            return None
+        key = tokens[:n_full]
+        e = self.prefixes.get(key)
+        if e is None:
+            blocks = self.alloc.alloc(n_full // BLOCK_SIZE)
+            e = PrefixEntry(tokens=key, blocks=blocks, length=n_full)
+            self.prefixes[key] = e
+            job = Sequence(None, list(key))
+            job.blocks = list(blocks)
+            job.num_cached = 0
+            job.prefix_entry = e
+            self.alloc.incref(blocks)          # the job's own reference
+            self.waiting.insert(0, job)
+        return e
+
+    def drop_prefixes(self):
+        """Release prefix entries (their blocks stay alive while requests use them)."""
+        for e in self.prefixes.values():
+            self.alloc.free(e.blocks)
+        self.prefixes.clear()
+
+    # ------------------------------------------------------------ requests
+    def submit(self, decoder, prompt_tokens: List[int], prefix_tokens: Optional[List[int]] = None,
+               on_done: Optional[Callable] = None) -> Sequence:
+        """Queue one grammar-constrained generation.  ``prefix_tokens`` is the
+        shareable leading part of the prompt (registry section)."""
+        prefix = None
+        full_prompt = list(prefix_tokens or []) + list(prompt_tokens)
+        if prefix_tokens:
+            prefix = self.get_prefix(prefix_tokens)
+        if prefix is not None:
+            self.alloc.incref(prefix.blocks)
+            seq = Sequence(decoder, full_prompt[prefix.length:], prefix, on_done)
+        else:
+            seq = Sequence(decoder, full_prompt, None, on_done)
+        self.waiting.append(seq)
+        return seq
+
+    def has_work(self) -> bool:
+        return bool(self.running or self.waiting)
+
+    # ---------------------------------------------------------------- step
+    def _admit(self):
+        while self.waiting and len(self.running) < self.max_batch:
+            self.running.append(self.waiting.pop(0))
+
+    def _ensure_blocks(self, seq: Sequence, total_tokens: int):
+        need = (total_tokens + BLOCK_SIZE - 1) // BLOCK_SIZE - len(seq.blocks)
+        if need > 0:
+            seq.blocks += self.alloc.alloc(need)
+
+    def _finish(self, seq: Sequence):
+        seq.done = True
+        seq.t_done = time.perf_counter()
+        self.alloc.free(seq.blocks)
+        seq.blocks = []
+        if seq.is_prefix_job:
+            seq.prefix_entry.computed = True
+        else:
+            try:
+                seq.result = seq.decoder.result()
+            except Exception as e:  # pragma: no cover - grammar guarantees JSON
+                seq.error = repr(e)
+            METRICS.plan_done(seq.t_done - seq.t_submit)
+        if seq.on_done is not None:
+            seq.on_done(seq)
+
+    def step(self) -> int:
+        """One forward over the runnable batch.  Returns tokens processed."""
+        self._admit()
+        if not self.running:
+            return 0
+        budget = self.max_step_tokens
+        ids, pos, slots = [], [], []
+        q_start, q_len, ctx_len, tables = [], [], [], []
+        logit_rows, sample_seqs = [], []
+        batch_seqs = []
+        T = 0
+        for seq in self.running:
+            # a request may not run before its shared prefix has been scheduled
+            if seq.prefix is not None and not seq.prefix.computed and not self._prefix_scheduled(seq.prefix, batch_seqs):
+                continue
+            n = len(seq.pending)
+            if n == 0:
+                continue
+            take = min(n, budget - T)
+            if take <= 0:
+                break
+            start = seq.num_cached
+            self._ensure_blocks(seq, start + take)
+            toks = seq.pending[:take]
+            q_start.append(T)
+            q_len.append(take)
+            ctx_len.append(start + take)
+            tables.append(seq.blocks)
+            ids += toks
+            p = np.arange(start, start + take, dtype=np.int32)
+            pos.append(p)
+            blk = np.asarray(seq.blocks, dtype=np.int32)
+            slots.append(blk[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE)
+            T += take
+            batch_seqs.append((seq, take))
+            if take == n and seq.wants_sample:
+                logit_rows.append(T - 1)
+                sample_seqs.append(seq)
+        if T == 0:
+            return 0
+        S = len(batch_seqs)
+        maxb = max(len(t) for t in tables)
+        bt = np.zeros((S, maxb), np.int32)
+        for i, t in enumerate(tables):
+            bt[i, :len(t)] = t
+        step = StepInputs(token_ids=np.asarray(ids, np.int32), positions=np.concatenate(pos),
+                          slots=np.concatenate(slots).astype(np.int32),
+                          q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
+                          ctx_len=np.asarray(ctx_len, np.int32), block_table=bt,
+                          logit_rows=np.asarray(logit_rows, np.int32))
+        dev = pack(step, self.model.cfg.group, self.device)
+        t0 = time.perf_counter()
+        hidden = self.model.forward(dev, self.kv)
+        new_tokens = self._sample(hidden, sample_seqs)
+        self.stats["forward_s"] += time.perf_counter() - t0
+        self.stats["tokens"] += T
+        self.stats["steps"] += 1
+        self.steps += 1
+        # ---- bookkeeping
+        for seq, take in batch_seqs:
+            seq.num_cached += take
+            del seq.pending[:take]
+            if seq.is_prefix_job and not seq.pending:
+                self._finish(seq)
+        for seq, tok in zip(sample_seqs, new_tokens):
+            if seq.t_first is None:
+                seq.t_first = time.perf_counter()
+            seq.n_samples += 1
+            seq.decoder.feed(int(tok))
+            seq.pending += seq.decoder.advance()
+        for seq, _ in batch_seqs:
+            if not seq.is_prefix_job and seq.decoder.done and not seq.done:
+                self._finish(seq)
+        self.running = [s for s in self.running if not s.done]
+        METRICS.set("batch_occupancy", len(self.running))
+        METRICS.set("kv_block_utilization", self.alloc.utilization())
+        return T
+
+    @staticmethod
+    def _prefix_scheduled(prefix: PrefixEntry, batch_seqs) -> bool:
+        # prefix KV written by an earlier job in the SAME forward is visible: rope_kv
+        # of layer l runs over every token before attention of layer l
+        for s, take in batch_seqs:
+            if s.is_prefix_job and s.prefix_entry is prefix and take == len(s.pending):
+                return True
+        return False
+
+    def _sample(self, hidden: torch.Tensor, seqs: List[Sequence]) -> List[int]:
+        if not seqs:
+            return []
+        allowed = [s.decoder.allowed() for s in seqs]
+        ptr = np.zeros(len(seqs) + 1, np.int32)
+        ptr[1:] = np.cumsum([len(a) for a in allowed])
+        flat = np.fromiter(itertools.chain.from_iterable(allowed), dtype=np.int32, count=int(ptr[-1]))
+        ctr = np.asarray([s.uid * 65536 + s.n_samples for s in seqs], np.int64)
+        dev = self.device
+        if dev.type == "cuda":
+            host = torch.from_numpy(np.concatenate([ptr, flat]))
+            d = host.pin_memory().to(dev, non_blocking=True)
+            ptr_t, ids_t = d[:ptr.size], d[ptr.size:]
+            ctr_t = torch.from_numpy(ctr).pin_memory().to(dev, non_blocking=True)
+        else:
+            ptr_t, ids_t, ctr_t = torch.from_numpy(ptr), torch.from_numpy(flat), torch.from_numpy(ctr)
+        tok = ops.sample_allowed(hidden, self.model.w.lm_head, ptr_t, ids_t, ctr_t, self.temperature,
+                                 self.seed + self.steps)
+        self.stats["samples"] += len(seqs)
+        return tok.cpu().tolist()
+
+    # -------------------------------------------------------------- driver
+    def run(self, max_steps: int = 1_000_000):
+        n = 0
+        while self.has_work() and n < max_steps:
+            if self.step() == 0 and not self.waiting:
+                # nothing runnable: sequences blocked on nothing -> bug guard
+                stuck = [s for s in self.running if not s.pending]
+                if stuck:
+                    raise RuntimeError("engine stalled with sequences that have no pending tokens")
+            n += 1
+        return n

@@ -1,0 +1,217 @@
+"""Llama-3 decoder (the on-node planner LLM).
+
+Replaces the reference's remote ``openai.ChatCompletion`` call
+(control_plane.py:69-73).  Shapes are Meta's public Llama-3 configs (8B / 70B);
+weights are random-init (no checkpoints are reachable here, BASELINE.json
+north star) or loaded from safetensors (``models.weights``).
+
+Forward of one ragged, paged step - every op is a gfx950 HIP
+kernel from ``ops`` on GPU:
+
+    x = embed(ids)                                   K8
+    per layer:  h = rmsnorm(x)                       K3
+                qkv = h Wqkv^T                       K1 (MFMA GEMM)
+                q, K/V cache <- rope(qkv)            K4 + K10
+                a = paged_attention(q, K, V)         K5/K6
+                x = x + a Wo^T      (residual fused in the GEMM epilogue)
+                [all-reduce over TP ranks]           C1 (RCCL / xGMI)
+                h = rmsnorm(x); g = silu(h Wg^T) * (h Wu^T)   K1 + K7
+                x = x + g Wd^T      (fused residual) [all-reduce]  C2
+    h_last = rmsnorm(x[rows that need a token])
+
+Tensor parallelism is Megatron 1-D: Wqkv / Wgate|up column-parallel (whole
+heads / FFN slices per rank), Wo / Wdown row-parallel followed by an
+all-reduce; embeddings and the LM head are replicated (the constrained sampler
+only touches a few LM-head rows, so every rank samples identically and no
+logit collective is needed).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import List, Optional
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+
+
+@dataclasses.dataclass(frozen=True)
+class LlamaConfig:
+    name: str
+    vocab_size: int = 128256
+    hidden: int = 4096
+    layers: int = 32
+    heads: int = 32
+    kv_heads: int = 8
+    head_dim: int = 128
+    ffn: int = 14336
+    rope_theta: float = 500000.0
+    eps: float = 1e-5
+    max_pos: int = 8192
+
+    @property
+    def group(self) -> int:
+        return self.heads // self.kv_heads
+
+    def params(self) -> int:
+        H, D = self.hidden, self.head_dim
+        per_layer = H * (self.heads + 2 * self.kv_heads) * D + self.heads * D * H + 3 * H * self.ffn + 2 * H
+        return self.layers * per_layer + 2 * self.vocab_size * H + H
+
+    def kv_bytes_per_token(self, tp: int = 1) -> int:
+        return self.layers * 2 * (self.kv_heads // tp) * self.head_dim * 2
+
+
+CONFIGS = {
+    "llama3-8b": LlamaConfig("llama3-8b"),
+    "llama3-70b": LlamaConfig("llama3-70b", hidden=8192, layers=80, heads=64, kv_heads=8, ffn=28672),
+    # reduced configs with the same kernels (tests / smoke): head_dim stays 128
+    "llama3-1b-ish": LlamaConfig("llama3-1b-ish", hidden=2048, layers=16, heads=16, kv_heads=4, ffn=8192),
+    "tiny": LlamaConfig("tiny", hidden=256, layers=2, heads=2, kv_heads=1, ffn=512),
+}
+
+
+def get_config(name: str) -> LlamaConfig:
+    if name not in CONFIGS:
+        raise KeyError(f"unknown model config {name!r}; have {sorted(CONFIGS)}")
+    return CONFIGS[name]
+
+
+@dataclasses.dataclass
+class LayerWeights:
+    attn_norm: torch.Tensor
+    wqkv: torch.Tensor        # [(Hq + 2 Hkv) * D / tp, H]
+    wo: torch.Tensor          # [H, Hq * D / tp]
+    mlp_norm: torch.Tensor
+    w_gate_up: torch.Tensor   # [2 F / tp, H]  (gate rows | up rows)
+    w_down: torch.Tensor      # [H, F / tp]
+
+
+@dataclasses.dataclass
+class LlamaWeights:
+    embed: torch.Tensor       # [V, H] (replicated)
+    layers: List[LayerWeights]
+    final_norm: torch.Tensor
+    lm_head: torch.Tensor     # [V, H] (replicated)
+
+
+def shard_rows(w: torch.Tensor, rank: int, tp: int) -> torch.Tensor:
+    n = w.shape[0] // tp
+    return w[rank * n:(rank + 1) * n].contiguous()
+
+
+def shard_cols(w: torch.Tensor, rank: int, tp: int) -> torch.Tensor:
+    n = w.shape[1] // tp
+    return w[:, rank * n:(rank + 1) * n].contiguous()
+
+
+def shard_layer(full: LayerWeights, cfg: LlamaConfig, rank: int, tp: int) -> LayerWeights:
+    """Megatron split of one full layer (used by tests and the safetensors loader)."""
+    D = cfg.head_dim
+    q, k, v = torch.split(full.wqkv, [cfg.heads * D, cfg.kv_heads * D, cfg.kv_heads * D])
+    wqkv = torch.cat([shard_rows(q, rank, tp), shard_rows(k, rank, tp), shard_rows(v, rank, tp)])
+    g, u = torch.split(full.w_gate_up, [cfg.ffn, cfg.ffn])
+    return LayerWeights(attn_norm=full.attn_norm, wqkv=wqkv.contiguous(),
+                        wo=shard_cols(full.wo, rank, tp), mlp_norm=full.mlp_norm,
+                        w_gate_up=torch.cat([shard_rows(g, rank, tp), shard_rows(u, rank, tp)]).contiguous(),
+                        w_down=shard_cols(full.w_down, rank, tp))
+
+
+def random_weights(cfg: LlamaConfig, device, dtype=torch.bfloat16, seed: int = 0, tp_rank: int = 0,
+                   tp: int = 1, std: float = 0.02) -> LlamaWeights:
+    """Random-init weights, generated shard-locally on the target device.
+
+    Each rank draws its own shard (70B at TP=8 never materialises the full
+    tensors).  Replicated tensors use a rank-independent seed."""
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    D, H = cfg.head_dim, cfg.hidden
+
+    def rnd(shape, s, scale=std):
+        g.manual_seed(s)
+        return (torch.randn(shape, generator=g, device=dev, dtype=torch.float32) * scale).to(dtype)
+
+    def norm_w():
+        return torch.ones(H, device=dev, dtype=dtype)
+
+    base = seed * 1_000_003
+    layers = []
+    hq, hk, f = cfg.heads // tp, cfg.kv_heads // tp, cfg.ffn // tp
+    out_std = std / math.sqrt(2 * cfg.layers)
+    for l in range(cfg.layers):
+        s = base + 1000 * (l + 1) + 97 * tp_rank
+        layers.append(LayerWeights(
+            attn_norm=norm_w(),
+            wqkv=rnd(((hq + 2 * hk) * D, H), s + 1),
+            wo=rnd((H, hq * D), s + 2, out_std),
+            mlp_norm=norm_w(),
+            w_gate_up=rnd((2 * f, H), s + 3),
+            w_down=rnd((H, f), s + 4, out_std)))
+    return LlamaWeights(embed=rnd((cfg.vocab_size, H), base + 11, 1.0),
+                        layers=layers, final_norm=norm_w(),
+                        lm_head=rnd((cfg.vocab_size, H), base + 13))
+
+
+class LlamaModel:
+    """Stateless forward over weights + an external paged KV cache."""
+
+    def __init__(self, cfg: LlamaConfig, weights: LlamaWeights, device, tp_rank: int = 0,
+                 tp: int = 1, tp_group=None):
+        self.cfg = cfg
+        self.w = weights
+        self.device = torch.device(device)
+        self.tp_rank, self.tp, self.tp_group = tp_rank, tp, tp_group
+        if cfg.heads % tp or cfg.kv_heads % tp or cfg.ffn % tp:
+            raise ValueError(f"tp={tp} does not divide heads/kv_heads/ffn of {cfg.name}")
+        self.hq, self.hkv = cfg.heads // tp, cfg.kv_heads // tp
+        self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self._allreduce = None
+        if tp > 1:
+            from ..parallel.comm import make_allreduce
+            self._allreduce = make_allreduce(tp_group, self.device)
+
+    @classmethod
+    def random(cls, name: str, device, seed: int = 0, tp_rank: int = 0, tp: int = 1, tp_group=None):
+        cfg = get_config(name)
+        return cls(cfg, random_weights(cfg, device, seed=seed, tp_rank=tp_rank, tp=tp), device,
+                   tp_rank, tp, tp_group)
+
+    # --------------------------------------------------------------- forward
+    def _residual_gemm(self, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """x + a w^T with the residual add fused in the GEMM epilogue; for TP the
+        row-parallel partial sums are all-reduced (rank 0 carries the residual)."""
+        if self.tp == 1:
+            return ops.gemm(a, w, R=x, out=x)
+        y = ops.gemm(a, w, R=x if self.tp_rank == 0 else None)
+        self._allreduce(y)
+        return y
+
+    def forward(self, step, kv) -> torch.Tensor:
+        """Runs one ragged step; returns final-normed hidden states of
+        ``step.logit_rows`` ([R, H], bf16)."""
+        cfg, D = self.cfg, self.cfg.head_dim
+        T = step.token_ids.numel()
+        x = ops.embedding(step.token_ids, self.w.embed)
+        L = cfg.layers
+        h = ops.rmsnorm(x, self.w.layers[0].attn_norm, cfg.eps)
+        q = torch.empty(T, self.hq, D, device=x.device, dtype=x.dtype)
+        for l in range(L):
+            lw = self.w.layers[l]
+            qkv = ops.gemm(h, lw.wqkv)
+            kc, vc = kv.layer(l)
+            ops.rope_kv(qkv, step.positions, step.slots, self.cos_sin, q, kc, vc, self.hq, self.hkv, D)
+            a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
+            x = self._residual_gemm(a.view(T, self.hq * D), lw.wo, x)
+            h = ops.rmsnorm(x, lw.mlp_norm, cfg.eps)
+            act = ops.silu_mul(ops.gemm(h, lw.w_gate_up))
+            x = self._residual_gemm(act, lw.w_down, x)
+            if l + 1 < L:
+                h = ops.rmsnorm(x, self.w.layers[l + 1].attn_norm, cfg.eps)
+        rows = step.logit_rows
+        if rows.numel() == 0:
+            return x.new_empty(0, cfg.hidden)
+        xl = x.index_select(0, rows.long())
+        return ops.rmsnorm(xl, self.w.final_norm, cfg.eps)

@@ -155,3 +155,38 @@ def add_inplace(y, x):
     else:
         y.add_(x)
     return y
+
+
+def l2norm_rows(x):
+    """In-place row L2 normalisation of a [N, D] bf16 matrix."""
+    if x.is_cuda:
+        lib().l2norm_rows(x)
+    else:
+        x.copy_(torch.nn.functional.normalize(x.float(), dim=-1).to(x.dtype))
+    return x
+
+
+def topk_cosine(queries, corpus, k: int, seg_len: int = 4096):
+    """Top-k cosine similarity of unit-norm ``queries`` [B, D] against unit-norm
+    ``corpus`` [N, D] (both bf16).  Returns (scores [B, k] f32, index [B, k] int32).
+
+    GPU: fp32-output MFMA GEMM for the scores, then hierarchical segmented
+    top-k selection (csrc/topk.hip) until one segment remains."""
+    B, N = queries.shape[0], corpus.shape[0]
+    k = min(k, N)
+    if not queries.is_cuda:
+        v, i = torch.topk(queries.float() @ corpus.float().t(), k=k, dim=-1)
+        return v, i.int()
+    L_ = lib()
+    scores = torch.empty(B, N, device=queries.device, dtype=torch.float32)
+    L_.gemm_f32out(queries, corpus, scores)
+    vals, idx, L = scores, None, N
+    while True:
+        sl = min(seg_len, max(L, k))
+        nseg = (L + sl - 1) // sl
+        ov = torch.empty(B, nseg * k, device=queries.device, dtype=torch.float32)
+        oi = torch.empty(B, nseg * k, device=queries.device, dtype=torch.int32)
+        L_.segment_topk(vals, idx, sl, k, ov, oi)
+        vals, idx, L = ov, oi, nseg * k
+        if nseg == 1:
+            return vals, idx

@@ -1,0 +1,166 @@
+"""On-node planner: intent -> grammar-constrained Llama-3 decode -> T2 DAG.
+
+This is the MI355X replacement of ``GraphPlanner.plan`` (control_plane.py:57-75):
+
+1. list the registry (sorted, control_plane.py:58 / SURVEY D12);
+2. if the registry is larger than ``retrieval_threshold``, keep the top-k
+   services by cosine similarity between the intent and the HBM-resident
+   schema embeddings (the never-called pgvector helper of
+   control_plane.py:51-55, now a HIP top-k kernel, ``retrieval``);
+3. build the prompt (shared registry prefix + per-intent suffix);
+4. decode under the DAG grammar on the local engine at temperature 0.2
+   (control_plane.py:72) - the output is valid T2 JSON by construction.
+
+Concurrency: a dedicated scheduler thread owns the engine (and the GPU); the
+asyncio side submits requests through a queue and awaits futures, so the
+FastAPI event loop never blocks (fixes SURVEY D9).  ``plan_many`` is the
+synchronous batch path used by the benchmark.
+"""
+from __future__ import annotations
+
+import asyncio
+import queue
+import threading
+import time
+from typing import Dict, List, Optional, Sequence
+
+from ..utils.metrics import METRICS
+from .base import Planner
+from .grammar import DagDecoder, GrammarSpec
+from .prompt import build_prompt_parts
+from .tokenizer import get_tokenizer
+
+
+class LocalPlanner(Planner):
+    def __init__(self, engine, registry, tokenizer=None, max_nodes: int = 6, retriever=None,
+                 retrieval_threshold: int = 48, topk: int = 32):
+        self.engine = engine
+        self.registry = registry
+        self.tok = tokenizer or get_tokenizer()
+        self.max_nodes = max_nodes
+        self.retriever = retriever
+        self.retrieval_threshold = retrieval_threshold
+        self.topk = topk
+        self._spec_cache: Dict[tuple, GrammarSpec] = {}
+        self._prefix_cache: Dict[tuple, List[int]] = {}
+        self._q: "queue.Queue" = queue.Queue()
+        self._thread: Optional[threading.Thread] = None
+        self._stop = threading.Event()
+        self._lock = threading.Lock()
+
+    # ----------------------------------------------------------- factory
+    @classmethod
+    def from_settings(cls, settings, registry):
+        import torch
+        from ..engine.engine import LLMEngine
+        from ..models.llama import LlamaModel
+        from ..retrieval.store import SchemaIndex
+        dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+        model = LlamaModel.random(settings.model, dev, seed=settings.seed)
+        kw = {} if dev != "cpu" else {"num_blocks": 512}
+        eng = LLMEngine(model, max_batch=settings.max_batch, max_step_tokens=settings.max_step_tokens,
+                        temperature=settings.temperature, seed=settings.seed, **kw)
+        retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)
+        return cls(eng, registry, max_nodes=settings.max_nodes, retriever=retr,
+                   retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
+
+    # ----------------------------------------------------------- prepare
+    def candidates(self, intent: str, services: Sequence[dict]) -> List[dict]:
+        if self.retriever is None or len(services) <= self.retrieval_threshold:
+            return list(services)
+        return self.retriever.search(intent, self.topk, services)
+
+    def prepare(self, intent: str, services: Optional[Sequence[dict]] = None):
+        services = self.registry.list_services() if services is None else services
+        cands = self.candidates(intent, services)
+        key = tuple(s["name"] for s in cands) + (getattr(self.registry, "version", 0),)
+        spec = self._spec_cache.get(key)
+        if spec is None:
+            spec = GrammarSpec(cands, self.tok, max_nodes=self.max_nodes)
+            if len(self._spec_cache) > 256:
+                self._spec_cache.clear()
+            self._spec_cache[key] = spec
+        prefix, suffix = build_prompt_parts(cands, intent)
+        ptoks = self._prefix_cache.get(key)
+        if ptoks is None:
+            ptoks = [self.tok.bos_id] + self.tok.encode(prefix)
+            self._prefix_cache[key] = ptoks
+        return DagDecoder(spec), ptoks, self.tok.encode(suffix)
+
+    # ------------------------------------------------------- batch (sync)
+    def plan_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> List[dict]:
+        """Plan a batch of intents to completion on the calling thread."""
+        with self._lock:
+            services = self.registry.list_services()
+            seqs = []
+            for it in intents:
+                dec, ptoks, stoks = self.prepare(it, services)
+                seqs.append(self.engine.submit(dec, stoks, prefix_tokens=ptoks))
+            if fresh_prefix:
+                self.engine.drop_prefixes()   # batch-local prefix: recomputed next batch
+            self.engine.run()
+        out = []
+        for s in seqs:
+            if s.error:
+                raise RuntimeError(s.error)
+            out.append(s.result)
+        return out
+
+    # ------------------------------------------------------ async service
+    def _ensure_thread(self):
+        if self._thread is None or not self._thread.is_alive():
+            self._thread = threading.Thread(target=self._loop, name="mcp-engine", daemon=True)
+            self._thread.start()
+
+    def _loop(self):
+        eng = self.engine
+        while not self._stop.is_set():
+            try:
+                block = not eng.has_work()
+                item = self._q.get(timeout=0.05) if block else self._q.get_nowait()
+            except queue.Empty:
+                item = None
+            while item is not None:
+                intent, loop, fut = item
+                try:
+                    dec, ptoks, stoks = self.prepare(intent)
+                    t0 = time.perf_counter()
+
+                    def done(seq, loop=loop, fut=fut, t0=t0):
+                        METRICS.observe("engine_latency_s", time.perf_counter() - t0)
+                        if seq.error:
+                            loop.call_soon_threadsafe(_set_exc, fut, RuntimeError(seq.error))
+                        else:
+                            loop.call_soon_threadsafe(_set_result, fut, seq.result)
+                    eng.submit(dec, stoks, prefix_tokens=ptoks, on_done=done)
+                except Exception as e:  # noqa: BLE001
+                    loop.call_soon_threadsafe(_set_exc, fut, e)
+                try:
+                    item = self._q.get_nowait()
+                except queue.Empty:
+                    item = None
+            if eng.has_work():
+                with self._lock:
+                    eng.step()
+
+    async def plan(self, intent: str) -> dict:
+        self._ensure_thread()
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._q.put((intent, loop, fut))
+        return await fut
+
+    async def aclose(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+
+
+def _set_result(fut, v):
+    if not fut.done():
+        fut.set_result(v)
+
+
+def _set_exc(fut, e):
+    if not fut.done():
+        fut.set_exception(e)

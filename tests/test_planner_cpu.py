@@ -1,0 +1,148 @@
+"""Planner tests on CPU: grammar, engine plumbing with the tiny
+Llama config through the fp32 reference ops, API wiring of the local planner."""
+import json
+import random
+
+import httpx
+import numpy as np
+import pytest
+import torch
+from fastapi.testclient import TestClient
+
+from mcp_amd.api.server import create_app
+from mcp_amd.config import Settings
+from mcp_amd.engine.batch import build_work
+from mcp_amd.engine.engine import LLMEngine
+from mcp_amd.engine.kv_cache import BlockAllocator
+from mcp_amd.models.llama import LlamaModel
+from mcp_amd.orchestrator import validate_dag
+from mcp_amd.planner.grammar import DagDecoder, GrammarSpec, build_trie
+from mcp_amd.planner.local import LocalPlanner
+from mcp_amd.planner.prompt import synthetic_intent
+from mcp_amd.planner.tokenizer import get_tokenizer
+from mcp_amd.registry import MemoryRegistry, make_service, synthetic_registry
+from mcp_amd.retrieval.store import SchemaIndex, hash_embed
+
+
+def random_walk(spec, rng):
+    dec = DagDecoder(spec)
+    toks = dec.advance()
+    n = 0
+    while not dec.done:
+        allowed = dec.allowed()
+        assert len(allowed) >= 2
+        dec.feed(rng.choice(allowed))
+        toks += dec.advance()
+        n += 1
+    return dec, toks, n
+
+
+@pytest.mark.parametrize("nsvc,max_nodes", [(1, 3), (3, 6), (10, 6), (50, 8)])
+def test_grammar_always_valid_t2(nsvc, max_nodes):
+    tok = get_tokenizer()
+    reg = synthetic_registry(nsvc, seed=nsvc)
+    spec = GrammarSpec(reg, tok, max_nodes=max_nodes)
+    rng = random.Random(0)
+    for _ in range(40):
+        dec, toks, n = random_walk(spec, rng)
+        dag = dec.result()
+        validate_dag(dag, [s["name"] for s in reg])
+        assert len(dag["nodes"]) <= max_nodes
+        # the token stream decodes to exactly the emitted JSON text
+        assert tok.decode(toks) == dec.text
+        by = {s["name"]: s for s in reg}
+        for node in dag["nodes"]:
+            assert node["endpoint"] == by[node["name"]]["endpoint"]
+            assert set(node["inputs"]) == set(by[node["name"]].input_keys())
+        for e in dag["edges"]:
+            if "fallback" in e:
+                assert e["fallback"] == by[e["to"]]["fallback"]
+
+
+def test_trie_prefix_free_check():
+    with pytest.raises(ValueError):
+        build_trie([[1, 2], [1, 2, 3]])
+    t = build_trie([[1, 2], [1, 3], [4]])
+    assert sorted(t.children) == [1, 4]
+
+
+def test_block_allocator_refcounts():
+    a = BlockAllocator(8)
+    b = a.alloc(3)
+    a.incref(b[:2])
+    a.free(b)
+    assert a.num_free == 6
+    a.free(b[:2])
+    assert a.num_free == 8
+    with pytest.raises(RuntimeError):
+        a.free(b[:1])
+
+
+def test_work_split():
+    w = build_work([1, 3, 40, 0, 17], group=4)
+    assert w[1] == ([0, 1], [0, 0])
+    assert w[4][0] == [2, 2, 2, 4, 4]
+    assert w[4][1] == [0, 16, 32, 0, 16]
+
+
+@pytest.fixture(scope="module")
+def tiny_engine():
+    torch.manual_seed(0)
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    return LLMEngine(model, num_blocks=256, max_batch=16, max_step_tokens=4096)
+
+
+def test_engine_plans_valid_dags(tiny_engine):
+    reg = MemoryRegistry(synthetic_registry(5, seed=2))
+    planner = LocalPlanner(tiny_engine, reg, max_nodes=4)
+    intents = [synthetic_intent(i) for i in range(3)]
+    dags = planner.plan_many(intents)
+    assert len(dags) == 3
+    for d in dags:
+        validate_dag(d, [s.name for s in reg.list_services()])
+    assert tiny_engine.alloc.num_free == tiny_engine.kv.num_blocks     # every block returned
+    # greedy decoding is deterministic across runs
+    tiny_engine.temperature = 0.0
+    a = planner.plan_many(intents[:2])
+    b = planner.plan_many(intents[:2])
+    tiny_engine.temperature = 0.2
+    assert a == b
+
+
+def test_prefix_sharing_matches_unshared(tiny_engine):
+    """A request decoded on shared prefix blocks equals the same request decoded alone."""
+    reg = MemoryRegistry(synthetic_registry(6, seed=3))
+    planner = LocalPlanner(tiny_engine, reg, max_nodes=3)
+    tiny_engine.temperature = 0.0
+    try:
+        together = planner.plan_many([synthetic_intent(1), synthetic_intent(2)])
+        alone = planner.plan_many([synthetic_intent(2)])
+    finally:
+        tiny_engine.temperature = 0.2
+    assert together[1] == alone[0]
+
+
+def test_local_planner_behind_api(tiny_engine):
+    reg = MemoryRegistry(synthetic_registry(4, seed=5))
+    planner = LocalPlanner(tiny_engine, reg, max_nodes=3)
+
+    def h(request):
+        return httpx.Response(200, json={"ok": True})
+    app = create_app(Settings(), registry=reg, planner=planner, transport=httpx.MockTransport(h))
+    with TestClient(app) as c:
+        r = c.post("/plan", json={"intent": "charge the order and email the receipt"})
+        assert r.status_code == 200
+        validate_dag(r.json()["graph"], [s.name for s in reg.list_services()])
+        r2 = c.post("/plan_and_execute", json={"intent": "score the order"})
+        assert r2.status_code == 200 and set(r2.json()) == {"results", "errors"}
+
+
+def test_retrieval_cpu_prunes_prompt():
+    reg = MemoryRegistry(synthetic_registry(300, seed=7))
+    idx = SchemaIndex(reg, dim=512, device="cpu")
+    svcs = reg.list_services()
+    got = idx.search("payment charge amount currency", 8, svcs)
+    assert len(got) == 8
+    assert any("payment" in s.name or "charge" in s.name for s in got)
+    e = hash_embed(["a b c", "a b c"], 64)
+    assert np.allclose(e[0], e[1]) and abs(np.linalg.norm(e[0]) - 1) < 1e-5
