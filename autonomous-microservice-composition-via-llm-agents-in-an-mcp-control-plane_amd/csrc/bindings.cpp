@@ -68,7 +68,8 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slo
                  k_cache.size(2), stream());
 }
 
-void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::optional<at::Tensor>& R) {
+void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::optional<at::Tensor>& R,
+          int64_t algo) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
   const int K = X.size(-1);
   const int M = X.numel() / K;
@@ -83,7 +84,7 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
     TORCH_CHECK(R->numel() == Y.numel(), "R shape");
     rp = R->data_ptr();
   }
-  launch_gemm_tn(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, stream());
+  launch_gemm_tn_algo(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, (int)algo, stream());
 }
 
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
@@ -164,6 +165,15 @@ void sample_dense(const at::Tensor& logits, const at::Tensor& ctr, double temper
                       (unsigned long long)seed, out_tok.data_ptr<int>(), stream());
 }
 
+void copy_blocks(at::Tensor& data, const at::Tensor& src, const at::Tensor& dst) {
+  CHECK_BF16_TENSOR(data); CHECK_I32_TENSOR(src); CHECK_I32_TENSOR(dst);
+  TORCH_CHECK(data.dim() == 6, "kv data [L, 2, nb, Hkv, BS, D]");
+  TORCH_CHECK(src.numel() == dst.numel(), "pairs");
+  const int64_t block_elems = data.size(3) * data.size(4) * data.size(5);
+  launch_copy_blocks(data.data_ptr(), src.data_ptr<int>(), dst.data_ptr<int>(), src.numel(),
+                     data.size(0) * 2, data.size(2), block_elems, stream());
+}
+
 void add_inplace(at::Tensor& y, const at::Tensor& x) {
   CHECK_BF16_TENSOR(y); CHECK_BF16_TENSOR(x);
   TORCH_CHECK(y.numel() == x.numel() && y.numel() % 8 == 0, "add_inplace shapes");
@@ -179,7 +189,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("silu_mul", &silu_mul);
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);
-  m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none());
+  m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none(),
+        py::arg("algo") = -1);
+  m.def("gemm_select", &gemm_select);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),
@@ -191,4 +203,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_tok"), py::arg("out_logit") = py::none());
   m.def("sample_dense", &sample_dense);
   m.def("add_inplace", &add_inplace);
+  m.def("copy_blocks", &copy_blocks);
 }

@@ -219,3 +219,25 @@ void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s) {
   if (grid > 4096) grid = 4096;
   add_kernel<<<grid, 256, 0, s>>>((bf16*)y, (const bf16*)x, nvec);
 }
+
+// ------------------------------------------------------- KV block copy (CoW)
+// data: [L, 2, num_blocks, block_elems]; copies block src[i] -> dst[i] for every
+// layer and K/V (prefix-cache tail blocks).  16 B per lane.
+__global__ __launch_bounds__(256) void copy_blocks_kernel(bf16* __restrict__ data,
+                                                          const int* __restrict__ src,
+                                                          const int* __restrict__ dst, int npairs,
+                                                          int nb, int block_vecs) {
+  const int pair = blockIdx.x % npairs;
+  const int lk = blockIdx.x / npairs;           // layer * 2 + kv
+  bf16x8* base = reinterpret_cast<bf16x8*>(data) + (size_t)lk * nb * block_vecs;
+  const bf16x8* s = base + (size_t)src[pair] * block_vecs;
+  bf16x8* d = base + (size_t)dst[pair] * block_vecs;
+  for (int i = threadIdx.x; i < block_vecs; i += 256) d[i] = s[i];
+}
+
+void launch_copy_blocks(void* data, const int* src, const int* dst, int npairs, int layers2,
+                        int nb, int block_elems, hipStream_t s) {
+  if (npairs <= 0) return;
+  copy_blocks_kernel<<<npairs * layers2, 256, 0, s>>>((bf16*)data, src, dst, npairs, nb,
+                                                      block_elems / 8);
+}

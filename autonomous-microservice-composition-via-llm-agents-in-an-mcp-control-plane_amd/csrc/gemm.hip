@@ -139,8 +139,23 @@ int gemm_tn_check(int M, int N, int K) {
   return 0;
 }
 
-void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                    hipStream_t s) {
+// Tile selection by a wave-quantisation time model calibrated on MI355X
+// (tools/bench_gemm.py): the 256x256 kernel sustains ~1.22 PF/s with one
+// workgroup per CU (256 concurrent tiles), the 128x128 kernel ~1.04 PF/s with
+// two per CU (512 concurrent tiles).  Predicted time = full waves of tiles x
+// per-wave time; pick the smaller.
+int gemm_select(int M, int N, int K) {
+  if (M < 256 || N < 256 || K < 128) return 0;
+  const double t256 = (double)(((M + 255) / 256) * ((N + 255) / 256));
+  const double t128 = (double)(((M + 127) / 128) * ((N + 127) / 128));
+  const double w256 = ceil(t256 / 256.0), w128 = ceil(t128 / 512.0);
+  const double cost256 = w256 * 256.0 * 4.0 / 1.22;     // in 128^2-tile units / PF
+  const double cost128 = w128 * 512.0 / 1.04;
+  return cost256 < cost128 ? 1 : 0;
+}
+
+static void launch_gemm_tn_128(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                               int K, hipStream_t s) {
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   const dim3 grid(nm * nn);
   if (R)
@@ -157,4 +172,19 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   gemm_tn_128<false, float><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, Y,
                                                           nullptr, M, N, K);
+}
+
+void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                    hipStream_t s) {
+  if (gemm_select(M, N, K) == 1)
+    launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
+  else
+    launch_gemm_tn_128(X, W, Y, R, M, N, K, s);
+}
+
+void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                         int algo, hipStream_t s) {
+  if (algo < 0) launch_gemm_tn(X, W, Y, R, M, N, K, s);
+  else if (algo == 1) launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
+  else launch_gemm_tn_128(X, W, Y, R, M, N, K, s);
 }

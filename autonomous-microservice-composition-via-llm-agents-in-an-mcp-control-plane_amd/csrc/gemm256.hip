@@ -1,0 +1,193 @@
+// K1 (large-M path): 256x256-tile bf16 TN GEMM with a 4-phase-per-K-tile
+// pipeline whose LDS-DMA prefetch stays in flight across barriers.
+//   Y[M,N] = X[M,K] . W[N,K]^T (+ R)        fp32 accumulate, bf16 out
+//
+// Why (cdna_hip_programming.md §5 "The step-3 structure's ~900 TF ceiling"):
+// a 128^2 tile with one vmcnt(0)+__syncthreads per K-step stalls on every
+// prefetch.  Here one workgroup (8 waves, 2(M) x 4(N), 128x64 outputs per wave)
+// owns a 256x256 tile; each 64-deep K-tile is split into four 16 KiB pieces
+// {A.k0, B.k0, A.k1, B.k1} (k0/k1 = the two 32-deep halves) held in an 8-slot
+// LDS ring (two K-tiles, 128 KiB, one __shared__ array).  Phase p of K-tile t:
+//
+//   ds_read fragments (A: 4 x b128, B: 4 x b128 on even phases)
+//   issue piece p of K-tile t+1 (2 x global_load_lds_dwordx4 per thread)
+//   16 x v_mfma_f32_16x16x32_bf16 (m-half p&1, k-half p>>1), s_setprio 1
+//   [p = 1, 3: s_waitcnt vmcnt(4) -> the pieces the next phase reads landed]
+//   s_barrier
+//
+// so every load has >= 2 phases of MFMA work to land, and vmcnt never drains
+// to 0 inside the main loop (T3+T4).  The waits are hand-counted: each thread
+// issues exactly 2 LDS-DMA ops per phase and no other VMEM op in the loop.
+// WAR safety: piece p of tile t+1 overwrites the slot of piece p of tile t-1,
+// whose last read precedes the barrier that ends tile t-1.
+// LDS rows are 64 B (32 bf16); swizzle chunk ^= ((row>>2)&1)<<1 on the glds
+// SOURCE and the ds_read address (conflict-free, tools/lds_banks.py).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, KH = 32;
+constexpr int PIECE = 256 * KH;                 // bf16 elements per piece (16 KiB)
+
+DEV int swz(int row, int chunk) { return chunk ^ (((row >> 2) & 1) << 1); }
+
+DEV void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool RESID>
+__global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X,
+                                                      const bf16* __restrict__ W,
+                                                      bf16* __restrict__ Y,
+                                                      const bf16* __restrict__ R, int M, int N,
+                                                      int K) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[8 * PIECE];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const int nwg = nm * nn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * nn;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP;
+  const int gsz = min(nm - first_m, GROUP);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging: wave w writes 1 KiB instructions 2w, 2w+1 of every piece
+  //      (rows (2w+j)*16 + lane/4, 16-B chunk lane%4 of the 64-B row)
+  const bf16* srcA[2];
+  const bf16* srcB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (2 * wave + j) * 16 + (lane >> 2);
+    const int ch = swz(row, lane & 3);
+    srcA[j] = X + (size_t)min(m0 + row, M - 1) * K + ch * 8;
+    srcB[j] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
+  }
+  auto stage = [&](int t, int i) {          // piece i of K-tile t
+    const int koff = t * BK + (i >> 1) * KH;
+    bf16* slot = smem + ((t & 1) * 4 + i) * PIECE;
+    const bf16* const* src = (i & 1) ? srcB : srcA;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(src[j] + koff, slot + (2 * wave + j) * 512);
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[2][4][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[a][b][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment offsets inside a piece (elements)
+  int offA[2][4], offB[4];
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int row = wm * 128 + mh * 64 + mt * 16 + fr;
+      offA[mh][mt] = row * KH + swz(row, fq) * 8;
+    }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int row = wn * 64 + nt * 16 + fr;
+    offB[nt] = row * KH + swz(row, fq) * 8;
+  }
+
+  const int nk = K / BK;
+  // prologue: K-tile 0 fully resident
+#pragma unroll
+  for (int i = 0; i < 4; ++i) stage(0, i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();
+
+  bf16x8 bfr[4];
+  auto phase = [&](int t, int p, bool prefetch, bool last) {
+    const int kh = p >> 1, mh = p & 1;
+    const bf16* sA = smem + ((t & 1) * 4 + 2 * kh) * PIECE;
+    const bf16* sB = sA + PIECE;
+    bf16x8 af[4];
+    if (mh == 0) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) bfr[nt] = *reinterpret_cast<const bf16x8*>(sB + offB[nt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = *reinterpret_cast<const bf16x8*>(sA + offA[mh][mt]);
+    if (prefetch) stage(t + 1, p);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mh][mt][nt] = mfma16x16x32(bfr[nt], af[mt], acc[mh][mt][nt]);
+    __builtin_amdgcn_s_setprio(0);
+    if (p == 1) {
+      if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (p == 3 && !last) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    barrier();
+  };
+
+  for (int t = 0; t + 1 < nk; ++t) {
+    phase(t, 0, true, false);
+    phase(t, 1, true, false);
+    phase(t, 2, true, false);
+    phase(t, 3, true, false);
+  }
+  {
+    const int t = nk - 1;
+    phase(t, 0, false, true);
+    phase(t, 1, false, true);
+    phase(t, 2, false, true);
+    phase(t, 3, false, true);
+  }
+
+  // ---- epilogue: lane holds Y[m][n .. n+3]
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = m0 + wm * 128 + mh * 64 + mt * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n = n0 + wn * 64 + nt * 16 + fq * 4;
+        if (n >= N) continue;
+        f32x4 v = acc[mh][mt][nt];
+        if (RESID) {
+          const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+        *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+      }
+    }
+}
+
+}  // namespace
+
+void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        hipStream_t s) {
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const dim3 grid(nm * nn);
+  if (R)
+    gemm_tn_256<true><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                           (const bf16*)R, M, N, K);
+  else
+    gemm_tn_256<false><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M,
+                                            N, K);
+}

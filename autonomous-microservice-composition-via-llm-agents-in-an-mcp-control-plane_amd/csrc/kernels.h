@@ -16,11 +16,19 @@ void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const voi
                     void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
                     int BS, hipStream_t s);
 void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
+void launch_copy_blocks(void* data, const int* src, const int* dst, int npairs, int layers2,
+                        int nb, int block_elems, hipStream_t s);
 
 // gemm.hip
 int gemm_tn_check(int M, int N, int K);
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s);
+void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        hipStream_t s);
+// algo: -1 auto, 0 = 128x128 two-barrier kernel, 1 = 256x256 multi-phase kernel
+int gemm_select(int M, int N, int K);
+void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                         int algo, hipStream_t s);
 void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N, int K,
                            hipStream_t s);
 

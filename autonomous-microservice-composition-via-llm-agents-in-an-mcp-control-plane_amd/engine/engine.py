@@ -7,8 +7,9 @@ One ``step()`` = one ragged forward over every runnable sequence:
   sampled last step, and grammar-forced spans (jump-forward: forced JSON text
   is fed in the same forward instead of one decode step per token);
 * KV goes into the paged cache; the shared registry-prompt prefix is computed
-  once per batch and its full blocks are shared by every request
-  (prefix caching by reference-counted blocks);
+  once (per batch in the benchmark) by a prefix job; every request then shares
+  its full blocks (reference counted) and gets a device-side copy of the
+  partial tail block (copy-on-write) instead of recomputing those tokens;
 * sequences waiting on a grammar choice get their last hidden state
   normalised and sampled by the fused allowed-set LM-head kernel (K9) at
   temperature 0.2 (control_plane.py:72);
@@ -39,10 +40,9 @@ _uid = itertools.count(1)
 @dataclasses.dataclass
 class PrefixEntry:
     tokens: tuple
-    blocks: List[int]
-    length: int                # tokens covered by the shared (full) blocks
+    blocks: List[int]          # ceil(length / 64) blocks; the last may be partial
+    length: int                # prefix tokens
     computed: bool = False
-    refs: int = 0
 
 
 class Sequence:
@@ -51,8 +51,9 @@ class Sequence:
         self.uid = next(_uid)
         self.decoder = decoder
         self.prefix = prefix
-        self.blocks: List[int] = list(prefix.blocks) if prefix else []
-        self.num_cached = prefix.length if prefix else 0     # tokens with KV in cache
+        self.materialized = prefix is None
+        self.blocks: List[int] = []
+        self.num_cached = 0                    # tokens whose KV is in this sequence's blocks
         self.pending: List[int] = list(prompt_tokens)
         self.n_samples = 0
         self.done = False
@@ -96,23 +97,18 @@ class LLMEngine:
 
     # ------------------------------------------------------------- prefixes
     def get_prefix(self, tokens: Seq[int]) -> Optional[PrefixEntry]:
-        """Shared prefix entry covering the full 64-token blocks of ``tokens``.
-
-        The first request creates a prefix job that computes those blocks; later
-        requests (same step or later) only reference them."""
+        """Shared prefix entry for ``tokens``; the first request creates a
+        prefix job that computes the prefix KV once."""
         tokens = tuple(tokens)
-        n_full = (len(tokens) // BLOCK_SIZE) * BLOCK_SIZE
-        if n_full == 0:
+        if len(tokens) < BLOCK_SIZE:
             return None
-        key = tokens[:n_full]
-        e = self.prefixes.get(key)
+        e = self.prefixes.get(tokens)
         if e is None:
-            blocks = self.alloc.alloc(n_full // BLOCK_SIZE)
-            e = PrefixEntry(tokens=key, blocks=blocks, length=n_full)
-            self.prefixes[key] = e
-            job = Sequence(None, list(key))
+            blocks = self.alloc.alloc((len(tokens) + BLOCK_SIZE - 1) // BLOCK_SIZE)
+            e = PrefixEntry(tokens=tokens, blocks=blocks, length=len(tokens))
+            self.prefixes[tokens] = e
+            job = Sequence(None, list(tokens))
             job.blocks = list(blocks)
-            job.num_cached = 0
             job.prefix_entry = e
             self.alloc.incref(blocks)          # the job's own reference
             self.waiting.insert(0, job)
@@ -124,20 +120,31 @@ class LLMEngine:
             self.alloc.free(e.blocks)
         self.prefixes.clear()
 
+    def _materialize(self, seq: Sequence, copies: list):
+        """Attach a request to its computed prefix: share the full blocks, copy
+        the partial tail block (device copy queued before the next forward)."""
+        e = seq.prefix
+        n_full, tail = divmod(e.length, BLOCK_SIZE)
+        seq.blocks = list(e.blocks[:n_full])
+        if tail:
+            nb = self.alloc.alloc(1)[0]
+            copies.append((e.blocks[-1], nb))
+            seq.blocks.append(nb)
+            self.alloc.free([e.blocks[-1]])    # the reference taken at submit
+        seq.num_cached = e.length
+        seq.materialized = True
+
     # ------------------------------------------------------------ requests
     def submit(self, decoder, prompt_tokens: List[int], prefix_tokens: Optional[List[int]] = None,
                on_done: Optional[Callable] = None) -> Sequence:
         """Queue one grammar-constrained generation.  ``prefix_tokens`` is the
         shareable leading part of the prompt (registry section)."""
-        prefix = None
-        full_prompt = list(prefix_tokens or []) + list(prompt_tokens)
-        if prefix_tokens:
-            prefix = self.get_prefix(prefix_tokens)
+        prefix = self.get_prefix(prefix_tokens) if prefix_tokens else None
         if prefix is not None:
             self.alloc.incref(prefix.blocks)
-            seq = Sequence(decoder, full_prompt[prefix.length:], prefix, on_done)
+            seq = Sequence(decoder, list(prompt_tokens), prefix, on_done)
         else:
-            seq = Sequence(decoder, full_prompt, None, on_done)
+            seq = Sequence(decoder, list(prefix_tokens or []) + list(prompt_tokens), None, on_done)
         self.waiting.append(seq)
         return seq
 
@@ -175,6 +182,15 @@ class LLMEngine:
         self._admit()
         if not self.running:
             return 0
+        copies = []
+        for seq in self.running:
+            if not seq.materialized and seq.prefix.computed:
+                self._materialize(seq, copies)
+        if copies:
+            pairs = torch.tensor(copies, dtype=torch.int32).t().contiguous()
+            if self.device.type == "cuda":
+                pairs = pairs.pin_memory().to(self.device, non_blocking=True)
+            ops.copy_blocks(self.kv.data, pairs[0], pairs[1])
         budget = self.max_step_tokens
         ids, pos, slots = [], [], []
         q_start, q_len, ctx_len, tables = [], [], [], []
@@ -182,8 +198,7 @@ class LLMEngine:
         batch_seqs = []
         T = 0
         for seq in self.running:
-            # a request may not run before its shared prefix has been scheduled
-            if seq.prefix is not None and not seq.prefix.computed and not self._prefix_scheduled(seq.prefix, batch_seqs):
+            if not seq.materialized:           # waiting for its prefix job
                 continue
             n = len(seq.pending)
             if n == 0:
@@ -247,15 +262,6 @@ class LLMEngine:
         METRICS.set("batch_occupancy", len(self.running))
         METRICS.set("kv_block_utilization", self.alloc.utilization())
         return T
-
-    @staticmethod
-    def _prefix_scheduled(prefix: PrefixEntry, batch_seqs) -> bool:
-        # prefix KV written by an earlier job in the SAME forward is visible: rope_kv
-        # of layer l runs over every token before attention of layer l
-        for s, take in batch_seqs:
-            if s.is_prefix_job and s.prefix_entry is prefix and take == len(s.pending):
-                return True
-        return False
 
     def _sample(self, hidden: torch.Tensor, seqs: List[Sequence]) -> List[int]:
         if not seqs:

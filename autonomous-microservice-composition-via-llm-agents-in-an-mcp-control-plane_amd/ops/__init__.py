@@ -94,11 +94,11 @@ def embedding(ids, table, out=None):
     return r if out is None else out.copy_(r)
 
 
-def gemm(X, W, R=None, out=None):
-    """Y = X @ W^T (+ R).  X [M, K], W [N, K]."""
+def gemm(X, W, R=None, out=None, algo: int = -1):
+    """Y = X @ W^T (+ R).  X [M, K], W [N, K].  algo: -1 auto, 0 = 128^2, 1 = 256^2."""
     if X.is_cuda:
         out = X.new_empty(*X.shape[:-1], W.shape[0]) if out is None else out
-        lib().gemm(X, W, out, R)
+        lib().gemm(X, W, out, R, algo)
         return out
     r = ref.gemm(X, W, R)
     return r if out is None else out.copy_(r)
@@ -178,9 +178,14 @@ def topk_cosine(queries, corpus, k: int, seg_len: int = 4096):
         v, i = torch.topk(queries.float() @ corpus.float().t(), k=k, dim=-1)
         return v, i.int()
     L_ = lib()
-    scores = torch.empty(B, N, device=queries.device, dtype=torch.float32)
+    N4 = (N + 3) // 4 * 4                 # the scoring GEMM writes 16-B column groups
+    if N4 != N:
+        corpus = torch.nn.functional.pad(corpus, (0, 0, 0, N4 - N))
+    scores = torch.empty(B, N4, device=queries.device, dtype=torch.float32)
     L_.gemm_f32out(queries, corpus, scores)
-    vals, idx, L = scores, None, N
+    if N4 != N:
+        scores[:, N:] = float("-inf")
+    vals, idx, L = scores, None, N4
     while True:
         sl = min(seg_len, max(L, k))
         nseg = (L + sl - 1) // sl
@@ -190,3 +195,12 @@ def topk_cosine(queries, corpus, k: int, seg_len: int = 4096):
         vals, idx, L = ov, oi, nseg * k
         if nseg == 1:
             return vals, idx
+
+
+def copy_blocks(kv_data, src, dst):
+    """kv_data [L, 2, nb, Hkv, BS, D]: copy block src[i] -> dst[i] (all layers, K and V)."""
+    if kv_data.is_cuda:
+        lib().copy_blocks(kv_data, src, dst)
+    else:
+        kv_data[:, :, dst.long()] = kv_data[:, :, src.long()]
+    return kv_data

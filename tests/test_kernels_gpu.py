@@ -179,3 +179,44 @@ def test_sample_allowed_greedy_and_distribution():
             counts[pos[x]] += 1
     freq = counts / counts.sum()
     assert (freq - p).abs().max().item() < 0.05
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 512, 192), (1000, 6144, 4096), (513, 1028, 256)])
+def test_gemm_256_tile(M, N, K):
+    torch.manual_seed(1)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    assert rel_err(ops.gemm(X, W, algo=1), ref.gemm(X, W)) < 1e-2
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    assert rel_err(ops.gemm(X, W, R=R, algo=1), ref.gemm(X, W, R)) < 1e-2
+    # in-place residual (out aliases R), as the model's Wo / Wdown use it
+    R2 = R.clone()
+    ops.gemm(X, W, R=R2, out=R2, algo=1)
+    assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+
+
+def test_copy_blocks():
+    data = torch.randn(3, 2, 10, 2, 64, 128, device=DEV).bfloat16()
+    exp = data.clone()
+    src = torch.tensor([1, 4], dtype=torch.int32, device=DEV)
+    dst = torch.tensor([7, 2], dtype=torch.int32, device=DEV)
+    ops.copy_blocks(data, src, dst)
+    exp[:, :, [7, 2]] = exp[:, :, [1, 4]]
+    assert torch.equal(data, exp)
+
+
+@pytest.mark.parametrize("B,N,D,k", [(1, 10000, 1024, 32), (4, 70000, 256, 64), (3, 50, 128, 8)])
+def test_topk_cosine(B, N, D, k):
+    torch.manual_seed(2)
+    corpus = torch.randn(N, D, device=DEV).bfloat16()
+    ops.l2norm_rows(corpus)
+    q = torch.randn(B, D, device=DEV).bfloat16()
+    ops.l2norm_rows(q)
+    vals, idx = ops.topk_cosine(q, corpus, k)
+    ref_s = q.float() @ corpus.float().t()
+    rv, ri = torch.topk(ref_s, k=min(k, N), dim=-1)
+    assert torch.allclose(vals, rv, atol=1e-4)
+    # indices may differ only where scores tie
+    got = ref_s.gather(1, idx.long())
+    assert torch.allclose(got, rv, atol=1e-4)
+    assert (vals[:, :-1] >= vals[:, 1:]).all()

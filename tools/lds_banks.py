@@ -64,3 +64,24 @@ if __name__ == "__main__":
     for n, f in cands256.items():
         print("ATTN K 256B rows", n, [gemm_a_read(f, 256, ks) for ks in range(4)],
               "V tr", [attn_v_tr_read(f, ks, dt, s) for ks in (0, 1) for dt in (0, 3) for s in (0, 1)])
+
+
+def search_64B_rows():
+    """256 x 32 bf16 k-half pieces: 64-B rows, 4 x 16-B chunks per row."""
+    import itertools
+    best = []
+    for a, b, c in itertools.product(range(4), repeat=3):
+        # g(r) = linear combination of bit-pairs of the row index
+        def swz(r, ch, a=a, b=b, c=c):
+            g = (((r >> 2) & 3) * a + ((r >> 4) & 3) * b + (r & 3) * c) & 3
+            return ch ^ g
+        costs = []
+        for t in range(4):                       # 4 row-tiles of 16 rows
+            addrs = []
+            for l in range(64):
+                r, ch = 16 * t + (l & 15), l >> 4
+                addrs.append(r * 64 + 16 * swz(r, ch))
+            costs.append(cost(addrs, 16, B128_GROUPS))
+        best.append((max(costs), (a, b, c)))
+    best.sort()
+    return best[:5]
