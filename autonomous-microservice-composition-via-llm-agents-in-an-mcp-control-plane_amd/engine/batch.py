@@ -80,31 +80,51 @@ class DeviceStep:
     attn: AttnMeta
 
 
-def pack(step: StepInputs, group: int, device, pin: bool = True) -> DeviceStep:
-    """Pack all int32 arrays into one buffer -> one H2D copy -> views."""
+def pack_host(step: StepInputs, group: int, copies=()):
+    """All int32 metadata of one step (+ prefix copy-on-write block pairs) in
+    ONE host array; ``layout`` = the segment sizes (also what TP workers need)."""
     work = build_work(step.q_len.tolist(), group)
+    cp = np.asarray(copies, np.int32).reshape(-1, 2) if len(copies) else np.zeros((0, 2), np.int32)
     parts = [step.token_ids, step.positions, step.slots, step.logit_rows, step.q_start,
              step.q_len, step.ctx_len, step.block_table.reshape(-1)]
     for nw in (1, 4):
         parts += [np.asarray(work[nw][0], np.int32), np.asarray(work[nw][1], np.int32)]
-    sizes = [int(p.size) for p in parts]
-    host = np.concatenate([np.asarray(p, dtype=np.int32).reshape(-1) for p in parts])
+    parts += [cp[:, 0].copy(), cp[:, 1].copy()]
+    layout = [int(p.size) for p in parts] + [int(step.q_len.shape[0])]
+    host = np.concatenate([np.asarray(p, dtype=np.int32).reshape(-1) for p in parts]) \
+        if sum(layout[:-1]) else np.zeros(0, np.int32)
+    return host, layout
+
+
+def to_device(host: np.ndarray, device, pin: bool = True) -> torch.Tensor:
     t = torch.from_numpy(host)
     if device is not None and torch.device(device).type == "cuda":
         if pin:
             t = t.pin_memory()
         t = t.to(device, non_blocking=True)
-    views, off = [], 0
+    return t
+
+
+def views(t: torch.Tensor, layout):
+    """Inverse of ``pack_host`` on an (already transferred) int32 tensor.
+    Returns (DeviceStep, copy_src, copy_dst)."""
+    sizes, S = layout[:-1], layout[-1]
+    vs, off = [], 0
     for n in sizes:
-        views.append(t[off:off + n])
+        vs.append(t[off:off + n])
         off += n
-    S = step.q_len.shape[0]
-    bt = views[7].view(S, -1) if S else views[7].view(0, 1)
+    bt = vs[7].view(S, -1) if S else vs[7].view(0, 1)
     work_l = []
     for i, nw in enumerate((1, 4)):
-        ws, wq = views[8 + 2 * i], views[9 + 2 * i]
+        ws, wq = vs[8 + 2 * i], vs[9 + 2 * i]
         if ws.numel():
             work_l.append((nw, ws, wq))
-    meta = AttnMeta(q_start=views[4], q_len=views[5], ctx_len=views[6], block_table=bt, work=work_l)
-    return DeviceStep(token_ids=views[0], positions=views[1], slots=views[2], logit_rows=views[3],
-                      attn=meta)
+    meta = AttnMeta(q_start=vs[4], q_len=vs[5], ctx_len=vs[6], block_table=bt, work=work_l)
+    return DeviceStep(token_ids=vs[0], positions=vs[1], slots=vs[2], logit_rows=vs[3],
+                      attn=meta), vs[12], vs[13]
+
+
+def pack(step: StepInputs, group: int, device, pin: bool = True) -> DeviceStep:
+    """Pack all int32 arrays into one buffer -> one H2D copy -> views."""
+    host, layout = pack_host(step, group)
+    return views(to_device(host, device, pin), layout)[0]

@@ -31,7 +31,7 @@ import torch
 
 from .. import ops
 from ..utils.metrics import METRICS
-from .batch import BLOCK_SIZE, StepInputs, pack
+from .batch import BLOCK_SIZE, StepInputs, pack_host, to_device, views
 from .kv_cache import KVCache
 
 _uid = itertools.count(1)
@@ -75,10 +75,11 @@ class Sequence:
 class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
-                 seed: int = 0):
+                 seed: int = 0, bcast=None):
         self.model = model
         cfg = model.cfg
         self.device = model.device
+        self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
         if num_blocks is not None:
             self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
         else:
@@ -186,11 +187,6 @@ class LLMEngine:
         for seq in self.running:
             if not seq.materialized and seq.prefix.computed:
                 self._materialize(seq, copies)
-        if copies:
-            pairs = torch.tensor(copies, dtype=torch.int32).t().contiguous()
-            if self.device.type == "cuda":
-                pairs = pairs.pin_memory().to(self.device, non_blocking=True)
-            ops.copy_blocks(self.kv.data, pairs[0], pairs[1])
         budget = self.max_step_tokens
         ids, pos, slots = [], [], []
         q_start, q_len, ctx_len, tables = [], [], [], []
@@ -224,6 +220,8 @@ class LLMEngine:
                 logit_rows.append(T - 1)
                 sample_seqs.append(seq)
         if T == 0:
+            if copies:     # copy-on-write blocks still have to land before later steps
+                self._launch(None, copies)
             return 0
         S = len(batch_seqs)
         maxb = max(len(t) for t in tables)
@@ -235,9 +233,8 @@ class LLMEngine:
                           q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
                           ctx_len=np.asarray(ctx_len, np.int32), block_table=bt,
                           logit_rows=np.asarray(logit_rows, np.int32))
-        dev = pack(step, self.model.cfg.group, self.device)
         t0 = time.perf_counter()
-        hidden = self.model.forward(dev, self.kv)
+        hidden = self._launch(step, copies)
         new_tokens = self._sample(hidden, sample_seqs)
         self.stats["forward_s"] += time.perf_counter() - t0
         self.stats["tokens"] += T
@@ -262,6 +259,28 @@ class LLMEngine:
         METRICS.set("batch_occupancy", len(self.running))
         METRICS.set("kv_block_utilization", self.alloc.utilization())
         return T
+
+    def _launch(self, step: Optional[StepInputs], copies) -> Optional[torch.Tensor]:
+        """Pack -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
+        if step is None:
+            empty = np.zeros(0, np.int32)
+            step = StepInputs(token_ids=empty, positions=empty, slots=empty, q_start=empty,
+                              q_len=empty, ctx_len=empty, block_table=np.zeros((0, 1), np.int32),
+                              logit_rows=empty)
+        host, layout = pack_host(step, self.model.cfg.group, copies)
+        payload = to_device(host, self.device)
+        if self.bcast is not None:
+            self.bcast.send(payload, layout)
+        dstep, csrc, cdst = views(payload, layout)
+        if csrc.numel():
+            ops.copy_blocks(self.kv.data, csrc, cdst)
+        if dstep.token_ids.numel() == 0:
+            return None
+        return self.model.forward(dstep, self.kv)
+
+    def shutdown_workers(self):
+        if self.bcast is not None:
+            self.bcast.stop()
 
     def _sample(self, hidden: torch.Tensor, seqs: List[Sequence]) -> List[int]:
         if not seqs:

@@ -70,6 +70,7 @@ CONFIGS = {
     # reduced configs with the same kernels (tests / smoke): head_dim stays 128
     "llama3-1b-ish": LlamaConfig("llama3-1b-ish", hidden=2048, layers=16, heads=16, kv_heads=4, ffn=8192),
     "tiny": LlamaConfig("tiny", hidden=256, layers=2, heads=2, kv_heads=1, ffn=512),
+    "tiny-tp": LlamaConfig("tiny-tp", hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024),
 }
 
 

@@ -1,0 +1,98 @@
+"""Process groups and collectives (collective sites C1-C5).
+
+One process per GPU; ``torch.distributed`` with backend ``"nccl"`` is RCCL on
+ROCm and runs over xGMI between the 8 MI355X of a node.  The CPU test tier
+uses ``gloo`` with the same code paths.
+
+* ``init_distributed``  – env:// rendezvous (torchrun), binds the local GPU.
+* ``make_allreduce``    – in-place sum for the row-parallel projections
+  (C1 after Wo, C2 after Wdown).  GPU: RCCL all-reduce, or the one-shot xGMI
+  peer-to-peer kernel of ``parallel.custom_allreduce`` for decode-sized
+  messages when enabled (``MCP_CUSTOM_ALLREDUCE=1``); CPU: gloo in fp32.
+* ``StepBroadcaster``   – C4: the driver rank broadcasts each step's packed
+  int32 descriptor (tokens, positions, slots, block tables, work lists, KV
+  copy-on-write pairs) to the TP worker ranks.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def init_distributed(backend: Optional[str] = None):
+    """Returns (rank, world_size, local_rank, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        if use_gpu:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend or "nccl", device_id=device)
+        else:
+            dist.init_process_group(backend or "gloo")
+    return rank, world, local_rank, device
+
+
+def make_allreduce(group, device) -> Callable[[torch.Tensor], None]:
+    device = torch.device(device)
+    if device.type != "cuda":
+        def cpu_allreduce(t: torch.Tensor):
+            tf = t.float()
+            dist.all_reduce(tf, group=group)
+            t.copy_(tf.to(t.dtype))
+        return cpu_allreduce
+    custom = None
+    if os.environ.get("MCP_CUSTOM_ALLREDUCE", "0") == "1":
+        from .custom_allreduce import CustomAllReduce
+        custom = CustomAllReduce(group, device)
+
+    def gpu_allreduce(t: torch.Tensor):
+        if custom is not None and custom.eligible(t):
+            custom(t)
+        else:
+            dist.all_reduce(t, group=group)
+    return gpu_allreduce
+
+
+class StepBroadcaster:
+    """Driver -> worker step descriptors for tensor-parallel engines."""
+
+    HDR = 32
+
+    def __init__(self, group, device, src: int = 0):
+        self.group, self.device, self.src = group, torch.device(device), src
+
+    def _bcast(self, t: torch.Tensor):
+        dist.broadcast(t, src=self.src, group=self.group)
+
+    def send(self, payload: torch.Tensor, layout) -> None:
+        hdr = np.full(self.HDR, 0, np.int32)
+        hdr[0], hdr[1] = payload.numel(), len(layout)
+        hdr[2:2 + len(layout)] = layout
+        self._bcast(torch.from_numpy(hdr).to(self.device))
+        if payload.numel():
+            self._bcast(payload if payload.device == self.device else payload.to(self.device))
+
+    def stop(self) -> None:
+        hdr = np.zeros(self.HDR, np.int32)
+        hdr[0] = -1
+        self._bcast(torch.from_numpy(hdr).to(self.device))
+
+    def recv(self):
+        hdr = torch.zeros(self.HDR, dtype=torch.int32, device=self.device)
+        self._bcast(hdr)
+        h = hdr.cpu().numpy()
+        n, nl = int(h[0]), int(h[1])
+        if n < 0:
+            return None
+        layout = [int(x) for x in h[2:2 + nl]]
+        payload = torch.empty(n, dtype=torch.int32, device=self.device)
+        if n:
+            self._bcast(payload)
+        return payload, layout
