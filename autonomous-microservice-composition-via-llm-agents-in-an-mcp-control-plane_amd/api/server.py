@@ -66,6 +66,11 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
         if planner is not None:
             return planner
         if settings.planner_backend == "local":
+            if settings.replicas > 1:
+                from ..parallel.router import ReplicaRouter, default_devices
+                return ReplicaRouter(default_devices(settings.replicas), settings.model, registry,
+                                     max_batch=settings.max_batch, max_nodes=settings.max_nodes,
+                                     seed=settings.seed)
             from ..planner.local import LocalPlanner
             return LocalPlanner.from_settings(settings, registry)
         return StubPlanner(registry)
