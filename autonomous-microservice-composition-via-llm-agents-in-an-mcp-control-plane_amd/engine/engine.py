@@ -92,7 +92,8 @@ class LLMEngine:
         self.seed = seed
         self.running: List[Sequence] = []
         self.waiting: List[Sequence] = []
-        self.prefixes: Dict[tuple, PrefixEntry] = {}
+        self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
+        self.max_prefixes = 64
         self.steps = 0
         self.stats = {"tokens": 0, "samples": 0, "forward_s": 0.0, "steps": 0}
 
@@ -103,8 +104,13 @@ class LLMEngine:
         tokens = tuple(tokens)
         if len(tokens) < BLOCK_SIZE:
             return None
-        e = self.prefixes.get(tokens)
-        if e is None:
+        e = self.prefixes.pop(tokens, None)
+        if e is not None:
+            self.prefixes[tokens] = e                  # refresh LRU position
+        else:
+            while len(self.prefixes) >= self.max_prefixes:   # evict the LRU entry
+                old = next(iter(self.prefixes))
+                self.alloc.free(self.prefixes.pop(old).blocks)
             blocks = self.alloc.alloc((len(tokens) + BLOCK_SIZE - 1) // BLOCK_SIZE)
             e = PrefixEntry(tokens=tokens, blocks=blocks, length=len(tokens))
             self.prefixes[tokens] = e

@@ -21,7 +21,7 @@ import time
 from typing import Optional
 
 from ..utils.metrics import METRICS
-from .prompt import build_prompt
+from .prompt import PromptCache
 
 
 class Planner:
@@ -46,11 +46,13 @@ class StubPlanner(Planner):
         self.canned = canned
         self.max_nodes = max_nodes
         self.last_prompt: Optional[str] = None
+        self._prompts = PromptCache()
 
     async def plan(self, intent: str) -> dict:
         t0 = time.perf_counter()
         services = self.registry.list_services() if self.registry is not None else []
-        self.last_prompt = build_prompt(services, intent)
+        prefix, suffix = self._prompts.parts(services, intent, getattr(self.registry, "version", None))
+        self.last_prompt = prefix + suffix
         if isinstance(self.canned, str):
             dag = json.loads(self.canned)
         elif self.canned is not None:

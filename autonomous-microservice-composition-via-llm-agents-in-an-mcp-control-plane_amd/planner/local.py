@@ -80,12 +80,14 @@ class LocalPlanner(Planner):
             if len(self._spec_cache) > 256:
                 self._spec_cache.clear()
             self._spec_cache[key] = spec
-        prefix, suffix = build_prompt_parts(cands, intent)
         ptoks = self._prefix_cache.get(key)
         if ptoks is None:
+            prefix, _ = build_prompt_parts(cands, intent)
             ptoks = [self.tok.bos_id] + self.tok.encode(prefix)
+            if len(self._prefix_cache) > 256:
+                self._prefix_cache.clear()
             self._prefix_cache[key] = ptoks
-        return DagDecoder(spec), ptoks, self.tok.encode(suffix)
+        return DagDecoder(spec), ptoks, self.tok.encode(f"\nUser intent: “{intent}”\n\nJSON DAG:")
 
     # ------------------------------------------------------- batch (sync)
     def plan_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> List[dict]:

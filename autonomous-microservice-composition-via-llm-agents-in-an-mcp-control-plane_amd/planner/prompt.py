@@ -39,6 +39,26 @@ def build_prompt_parts(services: Sequence, intent: str) -> Tuple[str, str]:
     return prefix, suffix
 
 
+class PromptCache:
+    """Registry prefix text cached per (registry version, candidate names): the
+    reference rebuilds it from every record on every call (control_plane.py:60-66)."""
+
+    def __init__(self, maxsize: int = 256):
+        self._c = {}
+        self.maxsize = maxsize
+
+    def parts(self, services: Sequence, intent: str, version=None) -> Tuple[str, str]:
+        key = (version, tuple(s["name"] for s in services)) if version is not None else None
+        prefix = self._c.get(key) if key is not None else None
+        if prefix is None:
+            prefix = HEADER + "".join(service_line(s) for s in services)
+            if key is not None:
+                if len(self._c) >= self.maxsize:
+                    self._c.clear()
+                self._c[key] = prefix
+        return prefix, f"\nUser intent: “{intent}”\n\nJSON DAG:"
+
+
 def build_prompt(services: Sequence, intent: str) -> str:
     p, s = build_prompt_parts(services, intent)
     return p + s

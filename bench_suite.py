@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Benchmarks for the BASELINE.json configs other than the headline one.
+
+  python bench_suite.py plumbing            # config 1: CPU, stub planner
+  python bench_suite.py topk [--n 10000]    # config 3: HBM top-k cosine (GPU)
+
+Config 1 mirrors the reference measurements in BASELINE.md / SURVEY §6 (stub
+LLM, MockTransport services, FastAPI TestClient, p50 of 30 runs):
+``/plan`` overhead at 3/10/50/1000 services and ``/execute`` overhead on
+3/10/50-node chains.  Each line is JSON.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+REF_PLAN_MS = {3: 1.42, 10: 1.53, 50: 1.81, 1000: 8.79}          # SURVEY §6 (reference plumbing)
+REF_EXEC_MS = {3: 1.89, 10: 3.16, 50: 10.08}
+
+
+def plumbing(runs: int = 30):
+    import httpx
+    from fastapi.testclient import TestClient
+    from mcp_amd.api.server import create_app
+    from mcp_amd.config import Settings
+    from mcp_amd.planner.base import StubPlanner
+    from mcp_amd.registry import MemoryRegistry, synthetic_registry
+
+    def handler(request):
+        return httpx.Response(200, json={"ok": True})
+    canned = {"nodes": [{"name": "a", "endpoint": "http://a/api", "inputs": {"x": "uid"}}], "edges": []}
+    for n in (3, 10, 50, 1000):
+        reg = MemoryRegistry(synthetic_registry(n, seed=1))
+        app = create_app(Settings(), registry=reg, planner=StubPlanner(reg, canned=canned),
+                         transport=httpx.MockTransport(handler))
+        with TestClient(app) as c:
+            for _ in range(5):
+                c.post("/plan", json={"intent": "warm"})
+            ts = []
+            for i in range(runs):
+                t = time.perf_counter()
+                r = c.post("/plan", json={"intent": f"charge order {i}"})
+                ts.append(time.perf_counter() - t)
+                assert r.status_code == 200
+        p50 = statistics.median(ts) * 1e3
+        print(json.dumps({"config": "plumbing/plan", "services": n, "p50_ms": round(p50, 3),
+                          "reference_ms": REF_PLAN_MS[n], "speedup": round(REF_PLAN_MS[n] / p50, 2)}))
+    for n in (3, 10, 50):
+        nodes = [{"name": f"n{i}", "endpoint": f"http://n{i}/api",
+                  "inputs": {"x": f"n{i - 1}" if i else "uid"}} for i in range(n)]
+        edges = [{"from": f"n{i - 1}", "to": f"n{i}"} for i in range(1, n)]
+        reg = MemoryRegistry(synthetic_registry(3))
+        app = create_app(Settings(), registry=reg, planner=StubPlanner(reg),
+                         transport=httpx.MockTransport(handler))
+        with TestClient(app) as c:
+            body = {"graph": {"nodes": nodes, "edges": edges}, "payload": {"uid": 1}}
+            for _ in range(5):
+                c.post("/execute", json=body)
+            ts = []
+            for _ in range(runs):
+                t = time.perf_counter()
+                r = c.post("/execute", json=body)
+                ts.append(time.perf_counter() - t)
+                assert r.status_code == 200
+        p50 = statistics.median(ts) * 1e3
+        print(json.dumps({"config": "plumbing/execute", "nodes": n, "p50_ms": round(p50, 3),
+                          "reference_ms": REF_EXEC_MS[n], "speedup": round(REF_EXEC_MS[n] / p50, 2)}))
+
+
+def topk(n: int, dim: int, k: int, batches=(1, 16, 64), iters: int = 50):
+    import torch
+    import mcp_amd.ops as ops
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    corpus = torch.randn(n, dim, device=dev, generator=g).bfloat16()
+    ops.l2norm_rows(corpus)
+    for b in batches:
+        q = torch.randn(b, dim, device=dev, generator=g).bfloat16()
+        ops.l2norm_rows(q)
+        v, i = ops.topk_cosine(q, corpus, k)
+        rv, _ = torch.topk(q.float() @ corpus.float().t(), k, dim=-1)
+        ok = bool(torch.allclose(v, rv, atol=1e-4))
+        for _ in range(3):
+            ops.topk_cosine(q, corpus, k)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            ops.topk_cosine(q, corpus, k)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        gbs = n * dim * 2 / ms / 1e6
+        print(json.dumps({"config": "topk_cosine", "corpus": n, "dim": dim, "k": k, "queries": b,
+                          "latency_ms": round(ms, 4), "corpus_GBps": round(gbs, 1), "exact": ok}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", choices=["plumbing", "topk"])
+    ap.add_argument("--n", type=int, default=10000)
+    ap.add_argument("--dim", type=int, default=1024)
+    ap.add_argument("--k", type=int, default=32)
+    a = ap.parse_args()
+    if a.which == "plumbing":
+        plumbing()
+    else:
+        topk(a.n, a.dim, a.k)
