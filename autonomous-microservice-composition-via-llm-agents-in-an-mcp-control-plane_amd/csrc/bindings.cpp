@@ -87,6 +87,14 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
   launch_gemm_tn_algo(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, (int)algo, stream());
 }
 
+void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64_t v) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
+  const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
+  TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_variant: unsupported shape");
+  TORCH_CHECK(launch_gemm_tn_256_variant(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, v,
+                                         stream()) == 0, "bad variant");
+}
+
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
   TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
@@ -192,6 +200,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none(),
         py::arg("algo") = -1);
   m.def("gemm_select", &gemm_select);
+  m.def("gemm_variant", &gemm_variant);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),

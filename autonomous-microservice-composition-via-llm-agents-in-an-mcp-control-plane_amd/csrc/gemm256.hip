@@ -38,7 +38,20 @@ DEV void barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool RESID>
+// Structural variants (A/B-tested in one process, tools/bench_gemm.py):
+//   BAR4  : barrier after every phase (else only where a new piece is consumed
+//           next, i.e. after phases 1 and 3 -- WAR/RAW need nothing more)
+//   PREA  : even phases also read the odd phase's A fragments, so odd phases
+//           issue no LDS reads and their MFMAs start immediately
+//   PRIO  : s_setprio 1 around the MFMA cluster
+//   GFIRST: issue the next K-tile's LDS-DMA piece before this phase's ds_reads
+template <bool BAR4, bool PREA, bool PRIO, bool GFIRST>
+struct V256 {
+  static constexpr bool bar4 = BAR4, prea = PREA, prio = PRIO, gfirst = GFIRST;
+};
+using V256Default = V256<false, false, false, true>;   // variant 8: best of the 16-way sweep
+
+template <bool RESID, class VAR = V256Default>
 __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X,
                                                       const bf16* __restrict__ W,
                                                       bf16* __restrict__ Y,
@@ -111,32 +124,40 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
   barrier();
 
   bf16x8 bfr[4];
+  bf16x8 afr[2][4];
   auto phase = [&](int t, int p, bool prefetch, bool last) {
     const int kh = p >> 1, mh = p & 1;
     const bf16* sA = smem + ((t & 1) * 4 + 2 * kh) * PIECE;
     const bf16* sB = sA + PIECE;
-    bf16x8 af[4];
+    if (VAR::gfirst && prefetch) stage(t + 1, p);
     if (mh == 0) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) bfr[nt] = *reinterpret_cast<const bf16x8*>(sB + offB[nt]);
     }
+    if (!VAR::prea || mh == 0) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) af[mt] = *reinterpret_cast<const bf16x8*>(sA + offA[mh][mt]);
-    if (prefetch) stage(t + 1, p);
-    __builtin_amdgcn_s_setprio(1);
+      for (int mt = 0; mt < 4; ++mt)
+        afr[mh][mt] = *reinterpret_cast<const bf16x8*>(sA + offA[mh][mt]);
+    }
+    if (VAR::prea && mh == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) afr[1][mt] = *reinterpret_cast<const bf16x8*>(sA + offA[1][mt]);
+    }
+    if (!VAR::gfirst && prefetch) stage(t + 1, p);
+    if (VAR::prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        acc[mh][mt][nt] = mfma16x16x32(bfr[nt], af[mt], acc[mh][mt][nt]);
-    __builtin_amdgcn_s_setprio(0);
+        acc[mh][mt][nt] = mfma16x16x32(bfr[nt], afr[mh][mt], acc[mh][mt][nt]);
+    if (VAR::prio) __builtin_amdgcn_s_setprio(0);
     if (p == 1) {
       if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else if (p == 3 && !last) {
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     }
-    barrier();
+    if (VAR::bar4 || p == 1 || p == 3) barrier();
   };
 
   for (int t = 0; t + 1 < nk; ++t) {
@@ -178,7 +199,41 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
     }
 }
 
+template <class VAR>
+void launch_var(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  gemm_tn_256<false, VAR><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                        nullptr, M, N, K);
+}
+
 }  // namespace
+
+int launch_gemm_tn_256_ring(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                            int K, int stages, hipStream_t s);
+
+int launch_gemm_tn_256w4(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                         int stages, hipStream_t s);
+
+int launch_gemm_tn_256w4m16(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                            int K, int stages, hipStream_t s);
+
+// tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
+int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
+                               hipStream_t s) {
+  switch (v) {
+#define VCASE(i) case i: launch_var<V256<(i & 1) != 0, (i & 2) != 0, (i & 4) != 0, (i & 8) != 0>>(X, W, Y, M, N, K, s); return 0;
+    VCASE(0) VCASE(1) VCASE(2) VCASE(3) VCASE(4) VCASE(5) VCASE(6) VCASE(7)
+    VCASE(8) VCASE(9) VCASE(10) VCASE(11) VCASE(12) VCASE(13) VCASE(14) VCASE(15)
+#undef VCASE
+    case 16: case 17: case 18:
+      return launch_gemm_tn_256_ring(X, W, Y, nullptr, M, N, K, v - 13, s);
+    case 20: case 21:
+      return launch_gemm_tn_256w4(X, W, Y, nullptr, M, N, K, v - 16, s);
+    case 22: case 23:
+      return launch_gemm_tn_256w4m16(X, W, Y, nullptr, M, N, K, v - 18, s);
+    default: return 1;
+  }
+}
 
 void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         hipStream_t s) {
@@ -190,4 +245,163 @@ void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, in
   else
     gemm_tn_256<false><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M,
                                             N, K);
+}
+
+// ============================================================================
+// Ring-pipelined 256x256 variant: 32-deep k-steps, an S-slot LDS ring (one
+// slot = A 256x32 + B 256x32 = 32 KiB), prefetch distance S-1 k-steps, ONE
+// barrier per k-step.  At k-step j the loads of k-step j+S-1 go into the slot
+// read at step j-1 (WAR-safe behind that step's barrier); before the barrier
+// ending step j every thread waits until step j+1's pieces landed: it may
+// leave 4 x (#later k-steps issued) LDS-DMA ops in flight (counted vmcnt).
+// Per k-step and wave: 12 ds_read_b128 (4 B + 8 A) and 32 MFMAs.
+namespace {
+
+template <int S, bool RESID>
+__global__ __launch_bounds__(512, 1) void gemm_tn_256_ring(const bf16* __restrict__ X,
+                                                           const bf16* __restrict__ W,
+                                                           bf16* __restrict__ Y,
+                                                           const bf16* __restrict__ R, int M,
+                                                           int N, int K) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[S * 2 * PIECE];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const int nwg = nm * nn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * nn;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP;
+  const int gsz = min(nm - first_m, GROUP);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const bf16* srcA[2];
+  const bf16* srcB[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (2 * wave + j) * 16 + (lane >> 2);
+    const int ch = swz(row, lane & 3);
+    srcA[j] = X + (size_t)min(m0 + row, M - 1) * K + ch * 8;
+    srcB[j] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
+  }
+  auto stage = [&](int step) {               // both pieces of k-step `step`
+    const int koff = step * KH;
+    bf16* slot = smem + (step % S) * 2 * PIECE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(srcA[j] + koff, slot + (2 * wave + j) * 512);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(srcB[j] + koff, slot + PIECE + (2 * wave + j) * 512);
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[2][4][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[a][b][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int offA[2][4], offB[4];
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int row = wm * 128 + mh * 64 + mt * 16 + fr;
+      offA[mh][mt] = row * KH + swz(row, fq) * 8;
+    }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int row = wn * 64 + nt * 16 + fr;
+    offB[nt] = row * KH + swz(row, fq) * 8;
+  }
+
+  const int ns = K / KH;
+  // prologue: k-steps 0 .. S-2 in flight, wait for step 0
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j)
+    if (j < ns) stage(j);
+  {
+    const int later = min(S - 1, ns) - 1;      // steps issued after step 0
+    if (later >= S - 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (S - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+
+  for (int j = 0; j < ns; ++j) {
+    if (j + S - 1 < ns) stage(j + S - 1);
+    const bf16* sA = smem + (j % S) * 2 * PIECE;
+    const bf16* sB = sA + PIECE;
+    bf16x8 bfr[4], afr[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bfr[nt] = *reinterpret_cast<const bf16x8*>(sB + offB[nt]);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        afr[mh][mt] = *reinterpret_cast<const bf16x8*>(sA + offA[mh][mt]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mh][mt][nt] = mfma16x16x32(bfr[nt], afr[mh][mt], acc[mh][mt][nt]);
+    __builtin_amdgcn_s_setprio(0);
+    // step j+1 must have landed; loads of steps j+2 .. min(j+S-1, ns-1) may stay in flight
+    const int later = min(j + S - 1, ns - 1) - (j + 1);
+    if (later >= S - 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (S - 2)) : "memory");
+    else if (later == 2 && S - 2 > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1 && S - 2 > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+  }
+
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = m0 + wm * 128 + mh * 64 + mt * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int n = n0 + wn * 64 + nt * 16 + fq * 4;
+        if (n >= N) continue;
+        f32x4 v = acc[mh][mt][nt];
+        if (RESID) {
+          const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += (float)r[q];
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)v[q];
+        *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+      }
+    }
+}
+
+}  // namespace
+
+int launch_gemm_tn_256_ring(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                            int K, int stages, hipStream_t s) {
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const dim3 grid(nm * nn);
+  auto x = (const bf16*)X;
+  auto w = (const bf16*)W;
+  auto y = (bf16*)Y;
+  auto r = (const bf16*)R;
+  switch (stages) {
+    case 3: if (R) gemm_tn_256_ring<3, true><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K);
+            else gemm_tn_256_ring<3, false><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K); return 0;
+    case 4: if (R) gemm_tn_256_ring<4, true><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K);
+            else gemm_tn_256_ring<4, false><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K); return 0;
+    case 5: if (R) gemm_tn_256_ring<5, true><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K);
+            else gemm_tn_256_ring<5, false><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K); return 0;
+    default: return 1;
+  }
 }
