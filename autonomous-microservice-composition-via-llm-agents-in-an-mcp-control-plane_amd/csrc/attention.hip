@@ -35,13 +35,38 @@ DEV bf16x4 tr_read(const bf16* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
-template <int NW, int G>
-__global__ __launch_bounds__(NW * 64) void attn_kernel(
-    const bf16* __restrict__ q, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
-    bf16* __restrict__ out, const int* __restrict__ q_start, const int* __restrict__ q_len,
-    const int* __restrict__ ctx_len, const int* __restrict__ block_table, int max_blocks,
-    const int* __restrict__ work_seq, const int* __restrict__ work_q0, int Hq, int Hkv,
-    float scale_log2) {
+struct AttnArgs {
+  const bf16* q;
+  const bf16* kc;
+  const bf16* vc;
+  bf16* out;
+  const int* q_start;
+  const int* q_len;
+  const int* ctx_len;
+  const int* block_table;
+  int max_blocks;
+  const int* work_seq;
+  const int* work_q0;
+  int Hq, Hkv;
+  float scale_log2;
+  // cascade (shared-prefix) attention
+  const int* kv_begin;     // MODE 0: per-sequence first key (multiple of 64) or null
+  const bf16* pre_o;       // MODE 0: normalised prefix partial O [T, Hq, D] to merge
+  const float* pre_lse;    // MODE 0: its log2-sum-exp [T, Hq]
+  float* lse_out;          // MODE 1: log2-sum-exp of the prefix partial
+  const int* pre_bt;       // MODE 1: block table of the shared prefix
+  int pre_keys;            // MODE 1: prefix keys (multiple of 64)
+  int pre_tokens;          // MODE 1: query tokens [0, pre_tokens) of the flat batch
+};
+
+// MODE 0: per (sequence, q-tile) work item, causal over keys
+//         [kv_begin[s], ctx_len[s]); merges the prefix partial when present.
+// MODE 1: shared-prefix pass: the flat query tokens [0, pre_tokens) of every
+//         sequence that shares one registry prefix, 16-token tiles that mix
+//         sequences (they attend to the same K/V), no mask (every query sits
+//         after the prefix).  Writes normalised O and its LSE.
+template <int NW, int G, int MODE>
+__global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   constexpr int TPW = 16 / G;                 // tokens per wave
   constexpr int QT = NW * TPW;                // tokens per work item
   constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
@@ -50,27 +75,43 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kvh = blockIdx.y;
-  const int s = work_seq[blockIdx.x];
-  const int q0 = work_q0[blockIdx.x];
-  const int qs = q_start[s], ql = q_len[s], cl = ctx_len[s];
-  const int* bt = block_table + (size_t)s * max_blocks;
-
   const int fr = lane & 15, fq = lane >> 4;
-  // this lane's query row
-  const int tok = q0 + wave * TPW + fr / G;   // index inside the sequence's query span
   const int head = kvh * G + fr % G;
-  const bool qvalid = tok < ql;
-  const int qpos = cl - ql + tok;             // absolute position (causal bound)
+  const int Hq = a.Hq, Hkv = a.Hkv;
 
-  // last position any row of this work item needs
-  const int last_tok = min(q0 + QT, ql) - 1;
-  const int kv_end = cl - ql + last_tok + 1;
-  const int ntiles = (kv_end + KT - 1) / KT;
+  int s = 0, qs, ql, cl, tok, qpos, kt0, ntiles;
+  bool qvalid;
+  const int* bt;
+  if (MODE == 1) {
+    tok = blockIdx.x * QT + wave * TPW + fr / G;          // flat token index
+    qvalid = tok < a.pre_tokens;
+    qs = 0;
+    ql = a.pre_tokens;
+    cl = a.pre_keys;
+    qpos = 1 << 30;                                       // no causal limit inside the prefix
+    kt0 = 0;
+    ntiles = a.pre_keys / KT;
+    bt = a.pre_bt;
+  } else {
+    s = a.work_seq[blockIdx.x];
+    const int q0 = a.work_q0[blockIdx.x];
+    qs = a.q_start[s];
+    ql = a.q_len[s];
+    cl = a.ctx_len[s];
+    bt = a.block_table + (size_t)s * a.max_blocks;
+    tok = q0 + wave * TPW + fr / G;                       // index inside the query span
+    qvalid = tok < ql;
+    qpos = cl - ql + tok;
+    const int last_tok = min(q0 + QT, ql) - 1;
+    const int kv_end = cl - ql + last_tok + 1;
+    ntiles = (kv_end + KT - 1) / KT;
+    kt0 = a.kv_begin ? a.kv_begin[s] / KT : 0;
+  }
 
   // Q fragments (B operand): lane holds Q[row fr][d = 32ks + 8fq + j]
   bf16x8 qf[4];
   {
-    const bf16* qp = q + ((size_t)(qs + (qvalid ? tok : 0)) * Hq + head) * D + 8 * fq;
+    const bf16* qp = a.q + ((size_t)(qs + (qvalid ? tok : 0)) * Hq + head) * D + 8 * fq;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 32 * ks);
@@ -82,8 +123,8 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(
   const int srow = lane >> 4;
   auto stage = [&](int kt, int buf) {
     const size_t blk = (size_t)bt[kt];
-    const bf16* kb = kc + (blk * Hkv + kvh) * (size_t)TILE;
-    const bf16* vb = vc + (blk * Hkv + kvh) * (size_t)TILE;
+    const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
+    const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
 #pragma unroll
     for (int i = 0; i < PIECES / NW; ++i) {
@@ -101,10 +142,10 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(
   for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_part = 0.f;
 
-  stage(0, 0);
+  if (kt0 < ntiles) stage(kt0, 0);
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
+  for (int kt = kt0; kt < ntiles; ++kt) {
+    const int cur = (kt - kt0) & 1;
     if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
     const bf16* Kl = smem + cur * 2 * TILE;
     const bf16* Vl = Kl + TILE;
@@ -129,7 +170,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt * KT + nt * 16 + fq * 4 + r;
-        float v = sacc[nt][r] * scale_log2;
+        float v = sacc[nt][r] * a.scale_log2;
         v = (key <= qpos && key < cl) ? v : -INFINITY;
         sacc[nt][r] = v;
         tmax = fmaxf(tmax, v);
@@ -177,56 +218,118 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
   if (!qvalid) return;
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16* op = out + ((size_t)(qs + tok) * Hq + head) * D + 4 * fq;
+  const size_t row = (size_t)(qs + tok) * Hq + head;
+  float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  float wa = 0.f, wb = 1.f;
+  const bf16* po = nullptr;
+  if (MODE == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
+    // merge with the shared-prefix partial: weights from the two log2-sum-exps
+    const float lse_b = m_run + __log2f(l_tot);
+    const float lse_a = a.pre_lse[row];
+    const float mx = fmaxf(lse_a, lse_b);
+    wa = exp2f(lse_a - mx);
+    wb = exp2f(lse_b - mx);
+    const float den = 1.f / (wa + wb);
+    wa *= den;
+    wb *= den;
+    po = a.pre_o + row * D + 4 * fq;
+  }
+  if (MODE == 1 && fq == 0) a.lse_out[row] = m_run + __log2f(l_tot);
+  bf16* op = a.out + row * D + 4 * fq;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
     bf16x4 w;
+    if (po) {
+      const bf16x4 pa = *reinterpret_cast<const bf16x4*>(po + dt * 16);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv);
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv * wb + (float)pa[r] * wa);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv);
+    }
     *reinterpret_cast<bf16x4*>(op + dt * 16) = w;
   }
 }
 
 template <int G>
-void attn_dispatch(int nw, const bf16* q, const bf16* kc, const bf16* vc, bf16* out,
-                   const int* q_start, const int* q_len, const int* ctx_len, const int* bt,
-                   int max_blocks, const int* ws, const int* wq, int nwork, int Hq, int Hkv,
-                   float sl2, hipStream_t s) {
-  const dim3 grid(nwork, Hkv);
+void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s) {
+  const dim3 grid(nwork, a.Hkv);
   if (nw == 1)
-    attn_kernel<1, G><<<grid, 64, 0, s>>>(q, kc, vc, out, q_start, q_len, ctx_len, bt, max_blocks,
-                                          ws, wq, Hq, Hkv, sl2);
+    attn_kernel<1, G, 0><<<grid, 64, 0, s>>>(a);
   else
-    attn_kernel<4, G><<<grid, 256, 0, s>>>(q, kc, vc, out, q_start, q_len, ctx_len, bt,
-                                           max_blocks, ws, wq, Hq, Hkv, sl2);
+    attn_kernel<4, G, 0><<<grid, 256, 0, s>>>(a);
+}
+
+template <int G>
+void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s) {
+  constexpr int QT = 4 * (16 / G);
+  const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
+  attn_kernel<4, G, 1><<<grid, 256, 0, s>>>(a);
 }
 
 }  // namespace
 
 int attn_tokens_per_item(int nw, int group) { return nw * (16 / group); }
 
+#define ATTN_SWITCH_G(G_, CALL)                     \
+  switch (G_) {                                     \
+    case 1: { constexpr int GG = 1; CALL; } break;  \
+    case 2: { constexpr int GG = 2; CALL; } break;  \
+    case 4: { constexpr int GG = 4; CALL; } break;  \
+    case 8: { constexpr int GG = 8; CALL; } break;  \
+    case 16: { constexpr int GG = 16; CALL; } break; \
+    default: return 3;                              \
+  }
+
 int launch_paged_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
                            const int* q_start, const int* q_len, const int* ctx_len,
                            const int* block_table, int max_blocks, const int* work_seq,
                            const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
-                           float scale, hipStream_t s) {
+                           float scale, const int* kv_begin, const void* pre_o,
+                           const float* pre_lse, hipStream_t s) {
   if (head_dim != D) return 1;
   if (nw != 1 && nw != 4) return 2;
   if (nwork <= 0) return 0;
-  const float sl2 = scale * 1.4426950408889634f;
-  const int G = Hq / Hkv;
-  auto qq = (const bf16*)q;
-  auto kk = (const bf16*)k_cache;
-  auto vv = (const bf16*)v_cache;
-  auto oo = (bf16*)out;
-  switch (G) {
-    case 1: attn_dispatch<1>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
-    case 2: attn_dispatch<2>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
-    case 4: attn_dispatch<4>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
-    case 8: attn_dispatch<8>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
-    case 16: attn_dispatch<16>(nw, qq, kk, vv, oo, q_start, q_len, ctx_len, block_table, max_blocks, work_seq, work_q0, nwork, Hq, Hkv, sl2, s); break;
-    default: return 3;
-  }
+  AttnArgs a{};
+  a.q = (const bf16*)q;
+  a.kc = (const bf16*)k_cache;
+  a.vc = (const bf16*)v_cache;
+  a.out = (bf16*)out;
+  a.q_start = q_start;
+  a.q_len = q_len;
+  a.ctx_len = ctx_len;
+  a.block_table = block_table;
+  a.max_blocks = max_blocks;
+  a.work_seq = work_seq;
+  a.work_q0 = work_q0;
+  a.Hq = Hq;
+  a.Hkv = Hkv;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.kv_begin = kv_begin;
+  a.pre_o = (const bf16*)pre_o;
+  a.pre_lse = pre_lse;
+  ATTN_SWITCH_G(Hq / Hkv, attn_dispatch<GG>(nw, a, nwork, s))
+  return 0;
+}
+
+int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
+                            float* lse_out, const int* pre_bt, int pre_keys, int pre_tokens,
+                            int Hq, int Hkv, int head_dim, float scale, hipStream_t s) {
+  if (head_dim != D) return 1;
+  if (pre_keys % KT) return 2;
+  if (pre_tokens <= 0 || pre_keys <= 0) return 0;
+  AttnArgs a{};
+  a.q = (const bf16*)q;
+  a.kc = (const bf16*)k_cache;
+  a.vc = (const bf16*)v_cache;
+  a.out = (bf16*)out;
+  a.Hq = Hq;
+  a.Hkv = Hkv;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.lse_out = lse_out;
+  a.pre_bt = pre_bt;
+  a.pre_keys = pre_keys;
+  a.pre_tokens = pre_tokens;
+  ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s))
   return 0;
 }

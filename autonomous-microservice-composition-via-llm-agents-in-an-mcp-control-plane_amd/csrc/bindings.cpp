@@ -128,7 +128,9 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
                      at::Tensor& out, const at::Tensor& q_start, const at::Tensor& q_len,
                      const at::Tensor& ctx_len, const at::Tensor& block_table,
                      const at::Tensor& work_seq, const at::Tensor& work_q0, int64_t nw,
-                     double scale) {
+                     double scale, const c10::optional<at::Tensor>& kv_begin,
+                     const c10::optional<at::Tensor>& pre_o,
+                     const c10::optional<at::Tensor>& pre_lse) {
   CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
   CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
   CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq); CHECK_I32_TENSOR(work_q0);
@@ -139,12 +141,42 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
   TORCH_CHECK(block_table.dim() == 2, "block_table [S, max_blocks]");
   TORCH_CHECK(work_seq.numel() == work_q0.numel(), "work list");
+  const int* kb = nullptr;
+  const void* po = nullptr;
+  const float* pl = nullptr;
+  if (kv_begin.has_value()) {
+    CHECK_I32_TENSOR((*kv_begin));
+    TORCH_CHECK(kv_begin->numel() == q_len.numel(), "kv_begin [S]");
+    TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "kv_begin needs pre_o / pre_lse");
+    CHECK_BF16_TENSOR((*pre_o));
+    TORCH_CHECK(pre_o->sizes() == q.sizes(), "pre_o shape");
+    TORCH_CHECK(pre_lse->scalar_type() == at::kFloat && pre_lse->numel() == q.size(0) * Hq, "pre_lse [T, Hq]");
+    kb = kv_begin->data_ptr<int>();
+    po = pre_o->data_ptr();
+    pl = pre_lse->data_ptr<float>();
+  }
   const int rc = launch_paged_attention(
       q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
       q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
       block_table.size(1), work_seq.data_ptr<int>(), work_q0.data_ptr<int>(), work_seq.numel(), nw,
-      Hq, Hkv, D, (float)scale, stream());
+      Hq, Hkv, D, (float)scale, kb, po, pl, stream());
   TORCH_CHECK(rc == 0, "paged_attention: unsupported config (code ", rc, ")");
+}
+
+void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                      at::Tensor& out, at::Tensor& lse, const at::Tensor& pre_bt, int64_t pre_keys,
+                      int64_t pre_tokens, double scale) {
+  CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
+  CHECK_I32_TENSOR(pre_bt); CHECK_DEV(lse); CHECK_CONTIG(lse);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat, "lse f32");
+  const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
+  TORCH_CHECK(out.sizes() == q.sizes() && lse.numel() == q.size(0) * Hq, "prefix attention shapes");
+  TORCH_CHECK(pre_tokens <= q.size(0) && pre_bt.numel() * 64 >= pre_keys, "prefix ranges");
+  const int rc = launch_prefix_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                         out.data_ptr(), lse.data_ptr<float>(),
+                                         pre_bt.data_ptr<int>(), pre_keys, pre_tokens, Hq, Hkv, D,
+                                         (float)scale, stream());
+  TORCH_CHECK(rc == 0, "prefix_attention: unsupported config (code ", rc, ")");
 }
 
 void sample_allowed(const at::Tensor& hidden, const at::Tensor& W, const at::Tensor& allow_ptr,
@@ -205,7 +237,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("l2norm_rows", &l2norm_rows);
   m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),
         py::arg("k"), py::arg("out_v"), py::arg("out_i"));
-  m.def("paged_attention", &paged_attention);
+  m.def("paged_attention", &paged_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("out"), py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"),
+        py::arg("block_table"), py::arg("work_seq"), py::arg("work_q0"), py::arg("nw"),
+        py::arg("scale"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
+        py::arg("pre_lse") = py::none());
+  m.def("prefix_attention", &prefix_attention);
   m.def("attn_tokens_per_item", &attn_tokens_per_item);
   m.def("sample_allowed", &sample_allowed, py::arg("hidden"), py::arg("W"), py::arg("allow_ptr"),
         py::arg("allow_ids"), py::arg("ctr"), py::arg("temperature"), py::arg("seed"),

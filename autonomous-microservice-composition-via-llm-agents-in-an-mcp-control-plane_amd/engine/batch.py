@@ -31,6 +31,11 @@ class AttnMeta:
     ctx_len: torch.Tensor      # [S]
     block_table: torch.Tensor  # [S, max_blocks]
     work: List[tuple]          # [(nw, work_seq[int32], work_q0[int32]), ...]
+    # cascade attention over one shared prefix (None when unused):
+    kv_begin: Optional[torch.Tensor] = None   # [S] first key each sequence attends itself
+    pre_bt: Optional[torch.Tensor] = None     # block ids of the shared prefix
+    pre_keys: int = 0                         # shared prefix keys (multiple of 64)
+    pre_tokens: int = 0                       # flat tokens [0, pre_tokens) attend to it
 
     def work_lists(self):
         return self.work
@@ -65,6 +70,9 @@ class StepInputs:
     ctx_len: np.ndarray        # [S]
     block_table: np.ndarray    # [S, max_blocks]
     logit_rows: np.ndarray     # [R] token row whose hidden feeds sampling
+    kv_begin: Optional[np.ndarray] = None   # [S] cascade: first own key per sequence
+    pre_bt: Optional[np.ndarray] = None     # cascade: shared prefix blocks
+    pre_tokens: int = 0                     # cascade: leading flat tokens that share it
 
     @property
     def num_tokens(self) -> int:
@@ -90,7 +98,11 @@ def pack_host(step: StepInputs, group: int, copies=()):
     for nw in (1, 4):
         parts += [np.asarray(work[nw][0], np.int32), np.asarray(work[nw][1], np.int32)]
     parts += [cp[:, 0].copy(), cp[:, 1].copy()]
-    layout = [int(p.size) for p in parts] + [int(step.q_len.shape[0])]
+    S = int(step.q_len.shape[0])
+    cascade = step.pre_bt is not None and step.pre_tokens > 0 and len(step.pre_bt) > 0
+    parts += [step.kv_begin if cascade else np.zeros(0, np.int32),
+              np.asarray(step.pre_bt, np.int32) if cascade else np.zeros(0, np.int32)]
+    layout = [int(p.size) for p in parts] + [S, int(step.pre_tokens) if cascade else 0]
     host = np.concatenate([np.asarray(p, dtype=np.int32).reshape(-1) for p in parts]) \
         if sum(layout[:-1]) else np.zeros(0, np.int32)
     return host, layout
@@ -108,7 +120,7 @@ def to_device(host: np.ndarray, device, pin: bool = True) -> torch.Tensor:
 def views(t: torch.Tensor, layout):
     """Inverse of ``pack_host`` on an (already transferred) int32 tensor.
     Returns (DeviceStep, copy_src, copy_dst)."""
-    sizes, S = layout[:-1], layout[-1]
+    sizes, S, pre_tokens = layout[:-2], layout[-2], layout[-1]
     vs, off = [], 0
     for n in sizes:
         vs.append(t[off:off + n])
@@ -120,6 +132,9 @@ def views(t: torch.Tensor, layout):
         if ws.numel():
             work_l.append((nw, ws, wq))
     meta = AttnMeta(q_start=vs[4], q_len=vs[5], ctx_len=vs[6], block_table=bt, work=work_l)
+    if pre_tokens > 0:
+        meta.kv_begin, meta.pre_bt = vs[14], vs[15]
+        meta.pre_keys, meta.pre_tokens = int(vs[15].numel()) * BLOCK_SIZE, pre_tokens
     return DeviceStep(token_ids=vs[0], positions=vs[1], slots=vs[2], logit_rows=vs[3],
                       attn=meta), vs[12], vs[13]
 

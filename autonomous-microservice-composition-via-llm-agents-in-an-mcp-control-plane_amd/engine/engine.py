@@ -75,11 +75,12 @@ class Sequence:
 class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
-                 seed: int = 0, bcast=None):
+                 seed: int = 0, bcast=None, cascade: bool = True):
         self.model = model
         cfg = model.cfg
         self.device = model.device
         self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
+        self.cascade = cascade      # shared-prefix (cascade) attention
         if num_blocks is not None:
             self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
         else:
@@ -95,7 +96,8 @@ class LLMEngine:
         self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
         self.max_prefixes = 64
         self.steps = 0
-        self.stats = {"tokens": 0, "samples": 0, "forward_s": 0.0, "steps": 0}
+        self.stats = {"tokens": 0, "samples": 0, "forward_s": 0.0, "steps": 0,
+                      "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
     def get_prefix(self, tokens: Seq[int]) -> Optional[PrefixEntry]:
@@ -186,6 +188,7 @@ class LLMEngine:
 
     def step(self) -> int:
         """One forward over the runnable batch.  Returns tokens processed."""
+        t_sched = time.perf_counter()
         self._admit()
         if not self.running:
             return 0
@@ -199,7 +202,25 @@ class LLMEngine:
         logit_rows, sample_seqs = [], []
         batch_seqs = []
         T = 0
-        for seq in self.running:
+        # cascade: requests that share the most common computed prefix go first,
+        # so their tokens form the leading range [0, pre_tokens) of the batch
+        casc = None
+        if self.cascade:
+            counts = {}
+            for seq in self.running:
+                e = seq.prefix
+                if e is not None and seq.materialized and seq.pending and e.length >= BLOCK_SIZE:
+                    counts[id(e)] = counts.get(id(e), 0) + 1
+            if counts:
+                best = max(counts, key=counts.get)
+                casc = next(q.prefix for q in self.running if q.prefix is not None and id(q.prefix) == best)
+        order = self.running
+        if casc is not None:
+            order = [q for q in self.running if q.prefix is casc and q.materialized] + \
+                    [q for q in self.running if not (q.prefix is casc and q.materialized)]
+        pre_tokens, kv_begin = 0, []
+        casc_keys = (casc.length // BLOCK_SIZE) * BLOCK_SIZE if casc is not None else 0
+        for seq in order:
             if not seq.materialized:           # waiting for its prefix job
                 continue
             n = len(seq.pending)
@@ -220,6 +241,11 @@ class LLMEngine:
             pos.append(p)
             blk = np.asarray(seq.blocks, dtype=np.int32)
             slots.append(blk[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE)
+            if casc is not None and seq.prefix is casc and seq.materialized:
+                pre_tokens = T + take
+                kv_begin.append(casc_keys)
+            else:
+                kv_begin.append(0)
             T += take
             batch_seqs.append((seq, take))
             if take == n and seq.wants_sample:
@@ -239,10 +265,19 @@ class LLMEngine:
                           q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
                           ctx_len=np.asarray(ctx_len, np.int32), block_table=bt,
                           logit_rows=np.asarray(logit_rows, np.int32))
+        if pre_tokens > 0:
+            step.kv_begin = np.asarray(kv_begin, np.int32)
+            step.pre_bt = np.asarray(casc.blocks[:casc_keys // BLOCK_SIZE], np.int32)
+            step.pre_tokens = pre_tokens
         t0 = time.perf_counter()
+        self.stats["schedule_s"] += t0 - t_sched
         hidden = self._launch(step, copies)
+        t1 = time.perf_counter()
         new_tokens = self._sample(hidden, sample_seqs)
-        self.stats["forward_s"] += time.perf_counter() - t0
+        t2 = time.perf_counter()
+        self.stats["launch_s"] += t1 - t0
+        self.stats["sample_s"] += t2 - t1
+        self.stats["forward_s"] += t2 - t0
         self.stats["tokens"] += T
         self.stats["steps"] += 1
         self.steps += 1
@@ -262,6 +297,7 @@ class LLMEngine:
             if not seq.is_prefix_job and seq.decoder.done and not seq.done:
                 self._finish(seq)
         self.running = [s for s in self.running if not s.done]
+        self.stats["update_s"] += time.perf_counter() - t2
         METRICS.set("batch_occupancy", len(self.running))
         METRICS.set("kv_block_utilization", self.alloc.utilization())
         return T

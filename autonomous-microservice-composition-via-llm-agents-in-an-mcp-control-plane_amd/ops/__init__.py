@@ -118,9 +118,18 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
     if q.is_cuda:
         out = torch.empty_like(q) if out is None else out
         L = lib()
+        kw = {}
+        if meta.pre_tokens > 0:
+            # cascade: all requests' query tokens vs the shared prefix K/V in full
+            # MFMA tiles, then each request's own keys + LSE merge (csrc/attention.hip)
+            pre_o = torch.empty_like(q)
+            pre_lse = torch.empty(q.shape[0], q.shape[1], device=q.device, dtype=torch.float32)
+            L.prefix_attention(q, k_cache, v_cache, pre_o, pre_lse, meta.pre_bt, meta.pre_keys,
+                               meta.pre_tokens, scale)
+            kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         for nw, ws, wq in meta.work_lists():
             L.paged_attention(q, k_cache, v_cache, out, meta.q_start, meta.q_len, meta.ctx_len,
-                              meta.block_table, ws, wq, nw, scale)
+                              meta.block_table, ws, wq, nw, scale, **kw)
         return out
     r = ref.paged_attention(q, k_cache, v_cache, meta.q_start, meta.q_len, meta.ctx_len,
                             meta.block_table, scale)

@@ -110,6 +110,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    st = engine.stats
+    log(f"[rank {rank}] engine totals: " + ", ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}"
+                                                  for k, v in st.items()))
     # per-request latencies were recorded by the engine's sequences via METRICS
     from mcp_amd.utils.metrics import METRICS
     w = METRICS.windows["plan_latency_s"]

@@ -220,3 +220,44 @@ def test_topk_cosine(B, N, D, k):
     got = ref_s.gather(1, idx.long())
     assert torch.allclose(got, rv, atol=1e-4)
     assert (vals[:, :-1] >= vals[:, 1:]).all()
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
+def test_cascade_prefix_attention(Hq, Hkv):
+    """Shared-prefix pass + per-sequence pass with LSE merge == full attention."""
+    torch.manual_seed(5)
+    D, BS = 128, 64
+    P_full = 640                                   # 10 shared blocks
+    q_lens = [1, 5, 17, 2, 40]
+    own_keys = [70, 5, 130, 64, 300]               # keys after the shared prefix
+    ctx = [P_full + k for k in own_keys]
+    n_pre = P_full // BS
+    own_blocks = [(k + BS - 1) // BS for k in own_keys]
+    nb = n_pre + sum(own_blocks) + 2
+    kc, vc = _cache(nb, Hkv)
+    pre = list(range(n_pre))
+    o = n_pre
+    tables = []
+    for nbk in own_blocks:
+        tables.append(pre + list(range(o, o + nbk)))
+        o += nbk
+    maxb = max(len(t) for t in tables)
+    bt = np.zeros((len(q_lens), maxb), np.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = t
+    T = sum(q_lens)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    qs = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    step = StepInputs(token_ids=np.zeros(T, np.int32), positions=np.zeros(T, np.int32),
+                      slots=np.zeros(T, np.int32), q_start=qs,
+                      q_len=np.asarray(q_lens, np.int32), ctx_len=np.asarray(ctx, np.int32),
+                      block_table=bt, logit_rows=np.zeros(0, np.int32),
+                      kv_begin=np.full(len(q_lens), P_full, np.int32),
+                      pre_bt=np.asarray(pre, np.int32), pre_tokens=T)
+    dev = pack(step, Hq // Hkv, DEV)
+    assert dev.attn.pre_tokens == T and dev.attn.pre_keys == P_full
+    out = ops.paged_attention(q, kc, vc, dev.attn, 1 / math.sqrt(D)).cpu()
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), torch.from_numpy(qs),
+                              torch.tensor(q_lens), torch.tensor(ctx), torch.from_numpy(bt),
+                              1 / math.sqrt(D))
+    assert rel_err(out, exp) < 2e-2
