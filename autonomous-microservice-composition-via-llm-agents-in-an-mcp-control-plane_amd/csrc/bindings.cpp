@@ -87,6 +87,16 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
   launch_gemm_tn_algo(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, (int)algo, stream());
 }
 
+void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
+  const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && N % 64 == 0, "gemm_silu: W [N, K], N % 64 == 0");
+  TORCH_CHECK(Y.numel() == (int64_t)M * (N / 2), "gemm_silu: Y [M, N/2]");
+  TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_silu: unsupported shape");
+  TORCH_CHECK(launch_gemm_silu(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, stream()) == 0,
+              "gemm_silu failed");
+}
+
 void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64_t v) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
   const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
@@ -233,6 +243,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("algo") = -1);
   m.def("gemm_select", &gemm_select);
   m.def("gemm_variant", &gemm_variant);
+  m.def("gemm_silu", &gemm_silu);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),

@@ -1,5 +1,8 @@
 // K1/K2: bf16 "TN" GEMM on MFMA for every Llama projection.
-//   Y[M,N] = X[M,K] · W[N,K]^T   (+ R[M,N] when RESID: fused residual add)
+//   Y[M,N] = X[M,K] · W[N,K]^T   epilogues: plain, + R[M,N] (residual add),
+//   or SwiGLU: W rows interleaved [gate 16 | up 16] per 32-row group, so each
+//   lane's adjacent 16-column tiles hold gate and up of the same 4 features and
+//   Y[M, N/2] = silu(gate) * up is written directly (no [M, N] intermediate).
 // X = activations (row-major, K contiguous), W = nn.Linear weight (out x in,
 // K contiguous), fp32 accumulation, bf16 out.
 //
@@ -22,7 +25,7 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_ELEMS = 128 * BK;          // one operand tile, bf16 elements (16 KiB)
 
-template <bool RESID, typename OutT = bf16>
+template <int EPI, typename OutT = bf16>     // EPI: 0 plain, 1 +residual, 2 SwiGLU
 __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X,
                                                       const bf16* __restrict__ W,
                                                       OutT* __restrict__ Y,
@@ -108,12 +111,26 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
   for (int mt = 0; mt < 4; ++mt) {
     const int m = m0 + wm * 64 + mt * 16 + fr;
     if (m >= M) continue;
+    if constexpr (EPI == 2) {
+      const int F = N >> 1;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int f = ((n0 + wn * 64) >> 1) + p * 16 + fq * 4;
+        if (f >= F) continue;
+        const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
+        *reinterpret_cast<bf16x4*>((bf16*)Y + (size_t)m * F + f) = o;
+      }
+      continue;
+    }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int n = n0 + wn * 64 + nt * 16 + fq * 4;
       if (n >= N) continue;
       f32x4 v = acc[mt][nt];
-      if (RESID) {
+      if (EPI == 1) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
@@ -159,19 +176,19 @@ static void launch_gemm_tn_128(const void* X, const void* W, void* Y, const void
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   const dim3 grid(nm * nn);
   if (R)
-    gemm_tn_128<true><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                           (const bf16*)R, M, N, K);
+    gemm_tn_128<1><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                        (const bf16*)R, M, N, K);
   else
-    gemm_tn_128<false><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M,
-                                            N, K);
+    gemm_tn_128<0><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N,
+                                        K);
 }
 
 // fp32-output variant (retrieval scores: bf16 would tie near-equal cosines)
 void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N, int K,
                            hipStream_t s) {
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  gemm_tn_128<false, float><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, Y,
-                                                          nullptr, M, N, K);
+  gemm_tn_128<0, float><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, Y,
+                                                      nullptr, M, N, K);
 }
 
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
@@ -187,4 +204,19 @@ void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, i
   if (algo < 0) launch_gemm_tn(X, W, Y, R, M, N, K, s);
   else if (algo == 1) launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
   else launch_gemm_tn_128(X, W, Y, R, M, N, K, s);
+}
+
+// SwiGLU-fused projection: W rows interleaved [gate 16 | up 16]; Y is [M, N/2]
+void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N, int K,
+                             hipStream_t s);
+int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
+  if (N % 64) return 1;
+  if (gemm_select(M, N, K) == 1) {
+    launch_gemm_tn_256_silu(X, W, Y, M, N, K, s);
+  } else {
+    const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+    gemm_tn_128<2><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                 nullptr, M, N, K);
+  }
+  return 0;
 }

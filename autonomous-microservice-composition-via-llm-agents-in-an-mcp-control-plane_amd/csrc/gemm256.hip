@@ -51,7 +51,7 @@ struct V256 {
 };
 using V256Default = V256<false, false, false, true>;   // variant 8: best of the 16-way sweep
 
-template <bool RESID, class VAR = V256Default>
+template <int EPI, class VAR = V256Default>   // EPI: 0 plain, 1 +residual, 2 SwiGLU
 __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X,
                                                       const bf16* __restrict__ W,
                                                       bf16* __restrict__ Y,
@@ -181,12 +181,26 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
     for (int mt = 0; mt < 4; ++mt) {
       const int m = m0 + wm * 128 + mh * 64 + mt * 16 + fr;
       if (m >= M) continue;
+      if constexpr (EPI == 2) {
+        const int F = N >> 1;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int f = ((n0 + wn * 64) >> 1) + p * 16 + fq * 4;
+          if (f >= F) continue;
+          const f32x4 gv = acc[mh][mt][2 * p], uv = acc[mh][mt][2 * p + 1];
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
+          *reinterpret_cast<bf16x4*>(Y + (size_t)m * F + f) = o;
+        }
+        continue;
+      }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int n = n0 + wn * 64 + nt * 16 + fq * 4;
         if (n >= N) continue;
         f32x4 v = acc[mh][mt][nt];
-        if (RESID) {
+        if (EPI == 1) {
           const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
@@ -202,8 +216,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
 template <class VAR>
 void launch_var(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  gemm_tn_256<false, VAR><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                        nullptr, M, N, K);
+  gemm_tn_256<0, VAR><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                    nullptr, M, N, K);
 }
 
 }  // namespace
@@ -240,11 +254,18 @@ void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, in
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   const dim3 grid(nm * nn);
   if (R)
-    gemm_tn_256<true><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                           (const bf16*)R, M, N, K);
+    gemm_tn_256<1><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                        (const bf16*)R, M, N, K);
   else
-    gemm_tn_256<false><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M,
-                                            N, K);
+    gemm_tn_256<0><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N,
+                                        K);
+}
+
+void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N, int K,
+                             hipStream_t s) {
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  gemm_tn_256<2><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr,
+                                               M, N, K);
 }
 
 // ============================================================================

@@ -27,6 +27,8 @@ void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, in
                         hipStream_t s);
 // algo: -1 auto, 0 = 128x128 two-barrier kernel, 1 = 256x256 multi-phase kernel
 int gemm_select(int M, int N, int K);
+// Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]
+int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
                                hipStream_t s);
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,

@@ -15,7 +15,7 @@ kernel from ``ops`` on GPU:
                 a = paged_attention(q, K, V)         K5/K6
                 x = x + a Wo^T      (residual fused in the GEMM epilogue)
                 [all-reduce over TP ranks]           C1 (RCCL / xGMI)
-                h = rmsnorm(x); g = silu(h Wg^T) * (h Wu^T)   K1 + K7
+                h = rmsnorm(x); g = silu(h Wg^T) * (h Wu^T)   K1 with K7 fused
                 x = x + g Wd^T      (fused residual) [all-reduce]  C2
     h_last = rmsnorm(x[rows that need a token])
 
@@ -86,7 +86,7 @@ class LayerWeights:
     wqkv: torch.Tensor        # [(Hq + 2 Hkv) * D / tp, H]
     wo: torch.Tensor          # [H, Hq * D / tp]
     mlp_norm: torch.Tensor
-    w_gate_up: torch.Tensor   # [2 F / tp, H]  (gate rows | up rows)
+    w_gate_up: torch.Tensor   # [2 F / tp, H]  gate/up rows interleaved in 16-row groups
     w_down: torch.Tensor      # [H, F / tp]
 
 
@@ -113,10 +113,11 @@ def shard_layer(full: LayerWeights, cfg: LlamaConfig, rank: int, tp: int) -> Lay
     D = cfg.head_dim
     q, k, v = torch.split(full.wqkv, [cfg.heads * D, cfg.kv_heads * D, cfg.kv_heads * D])
     wqkv = torch.cat([shard_rows(q, rank, tp), shard_rows(k, rank, tp), shard_rows(v, rank, tp)])
-    g, u = torch.split(full.w_gate_up, [cfg.ffn, cfg.ffn])
+    g, u = ref.deinterleave_gate_up(full.w_gate_up)
     return LayerWeights(attn_norm=full.attn_norm, wqkv=wqkv.contiguous(),
                         wo=shard_cols(full.wo, rank, tp), mlp_norm=full.mlp_norm,
-                        w_gate_up=torch.cat([shard_rows(g, rank, tp), shard_rows(u, rank, tp)]).contiguous(),
+                        w_gate_up=ref.interleave_gate_up(shard_rows(g, rank, tp),
+                                                         shard_rows(u, rank, tp)).contiguous(),
                         w_down=shard_cols(full.w_down, rank, tp))
 
 
@@ -207,7 +208,7 @@ class LlamaModel:
             a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
             x = self._residual_gemm(a.view(T, self.hq * D), lw.wo, x)
             h = ops.rmsnorm(x, lw.mlp_norm, cfg.eps)
-            act = ops.silu_mul(ops.gemm(h, lw.w_gate_up))
+            act = ops.gemm_silu(h, lw.w_gate_up)          # SwiGLU fused in the epilogue
             x = self._residual_gemm(act, lw.w_down, x)
             if l + 1 < L:
                 h = ops.rmsnorm(x, self.w.layers[l + 1].attn_norm, cfg.eps)

@@ -104,6 +104,17 @@ def gemm(X, W, R=None, out=None, algo: int = -1):
     return r if out is None else out.copy_(r)
 
 
+def gemm_silu(X, W, out=None):
+    """SwiGLU projection: silu(X Wg^T) * (X Wu^T) with W = interleave_gate_up(Wg, Wu)
+    ([2F, K], 16-row groups); the activation is fused into the MFMA GEMM epilogue."""
+    if X.is_cuda:
+        out = X.new_empty(*X.shape[:-1], W.shape[0] // 2) if out is None else out
+        lib().gemm_silu(X, W, out)
+        return out
+    r = ref.gemm_silu(X, W)
+    return r if out is None else out.copy_(r)
+
+
 def rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D):
     if qkv.is_cuda:
         lib().rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)

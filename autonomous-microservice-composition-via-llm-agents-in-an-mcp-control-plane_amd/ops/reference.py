@@ -30,6 +30,30 @@ def silu_mul(x: torch.Tensor) -> torch.Tensor:
     return (torch.nn.functional.silu(g) * u).to(x.dtype)
 
 
+GU_GROUP = 16   # gate/up row interleave granularity of the fused SwiGLU GEMM
+
+
+def interleave_gate_up(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """[F, H] gate + [F, H] up -> [2F, H] rows [g0..g15, u0..u15, g16..g31, ...]."""
+    F, H = g.shape
+    return torch.stack([g.view(F // GU_GROUP, GU_GROUP, H), u.view(F // GU_GROUP, GU_GROUP, H)],
+                       dim=1).reshape(2 * F, H)
+
+
+def deinterleave_gate_up(w: torch.Tensor):
+    F2, H = w.shape
+    v = w.view(F2 // (2 * GU_GROUP), 2, GU_GROUP, H)
+    return v[:, 0].reshape(F2 // 2, H), v[:, 1].reshape(F2 // 2, H)
+
+
+def gemm_silu(X, W_interleaved):
+    y = (X.float() @ W_interleaved.float().t())
+    T, F2 = y.shape
+    y = y.view(T, F2 // (2 * GU_GROUP), 2, GU_GROUP)
+    g, u = y[:, :, 0], y[:, :, 1]
+    return (torch.nn.functional.silu(g) * u).reshape(T, F2 // 2).to(X.dtype)
+
+
 def gemm(X, W, R: Optional[torch.Tensor] = None):
     y = X.float() @ W.float().t()
     if R is not None:

@@ -69,10 +69,13 @@ class GrammarSpec:
     """Per-plan constants: candidate services, their token tries, caches."""
 
     def __init__(self, services: Sequence[dict], tokenizer, max_nodes: int = 6,
-                 allow_retries: bool = True):
+                 allow_retries: bool = True, min_nodes: int = 1):
         self.services = list(services)
         self.tok = tokenizer
         self.max_nodes = max(1, max_nodes)
+        # the model decides when to stop only between min_nodes and max_nodes
+        # (a fixed-size plan gives the benchmark a model-independent token count)
+        self.min_nodes = max(1, min(min_nodes, self.max_nodes, len(self.services)))
         self.allow_retries = allow_retries
         self.names = [s["name"] for s in self.services]
         self.keys = [self._input_keys(s) for s in self.services]
@@ -158,6 +161,9 @@ class DagDecoder:
             can_more = len(chosen) < sp.max_nodes and used_mask != (1 << len(sp.names)) - 1
             if not can_more:
                 break
+            if len(chosen) < sp.min_nodes:
+                yield (',{"name":', None)
+                continue
             alts_c = (',{"name":', '],"edges":[')
             ci = yield (None, (alts_c, sp.trie(alts_c), 3))
             if ci == 1:

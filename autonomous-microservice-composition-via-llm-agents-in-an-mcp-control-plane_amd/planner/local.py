@@ -33,11 +33,12 @@ from .tokenizer import get_tokenizer
 
 class LocalPlanner(Planner):
     def __init__(self, engine, registry, tokenizer=None, max_nodes: int = 6, retriever=None,
-                 retrieval_threshold: int = 48, topk: int = 32):
+                 retrieval_threshold: int = 48, topk: int = 32, min_nodes: int = 1):
         self.engine = engine
         self.registry = registry
         self.tok = tokenizer or get_tokenizer()
         self.max_nodes = max_nodes
+        self.min_nodes = min_nodes
         self.retriever = retriever
         self.retrieval_threshold = retrieval_threshold
         self.topk = topk
@@ -76,7 +77,7 @@ class LocalPlanner(Planner):
         key = tuple(s["name"] for s in cands) + (getattr(self.registry, "version", 0),)
         spec = self._spec_cache.get(key)
         if spec is None:
-            spec = GrammarSpec(cands, self.tok, max_nodes=self.max_nodes)
+            spec = GrammarSpec(cands, self.tok, max_nodes=self.max_nodes, min_nodes=self.min_nodes)
             if len(self._spec_cache) > 256:
                 self._spec_cache.clear()
             self._spec_cache[key] = spec

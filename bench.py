@@ -53,7 +53,10 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="concurrent intents per GPU per step")
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--services", type=int, default=10)
-    ap.add_argument("--max-nodes", type=int, default=6)
+    ap.add_argument("--min-nodes", type=int, default=5,
+                    help="plans have between min and max nodes; min == max fixes the DAG size so "
+                         "the work per plan does not depend on the random weights' choices")
+    ap.add_argument("--max-nodes", type=int, default=5)
     ap.add_argument("--max-step-tokens", type=int, default=16384)
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
@@ -76,7 +79,7 @@ def main():
     log(f"[rank {rank}] KV cache: {engine.kv.num_blocks} blocks x 64 tokens "
         f"({engine.kv.data.numel() * 2 / 1e9:.1f} GB)")
     reg = MemoryRegistry(synthetic_registry(args.services, seed=1))
-    planner = LocalPlanner(engine, reg, max_nodes=args.max_nodes)
+    planner = LocalPlanner(engine, reg, max_nodes=args.max_nodes, min_nodes=args.min_nodes)
     names = [s.name for s in reg.list_services()]
 
     def one_step(step_idx):
@@ -150,7 +153,8 @@ def main():
             "tokens_per_s": round(tokens_total / (ms_per_step * args.steps / 1e3), 1),
             "config": {"model": args.model, "global_batch": args.batch * world,
                        "seq_len": None, "parallelism": f"dp{world}", "tp": 1,
-                       "services": args.services, "max_nodes": args.max_nodes,
+                       "services": args.services, "nodes_per_plan": [args.min_nodes, args.max_nodes],
+                       "tokens_per_plan": round(tokens_total / plans_total, 1),
                        "temperature": 0.2},
         }), flush=True)
     if world > 1:

@@ -261,3 +261,15 @@ def test_cascade_prefix_attention(Hq, Hkv):
                               torch.tensor(q_lens), torch.tensor(ctx), torch.from_numpy(bt),
                               1 / math.sqrt(D))
     assert rel_err(out, exp) < 2e-2
+
+
+@pytest.mark.parametrize("M,F,K", [(7, 512, 256), (300, 1792, 4096), (3000, 14336, 4096), (520, 3584, 1024)])
+def test_gemm_silu_fused(M, F, K):
+    torch.manual_seed(3)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    g = (torch.randn(F, K, device=DEV) / math.sqrt(K)).bfloat16()
+    u = (torch.randn(F, K, device=DEV) / math.sqrt(K)).bfloat16()
+    W = ref.interleave_gate_up(g, u).contiguous()
+    y = ops.gemm_silu(X, W)
+    exp = (torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t()))
+    assert rel_err(y, exp) < 2e-2

@@ -146,3 +146,13 @@ def test_retrieval_cpu_prunes_prompt():
     assert any("payment" in s.name or "charge" in s.name for s in got)
     e = hash_embed(["a b c", "a b c"], 64)
     assert np.allclose(e[0], e[1]) and abs(np.linalg.norm(e[0]) - 1) < 1e-5
+
+
+def test_gate_up_interleave_roundtrip():
+    from mcp_amd.ops import reference as ref
+    g, u = torch.randn(64, 8), torch.randn(64, 8)
+    w = ref.interleave_gate_up(g, u)
+    g2, u2 = ref.deinterleave_gate_up(w)
+    assert torch.equal(g, g2) and torch.equal(u, u2)
+    X = torch.randn(3, 8)
+    assert torch.allclose(ref.gemm_silu(X, w), torch.nn.functional.silu(X @ g.t()) * (X @ u.t()), atol=1e-5)
