@@ -194,14 +194,14 @@ void sample_allowed(const at::Tensor& hidden, const at::Tensor& W, const at::Ten
                     int64_t seed, at::Tensor& out_tok, const c10::optional<at::Tensor>& out_logit) {
   CHECK_BF16_TENSOR(hidden); CHECK_BF16_TENSOR(W);
   CHECK_I32_TENSOR(allow_ptr); CHECK_I32_TENSOR(allow_ids); CHECK_I32_TENSOR(out_tok);
-  CHECK_DEV(ctr); TORCH_CHECK(ctr.scalar_type() == at::kLong, "ctr int64");
+  CHECK_I32_TENSOR(ctr);
   const int S = hidden.size(0), H = hidden.size(1);
   TORCH_CHECK(W.size(1) == H && H % 8 == 0, "W [V, H]");
   TORCH_CHECK(allow_ptr.numel() == S + 1 && out_tok.numel() == S && ctr.numel() == S, "sample shapes");
   float* lp = nullptr;
   if (out_logit.has_value()) lp = out_logit->data_ptr<float>();
   launch_sample_allowed(hidden.data_ptr(), W.data_ptr(), allow_ptr.data_ptr<int>(),
-                        allow_ids.data_ptr<int>(), (const long long*)ctr.data_ptr<int64_t>(),
+                        allow_ids.data_ptr<int>(), ctr.data_ptr<int>(),
                         (float)temperature, (unsigned long long)seed, S, H,
                         out_tok.data_ptr<int>(), lp, stream());
 }
@@ -209,9 +209,9 @@ void sample_allowed(const at::Tensor& hidden, const at::Tensor& W, const at::Ten
 void sample_dense(const at::Tensor& logits, const at::Tensor& ctr, double temperature,
                   int64_t seed, at::Tensor& out_tok) {
   CHECK_BF16_TENSOR(logits); CHECK_I32_TENSOR(out_tok);
-  TORCH_CHECK(ctr.scalar_type() == at::kLong, "ctr int64");
+  CHECK_I32_TENSOR(ctr);
   launch_sample_dense(logits.data_ptr(), logits.size(0), logits.size(1),
-                      (const long long*)ctr.data_ptr<int64_t>(), (float)temperature,
+                      ctr.data_ptr<int>(), (float)temperature,
                       (unsigned long long)seed, out_tok.data_ptr<int>(), stream());
 }
 

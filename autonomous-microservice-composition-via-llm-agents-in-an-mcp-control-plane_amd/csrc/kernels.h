@@ -55,8 +55,8 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
 
 // sampling.hip
 void launch_sample_allowed(const void* hidden, const void* W, const int* allow_ptr,
-                           const int* allow_ids, const long long* ctr, float temperature,
+                           const int* allow_ids, const int* ctr, float temperature,
                            unsigned long long seed, int S, int H, int* out_tok, float* out_logit,
                            hipStream_t s);
-void launch_sample_dense(const void* logits, int S, int V, const long long* ctr, float temperature,
+void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float temperature,
                          unsigned long long seed, int* out_tok, hipStream_t s);

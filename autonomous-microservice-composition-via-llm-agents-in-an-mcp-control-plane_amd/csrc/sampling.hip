@@ -13,7 +13,7 @@
 
 __global__ __launch_bounds__(256) void sample_allowed_kernel(
     const bf16* __restrict__ hidden, const bf16* __restrict__ W, const int* __restrict__ allow_ptr,
-    const int* __restrict__ allow_ids, const long long* __restrict__ ctr, float inv_temp,
+    const int* __restrict__ allow_ids, const int* __restrict__ ctr, float inv_temp,
     unsigned long long seed, int H, int* __restrict__ out_tok, float* __restrict__ out_logit) {
   const int s = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void sample_allowed_kernel(
     acc = wave_sum(acc);
     float score = acc;
     if (inv_temp > 0.f) {
-      const float u = uniform01(seed, (unsigned long long)ctr[s], (unsigned long long)tok);
+      const float u = uniform01(seed, (unsigned long long)(unsigned)ctr[s], (unsigned long long)tok);
       score = acc * inv_temp - __logf(-__logf(u));
     }
     if (score > best) {
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void sample_allowed_kernel(
 }
 
 void launch_sample_allowed(const void* hidden, const void* W, const int* allow_ptr,
-                           const int* allow_ids, const long long* ctr, float temperature,
+                           const int* allow_ids, const int* ctr, float temperature,
                            unsigned long long seed, int S, int H, int* out_tok, float* out_logit,
                            hipStream_t s) {
   if (S <= 0) return;
@@ -74,7 +74,7 @@ void launch_sample_allowed(const void* hidden, const void* W, const int* allow_p
 // Dense variant: logits [S, V] (fp32 or bf16 via the GEMM), optional -inf mask
 // folded in by the caller.  One block per row, Gumbel-max over the full vocab.
 __global__ __launch_bounds__(256) void sample_dense_kernel(const bf16* __restrict__ logits, int V,
-                                                           const long long* __restrict__ ctr,
+                                                           const int* __restrict__ ctr,
                                                            float inv_temp,
                                                            unsigned long long seed,
                                                            int* __restrict__ out_tok) {
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void sample_dense_kernel(const bf16* __restric
   for (int i = threadIdx.x; i < V; i += 256) {
     const float l = (float)row[i];
     float sc = l;
-    if (inv_temp > 0.f) sc = l * inv_temp - __logf(-__logf(uniform01(seed, (unsigned long long)ctr[s], (unsigned long long)i)));
+    if (inv_temp > 0.f) sc = l * inv_temp - __logf(-__logf(uniform01(seed, (unsigned long long)(unsigned)ctr[s], (unsigned long long)i)));
     if (sc > best) { best = sc; bt = i; }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void sample_dense_kernel(const bf16* __restric
   }
 }
 
-void launch_sample_dense(const void* logits, int S, int V, const long long* ctr, float temperature,
+void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float temperature,
                          unsigned long long seed, int* out_tok, hipStream_t s) {
   if (S <= 0) return;
   const float inv_t = temperature > 0.f ? 1.f / temperature : 0.f;

@@ -73,6 +73,9 @@ class StepInputs:
     kv_begin: Optional[np.ndarray] = None   # [S] cascade: first own key per sequence
     pre_bt: Optional[np.ndarray] = None     # cascade: shared prefix blocks
     pre_tokens: int = 0                     # cascade: leading flat tokens that share it
+    allow_ptr: Optional[np.ndarray] = None  # [R+1] sampling: CSR of grammar-allowed tokens
+    allow_ids: Optional[np.ndarray] = None  # [A]
+    sample_ctr: Optional[np.ndarray] = None  # [R] RNG counters
 
     @property
     def num_tokens(self) -> int:
@@ -86,6 +89,9 @@ class DeviceStep:
     slots: torch.Tensor
     logit_rows: torch.Tensor
     attn: AttnMeta
+    allow_ptr: Optional[torch.Tensor] = None
+    allow_ids: Optional[torch.Tensor] = None
+    sample_ctr: Optional[torch.Tensor] = None
 
 
 def pack_host(step: StepInputs, group: int, copies=()):
@@ -102,10 +108,48 @@ def pack_host(step: StepInputs, group: int, copies=()):
     cascade = step.pre_bt is not None and step.pre_tokens > 0 and len(step.pre_bt) > 0
     parts += [step.kv_begin if cascade else np.zeros(0, np.int32),
               np.asarray(step.pre_bt, np.int32) if cascade else np.zeros(0, np.int32)]
+    z = np.zeros(0, np.int32)
+    parts += [step.allow_ptr if step.allow_ptr is not None else z,
+              step.allow_ids if step.allow_ids is not None else z,
+              step.sample_ctr if step.sample_ctr is not None else z]
     layout = [int(p.size) for p in parts] + [S, int(step.pre_tokens) if cascade else 0]
     host = np.concatenate([np.asarray(p, dtype=np.int32).reshape(-1) for p in parts]) \
         if sum(layout[:-1]) else np.zeros(0, np.int32)
     return host, layout
+
+
+class HostStager:
+    """Persistent pinned host staging for the per-step H2D copy.
+
+    Two pinned int32 buffers alternate; before one is reused the event recorded
+    after its last async copy is waited on (in steady state it completed long
+    ago, because every step synchronises on the sampled tokens)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device) if device is not None else None
+        self._buf = [None, None]
+        self._ev = [None, None]
+        self._i = 0
+
+    def to_device(self, host: np.ndarray) -> torch.Tensor:
+        if self.device is None or self.device.type != "cuda":
+            return torch.from_numpy(host)
+        i = self._i
+        self._i ^= 1
+        n = int(host.size)
+        b = self._buf[i]
+        if self._ev[i] is not None:
+            self._ev[i].synchronize()
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 2 * (b.numel() if b is not None else 4096)), dtype=torch.int32,
+                            pin_memory=True)
+            self._buf[i] = b
+        np.copyto(b.numpy()[:n], host)
+        d = b[:n].to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ev[i] = ev
+        return d
 
 
 def to_device(host: np.ndarray, device, pin: bool = True) -> torch.Tensor:
@@ -135,8 +179,9 @@ def views(t: torch.Tensor, layout):
     if pre_tokens > 0:
         meta.kv_begin, meta.pre_bt = vs[14], vs[15]
         meta.pre_keys, meta.pre_tokens = int(vs[15].numel()) * BLOCK_SIZE, pre_tokens
-    return DeviceStep(token_ids=vs[0], positions=vs[1], slots=vs[2], logit_rows=vs[3],
-                      attn=meta), vs[12], vs[13]
+    d = DeviceStep(token_ids=vs[0], positions=vs[1], slots=vs[2], logit_rows=vs[3], attn=meta)
+    d.allow_ptr, d.allow_ids, d.sample_ctr = vs[16], vs[17], vs[18]
+    return d, vs[12], vs[13]
 
 
 def pack(step: StepInputs, group: int, device, pin: bool = True) -> DeviceStep:

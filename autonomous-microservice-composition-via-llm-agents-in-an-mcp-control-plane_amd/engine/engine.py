@@ -31,7 +31,7 @@ import torch
 
 from .. import ops
 from ..utils.metrics import METRICS
-from .batch import BLOCK_SIZE, StepInputs, pack_host, to_device, views
+from .batch import BLOCK_SIZE, HostStager, StepInputs, pack_host, views
 from .kv_cache import KVCache
 
 _uid = itertools.count(1)
@@ -81,6 +81,7 @@ class LLMEngine:
         self.device = model.device
         self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
         self.cascade = cascade      # shared-prefix (cascade) attention
+        self.stager = HostStager(self.device)
         if num_blocks is not None:
             self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
         else:
@@ -265,15 +266,24 @@ class LLMEngine:
                           q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
                           ctx_len=np.asarray(ctx_len, np.int32), block_table=bt,
                           logit_rows=np.asarray(logit_rows, np.int32))
+        if sample_seqs:            # grammar masks go in the same single H2D copy
+            allowed = [q.decoder.allowed() for q in sample_seqs]
+            ptr = np.zeros(len(allowed) + 1, np.int32)
+            ptr[1:] = np.cumsum([len(a) for a in allowed])
+            step.allow_ptr = ptr
+            step.allow_ids = np.fromiter(itertools.chain.from_iterable(allowed), dtype=np.int32,
+                                         count=int(ptr[-1]))
+            step.sample_ctr = np.asarray([(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF
+                                          for q in sample_seqs], np.int32)
         if pre_tokens > 0:
             step.kv_begin = np.asarray(kv_begin, np.int32)
             step.pre_bt = np.asarray(casc.blocks[:casc_keys // BLOCK_SIZE], np.int32)
             step.pre_tokens = pre_tokens
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
-        hidden = self._launch(step, copies)
+        hidden, dstep = self._launch(step, copies)
         t1 = time.perf_counter()
-        new_tokens = self._sample(hidden, sample_seqs)
+        new_tokens = self._sample(hidden, dstep, len(sample_seqs))
         t2 = time.perf_counter()
         self.stats["launch_s"] += t1 - t0
         self.stats["sample_s"] += t2 - t1
@@ -302,7 +312,7 @@ class LLMEngine:
         METRICS.set("kv_block_utilization", self.alloc.utilization())
         return T
 
-    def _launch(self, step: Optional[StepInputs], copies) -> Optional[torch.Tensor]:
+    def _launch(self, step: Optional[StepInputs], copies):
         """Pack -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
         if step is None:
             empty = np.zeros(0, np.int32)
@@ -310,39 +320,28 @@ class LLMEngine:
                               q_len=empty, ctx_len=empty, block_table=np.zeros((0, 1), np.int32),
                               logit_rows=empty)
         host, layout = pack_host(step, self.model.cfg.group, copies)
-        payload = to_device(host, self.device)
+        payload = self.stager.to_device(host)
         if self.bcast is not None:
             self.bcast.send(payload, layout)
         dstep, csrc, cdst = views(payload, layout)
         if csrc.numel():
             ops.copy_blocks(self.kv.data, csrc, cdst)
         if dstep.token_ids.numel() == 0:
-            return None
-        return self.model.forward(dstep, self.kv)
+            return None, dstep
+        return self.model.forward(dstep, self.kv), dstep
 
     def shutdown_workers(self):
         if self.bcast is not None:
             self.bcast.stop()
 
-    def _sample(self, hidden: torch.Tensor, seqs: List[Sequence]) -> List[int]:
-        if not seqs:
+    def _sample(self, hidden: torch.Tensor, dstep, n: int) -> List[int]:
+        """Fused LM-head-rows + grammar mask + Gumbel-max sampling (K9) on the
+        allowed sets that travelled with the step descriptor."""
+        if n == 0:
             return []
-        allowed = [s.decoder.allowed() for s in seqs]
-        ptr = np.zeros(len(seqs) + 1, np.int32)
-        ptr[1:] = np.cumsum([len(a) for a in allowed])
-        flat = np.fromiter(itertools.chain.from_iterable(allowed), dtype=np.int32, count=int(ptr[-1]))
-        ctr = np.asarray([s.uid * 65536 + s.n_samples for s in seqs], np.int64)
-        dev = self.device
-        if dev.type == "cuda":
-            host = torch.from_numpy(np.concatenate([ptr, flat]))
-            d = host.pin_memory().to(dev, non_blocking=True)
-            ptr_t, ids_t = d[:ptr.size], d[ptr.size:]
-            ctr_t = torch.from_numpy(ctr).pin_memory().to(dev, non_blocking=True)
-        else:
-            ptr_t, ids_t, ctr_t = torch.from_numpy(ptr), torch.from_numpy(flat), torch.from_numpy(ctr)
-        tok = ops.sample_allowed(hidden, self.model.w.lm_head, ptr_t, ids_t, ctr_t, self.temperature,
-                                 self.seed + self.steps)
-        self.stats["samples"] += len(seqs)
+        tok = ops.sample_allowed(hidden, self.model.w.lm_head, dstep.allow_ptr, dstep.allow_ids,
+                                 dstep.sample_ctr, self.temperature, self.seed + self.steps)
+        self.stats["samples"] += n
         return tok.cpu().tolist()
 
     # -------------------------------------------------------------- driver

@@ -153,7 +153,7 @@ def test_sample_allowed_greedy_and_distribution():
     ptr = np.cumsum([0] + [len(a) for a in allowed]).astype(np.int32)
     ids = torch.tensor(sum(allowed, []), dtype=torch.int32, device=DEV)
     ptr_t = torch.from_numpy(ptr).to(DEV)
-    ctr = torch.arange(S, dtype=torch.int64, device=DEV)
+    ctr = torch.arange(S, dtype=torch.int32, device=DEV)
     tok = ops.sample_allowed(hidden, W, ptr_t, ids, ctr, 0.0, 1234)
     for s, (aid, logits) in enumerate(ref.sample_allowed_logits(hidden.cpu(), W.cpu(), ptr, ids.cpu())):
         assert int(tok[s]) == int(aid[int(torch.argmax(logits))])
@@ -173,7 +173,7 @@ def test_sample_allowed_greedy_and_distribution():
         pp = torch.arange(0, 201, dtype=torch.int32, device=DEV) * 0
         ptr_b = torch.tensor(np.arange(201) * len(aid), dtype=torch.int32, device=DEV)
         ids_b = ids1.repeat(200)
-        c = torch.arange(i * 200, (i + 1) * 200, dtype=torch.int64, device=DEV)
+        c = torch.arange(i * 200, (i + 1) * 200, dtype=torch.int32, device=DEV)
         t = ops.sample_allowed(hh, W, ptr_b, ids_b, c, T, 99)
         for x in t.cpu().tolist():
             counts[pos[x]] += 1
