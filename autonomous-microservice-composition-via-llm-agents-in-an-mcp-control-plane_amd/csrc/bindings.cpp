@@ -230,6 +230,30 @@ void add_inplace(at::Tensor& y, const at::Tensor& x) {
   launch_add_inplace(y.data_ptr(), x.data_ptr(), y.numel(), stream());
 }
 
+// ---- K12 custom all-reduce: the state is an opaque int64 handle on the Python side
+int64_t car_init(int64_t rank, int64_t world, int64_t buf_bytes, at::Tensor& handles_out) {
+  TORCH_CHECK(handles_out.device().is_cpu() && handles_out.scalar_type() == at::kByte &&
+              handles_out.numel() == (int64_t)car_handle_bytes(), "handles_out: uint8 cpu");
+  void* st = car_create(rank, world, buf_bytes, handles_out.data_ptr());
+  TORCH_CHECK(st != nullptr, "custom all-reduce: allocation / IPC export failed");
+  return (int64_t)(intptr_t)st;
+}
+
+void car_connect(int64_t h, const at::Tensor& all_handles) {
+  TORCH_CHECK(all_handles.device().is_cpu() && all_handles.scalar_type() == at::kByte &&
+              all_handles.is_contiguous(), "all_handles: uint8 cpu [world, handle_bytes]");
+  const int rc = car_open((void*)(intptr_t)h, all_handles.data_ptr());
+  TORCH_CHECK(rc == 0, "custom all-reduce: hipIpcOpenMemHandle failed (", rc, ")");
+}
+
+void car_run(int64_t h, const at::Tensor& inp, at::Tensor& out, int64_t mode, int64_t blocks) {
+  CHECK_BF16_TENSOR(inp); CHECK_BF16_TENSOR(out);
+  TORCH_CHECK(inp.numel() == out.numel(), "all-reduce shapes");
+  const int rc = car_allreduce((void*)(intptr_t)h, inp.data_ptr(), out.data_ptr(), inp.numel(),
+                               (int)mode, (int)blocks, stream());
+  TORCH_CHECK(rc == 0, "custom all-reduce launch failed (", rc, ")");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -261,4 +285,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_dense", &sample_dense);
   m.def("add_inplace", &add_inplace);
   m.def("copy_blocks", &copy_blocks);
+  m.def("car_handle_bytes", []() { return (int64_t)car_handle_bytes(); });
+  m.def("car_init", &car_init);
+  m.def("car_connect", &car_connect);
+  m.def("car_run", &car_run);
+  m.def("car_error", [](int64_t h) { return car_error((void*)(intptr_t)h); });
+  m.def("car_destroy", [](int64_t h) { car_destroy((void*)(intptr_t)h); });
 }

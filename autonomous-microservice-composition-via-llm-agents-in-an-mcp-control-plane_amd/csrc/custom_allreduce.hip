@@ -1,0 +1,269 @@
+// K12: custom all-reduce over xGMI peer-to-peer.
+//
+// RCCL's ring all-reduce moves 2(N-1)/N of the message through every link in
+// 2(N-1) latency-bound hops.  For decode-sized tensor-parallel messages
+// ([B, 8192] bf16 = 16 KiB * B) the hops dominate, and the MI355X topology
+// (every GPU has its own xGMI link to each of the 7 others, MI355X_MICROARCH.md)
+// lets a kernel read all 7 peers' buffers in parallel instead:
+//
+//  * one-shot (small messages): every rank copies its input into its own
+//    IPC-shared staging buffer, signals every peer, waits for every peer's
+//    signal, then reads the same slice from all N buffers and sums in fp32.
+//    One barrier, N-1 remote reads of the whole message per rank.
+//  * two-shot (mid-size): reduce-scatter (each rank sums its 1/N slice from all
+//    peers into its own buffer), barrier, all-gather (read the reduced slices
+//    of all peers).  2(N-1)/N of the message crosses the links per rank, like a
+//    ring, but in 2 barriers instead of 2(N-1) hops.
+//
+// Synchronisation: per-block flags in uncached, IPC-shared signal memory,
+// written with system-scope release stores and polled with system-scope
+// acquire loads.  Flags carry a monotonically increasing epoch (no reset).
+// Staging buffers are double-buffered by epoch parity, so no end-of-kernel
+// barrier is needed: a rank can only overwrite a buffer two calls later, after
+// every peer has passed the next call's start barrier (stream order).
+// Every wait has a wall-clock timeout (no hang if a peer dies): the kernel
+// records an error code the host checks and gives up instead of spinning.
+#include <string.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int CAR_MAX_RANKS = 8;
+constexpr int CAR_MAX_BLOCKS = 128;
+constexpr int CAR_THREADS = 512;
+// ~2 s at the 100 MHz constant clock behind wall_clock64()
+constexpr long long CAR_TIMEOUT_TICKS = 200000000ll;
+
+struct CarArgs {
+  const bf16x8* inp;
+  bf16x8* out;
+  bf16x8* bufs[CAR_MAX_RANKS];       // staging buffers of this epoch's parity
+  unsigned* sigs[CAR_MAX_RANKS];     // signal arrays of every rank
+  int* err;
+  long long nvec;                    // message length in 16-byte vectors
+  int rank, world;
+  unsigned epoch;
+};
+
+// flag slot of (phase, block, source rank) inside one rank's signal array
+DEV int sig_slot(int phase, int block, int src) {
+  return (phase * CAR_MAX_BLOCKS + block) * CAR_MAX_RANKS + src;
+}
+
+// All threads: make this block's prior writes visible system-wide, then
+// thread p < world raises our flag in rank p's signal array and waits for
+// rank p's flag in ours.
+DEV void block_barrier(const CarArgs& a, int phase) {
+  __threadfence_system();
+  __syncthreads();
+  const int p = threadIdx.x;
+  if (p < a.world) {
+    __hip_atomic_store(a.sigs[p] + sig_slot(phase, blockIdx.x, a.rank), a.epoch,
+                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned* mine = a.sigs[a.rank] + sig_slot(phase, blockIdx.x, p);
+    const long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+      if (wall_clock64() - t0 > CAR_TIMEOUT_TICKS) {
+        atomicExch(a.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);   // later plain loads see peers' data
+}
+
+DEV void acc8(float (&s)[8], const bf16x8& v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+}
+
+DEV bf16x8 pack8(const float (&s)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)s[j];
+  return r;
+}
+
+template <int W>
+DEV void sum_range(const CarArgs& a, long long v0, long long v1, bf16x8* dst) {
+  for (long long v = v0 + threadIdx.x; v < v1; v += CAR_THREADS) {
+    bf16x8 x[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) x[p] = a.bufs[p][v];      // W loads in flight
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < W; ++p) acc8(s, x[p]);
+    dst[v] = pack8(s);
+  }
+}
+
+DEV void sum_range_dyn(const CarArgs& a, long long v0, long long v1, bf16x8* dst) {
+  switch (a.world) {
+    case 2: sum_range<2>(a, v0, v1, dst); break;
+    case 3: sum_range<3>(a, v0, v1, dst); break;
+    case 4: sum_range<4>(a, v0, v1, dst); break;
+    case 5: sum_range<5>(a, v0, v1, dst); break;
+    case 6: sum_range<6>(a, v0, v1, dst); break;
+    case 7: sum_range<7>(a, v0, v1, dst); break;
+    default: sum_range<8>(a, v0, v1, dst); break;
+  }
+}
+
+DEV void block_range(long long n, long long& v0, long long& v1) {
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  v0 = min(n, per * blockIdx.x);
+  v1 = min(n, v0 + per);
+}
+
+__global__ __launch_bounds__(CAR_THREADS) void car_one_shot(CarArgs a) {
+  long long v0, v1;
+  block_range(a.nvec, v0, v1);
+  bf16x8* mine = a.bufs[a.rank];
+  for (long long v = v0 + threadIdx.x; v < v1; v += CAR_THREADS) mine[v] = a.inp[v];
+  block_barrier(a, 0);
+  sum_range_dyn(a, v0, v1, a.out);
+}
+
+__global__ __launch_bounds__(CAR_THREADS) void car_two_shot(CarArgs a) {
+  long long v0, v1;
+  block_range(a.nvec, v0, v1);
+  bf16x8* mine = a.bufs[a.rank];
+  for (long long v = v0 + threadIdx.x; v < v1; v += CAR_THREADS) mine[v] = a.inp[v];
+  block_barrier(a, 0);
+  // reduce-scatter: my slice of this block's range, summed into my own buffer
+  const long long n = v1 - v0, per = (n + a.world - 1) / a.world;
+  const long long s0 = v0 + min(n, per * a.rank), s1 = v0 + min(n, per * (a.rank + 1));
+  sum_range_dyn(a, s0, s1, mine);
+  block_barrier(a, 1);
+  // all-gather: every rank's reduced slice
+  for (int q = 0; q < a.world; ++q) {
+    const int p = (a.rank + q) % a.world;            // stagger peers across ranks
+    const long long t0 = v0 + min(n, per * p), t1 = v0 + min(n, per * (p + 1));
+    const bf16x8* src = a.bufs[p];
+    for (long long v = t0 + threadIdx.x; v < t1; v += CAR_THREADS) a.out[v] = src[v];
+  }
+}
+
+struct CarState {
+  int rank = 0, world = 1;
+  size_t buf_bytes = 0;
+  char* data = nullptr;              // own staging: 2 x buf_bytes (epoch parity)
+  unsigned* sig = nullptr;           // own signal array (uncached)
+  int* err = nullptr;
+  char* peer_data[CAR_MAX_RANKS] = {};
+  unsigned* peer_sig[CAR_MAX_RANKS] = {};
+  unsigned epoch = 0;
+  bool opened = false;
+};
+
+constexpr size_t SIG_BYTES = sizeof(unsigned) * 2 * CAR_MAX_BLOCKS * CAR_MAX_RANKS;
+
+}  // namespace
+
+size_t car_handle_bytes() { return 2 * sizeof(hipIpcMemHandle_t); }
+
+void* car_create(int rank, int world, size_t buf_bytes, void* handles_out) {
+  if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return nullptr;
+  CarState* st = new CarState();
+  st->rank = rank;
+  st->world = world;
+  st->buf_bytes = (buf_bytes + 255) & ~size_t(255);
+  bool ok = hipMalloc(&st->data, 2 * st->buf_bytes) == hipSuccess &&
+            hipExtMallocWithFlags((void**)&st->sig, SIG_BYTES, hipDeviceMallocUncached) ==
+                hipSuccess &&
+            hipMalloc(&st->err, sizeof(int)) == hipSuccess &&
+            hipMemset(st->sig, 0, SIG_BYTES) == hipSuccess &&
+            hipMemset(st->err, 0, sizeof(int)) == hipSuccess &&
+            hipDeviceSynchronize() == hipSuccess;
+  hipIpcMemHandle_t h[2];
+  ok = ok && hipIpcGetMemHandle(&h[0], st->data) == hipSuccess &&
+       hipIpcGetMemHandle(&h[1], st->sig) == hipSuccess;
+  if (!ok) {
+    if (st->data) (void)hipFree(st->data);
+    if (st->sig) (void)hipFree(st->sig);
+    if (st->err) (void)hipFree(st->err);
+    delete st;
+    return nullptr;
+  }
+  memcpy(handles_out, h, sizeof(h));
+  return st;
+}
+
+// all_handles: world x car_handle_bytes(), rank-major
+int car_open(void* state, const void* all_handles) {
+  CarState* st = (CarState*)state;
+  const hipIpcMemHandle_t* h = (const hipIpcMemHandle_t*)all_handles;
+  for (int p = 0; p < st->world; ++p) {
+    if (p == st->rank) {
+      st->peer_data[p] = st->data;
+      st->peer_sig[p] = st->sig;
+      continue;
+    }
+    void* d = nullptr;
+    void* s = nullptr;
+    if (hipIpcOpenMemHandle(&d, h[2 * p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -1;
+    if (hipIpcOpenMemHandle(&s, h[2 * p + 1], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+      return -2;
+    st->peer_data[p] = (char*)d;
+    st->peer_sig[p] = (unsigned*)s;
+  }
+  st->opened = true;
+  return 0;
+}
+
+// in-place allowed (inp == out).  mode: 1 one-shot, 2 two-shot.  Returns 0 on
+// success (the launch is asynchronous; check car_error for peer timeouts).
+int car_allreduce(void* state, const void* inp, void* out, long long n_elems, int mode,
+                  int blocks, hipStream_t s) {
+  CarState* st = (CarState*)state;
+  if (!st->opened) return -1;
+  if (n_elems % 8 || (size_t)n_elems * 2 > st->buf_bytes) return -2;
+  st->epoch += 1;
+  CarArgs a;
+  a.inp = (const bf16x8*)inp;
+  a.out = (bf16x8*)out;
+  const size_t off = (st->epoch & 1) ? st->buf_bytes : 0;
+  for (int p = 0; p < CAR_MAX_RANKS; ++p) {
+    a.bufs[p] = p < st->world ? (bf16x8*)(st->peer_data[p] + off) : nullptr;
+    a.sigs[p] = p < st->world ? st->peer_sig[p] : nullptr;
+  }
+  a.err = st->err;
+  a.nvec = n_elems / 8;
+  a.rank = st->rank;
+  a.world = st->world;
+  a.epoch = st->epoch;
+  long long want = (a.nvec + CAR_THREADS * 4 - 1) / (CAR_THREADS * 4);
+  if (blocks <= 0) blocks = (int)min(want, (long long)CAR_MAX_BLOCKS);
+  blocks = max(1, min(blocks, CAR_MAX_BLOCKS));
+  if (mode == 2)
+    car_two_shot<<<blocks, CAR_THREADS, 0, s>>>(a);
+  else
+    car_one_shot<<<blocks, CAR_THREADS, 0, s>>>(a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int car_error(void* state) {
+  CarState* st = (CarState*)state;
+  int e = 0;
+  if (hipMemcpy(&e, st->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return e;
+}
+
+void car_destroy(void* state) {
+  CarState* st = (CarState*)state;
+  if (!st) return;
+  (void)hipDeviceSynchronize();
+  for (int p = 0; p < st->world; ++p)
+    if (p != st->rank && st->peer_data[p]) {
+      (void)hipIpcCloseMemHandle(st->peer_data[p]);
+      (void)hipIpcCloseMemHandle(st->peer_sig[p]);
+    }
+  (void)hipFree(st->data);
+  (void)hipFree(st->sig);
+  (void)hipFree(st->err);
+  delete st;
+}

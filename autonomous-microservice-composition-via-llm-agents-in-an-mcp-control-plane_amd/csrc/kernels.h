@@ -60,3 +60,12 @@ void launch_sample_allowed(const void* hidden, const void* W, const int* allow_p
                            hipStream_t s);
 void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float temperature,
                          unsigned long long seed, int* out_tok, hipStream_t s);
+
+// custom_allreduce.hip (K12): opaque state handle, IPC handles exchanged by the caller
+size_t car_handle_bytes();
+void* car_create(int rank, int world, size_t buf_bytes, void* handles_out);
+int car_open(void* state, const void* all_handles);
+int car_allreduce(void* state, const void* inp, void* out, long long n_elems, int mode,
+                  int blocks, hipStream_t s);
+int car_error(void* state);
+void car_destroy(void* state);

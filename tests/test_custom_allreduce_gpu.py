@@ -1,0 +1,98 @@
+"""K12 custom all-reduce: two ranks in two processes sharing the box's one GPU.
+
+The kernel's IPC export/open, the flag barriers with epochs, the double-
+buffered staging and both one-shot and two-shot reductions run exactly as on
+an 8-GPU node; only the xGMI hop is replaced by a local HBM read.  The result
+is compared against a plain fp32 PyTorch sum of both ranks' inputs.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [8, 4096, 8192 * 16, 8192 * 256]
+
+
+def _data(rank, n, it):
+    g = torch.Generator().manual_seed(1000 * rank + 7 * it + n)
+    return torch.randn(n, generator=g).to(torch.bfloat16)
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        import mcp_amd  # noqa: F401
+        from mcp_amd.parallel.custom_allreduce import CustomAllReduce
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        car = CustomAllReduce(dist.group.WORLD, "cuda:0", max_bytes=8 << 20)
+        errs = []
+        for mode in (1, 2):
+            for n in SIZES:
+                for it in range(3):                  # epochs / buffer parity
+                    x = _data(rank, n, it).cuda()
+                    y = car(x.clone(), mode=mode)
+                    torch.cuda.synchronize()
+                    ref = sum(_data(r, n, it).float() for r in range(world))
+                    err = (y.float().cpu() - ref).abs().max().item()
+                    tol = 2e-2 * ref.abs().max().item() + 1e-2
+                    if err > tol:
+                        errs.append((mode, n, it, err, tol))
+        # timing of the decode-sized message (one-shot) and a 4 MiB one (two-shot)
+        times = {}
+        for n, mode in ((8192 * 8, 1), (8192 * 256, 2)):
+            x = torch.randn(n, device="cuda").bfloat16()
+            for _ in range(5):
+                car(x, mode=mode)
+            torch.cuda.synchronize()
+            dist.barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                car(x, mode=mode)
+            e1.record()
+            torch.cuda.synchronize()
+            times[(n, mode)] = e0.elapsed_time(e1) / 50 * 1e3
+        car.check()
+        car.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, errs, times))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, [repr(e)], {}))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_custom_allreduce_two_ranks_one_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, errs, times = q.get(timeout=240)
+            results[rank] = (errs, times)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, (errs, times) in results.items():
+        assert not errs, f"rank {rank}: {errs}"
+        print(f"rank {rank} custom all-reduce us/call: {times}")
