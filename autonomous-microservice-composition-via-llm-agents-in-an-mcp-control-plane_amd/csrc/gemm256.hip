@@ -45,10 +45,24 @@ DEV void barrier() {
 //           issue no LDS reads and their MFMAs start immediately
 //   PRIO  : s_setprio 1 around the MFMA cluster
 //   GFIRST: issue the next K-tile's LDS-DMA piece before this phase's ds_reads
-template <bool BAR4, bool PREA, bool PRIO, bool GFIRST>
+//   PP    : ping-pong (cdna_hip_programming.md §5 8-phase template): two
+//           barriers per phase {reads + LDS-DMA issue | barrier | MFMA |
+//           barrier} and the two M-half wave groups offset by one barrier, so
+//           on every SIMD one wave runs its MFMA cluster while the other
+//           issues its LDS reads and loads.
+template <bool BAR4, bool PREA, bool PRIO, bool GFIRST, bool PP = false>
 struct V256 {
-  static constexpr bool bar4 = BAR4, prea = PREA, prio = PRIO, gfirst = GFIRST;
+  static constexpr bool bar4 = BAR4, prea = PREA, prio = PRIO, gfirst = GFIRST, pp = PP;
 };
+using V256PingPong = V256<false, false, true, true, true>;
+
+DEV void sched_barrier_full() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 using V256Default = V256<false, false, false, true>;   // variant 8: best of the 16-way sweep
 
 template <int EPI, class VAR = V256Default>   // EPI: 0 plain, 1 +residual, 2 SwiGLU
@@ -144,6 +158,27 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
       for (int mt = 0; mt < 4; ++mt) afr[1][mt] = *reinterpret_cast<const bf16x8*>(sA + offA[1][mt]);
     }
     if (!VAR::gfirst && prefetch) stage(t + 1, p);
+    if constexpr (VAR::pp) {
+      // RAW: pieces read first in phase 0 / 2 of a K-tile retire here in
+      // phases 3 / 1, before the barrier both wave groups pass before reading
+      if (p == 1) {
+        if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else if (p == 3 && !last) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      sched_barrier_full();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (VAR::prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mh][mt][nt] = mfma16x16x32(bfr[nt], afr[mh][mt], acc[mh][mt][nt]);
+      if (VAR::prio) __builtin_amdgcn_s_setprio(0);
+      sched_barrier_full();
+      return;
+    }
     if (VAR::prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -160,6 +195,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
     if (VAR::bar4 || p == 1 || p == 3) barrier();
   };
 
+  if (VAR::pp && wm == 1) sched_barrier_full();    // stagger the two wave groups
   for (int t = 0; t + 1 < nk; ++t) {
     phase(t, 0, true, false);
     phase(t, 1, true, false);
@@ -173,6 +209,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
     phase(t, 2, false, true);
     phase(t, 3, false, true);
   }
+  if (VAR::pp && wm == 0) sched_barrier_full();
 
   // ---- epilogue: lane holds Y[m][n .. n+3]
 #pragma unroll
@@ -245,6 +282,9 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
       return launch_gemm_tn_256w4(X, W, Y, nullptr, M, N, K, v - 16, s);
     case 22: case 23:
       return launch_gemm_tn_256w4m16(X, W, Y, nullptr, M, N, K, v - 18, s);
+    case 24: launch_var<V256PingPong>(X, W, Y, M, N, K, s); return 0;
+    case 25: launch_var<V256<false, false, false, true, true>>(X, W, Y, M, N, K, s); return 0;
+    case 26: launch_var<V256<false, true, true, true, true>>(X, W, Y, M, N, K, s); return 0;
     default: return 1;
   }
 }

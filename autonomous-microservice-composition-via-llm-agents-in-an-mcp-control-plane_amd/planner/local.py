@@ -18,6 +18,8 @@ synchronous batch path used by the benchmark.
 """
 from __future__ import annotations
 
+import os
+
 import asyncio
 import queue
 import threading
@@ -56,8 +58,12 @@ class LocalPlanner(Planner):
         from ..engine.engine import LLMEngine
         from ..models.llama import LlamaModel
         from ..retrieval.store import SchemaIndex
+        from ..models.weights import model_from_checkpoint
         dev = "cuda:0" if torch.cuda.is_available() else "cpu"
-        model = LlamaModel.random(settings.model, dev, seed=settings.seed)
+        if os.path.isdir(settings.model):        # an HF safetensors checkpoint directory
+            model = model_from_checkpoint(settings.model, dev)
+        else:                                     # a named architecture, random-init weights
+            model = LlamaModel.random(settings.model, dev, seed=settings.seed)
         kw = {} if dev != "cpu" else {"num_blocks": 512}
         eng = LLMEngine(model, max_batch=settings.max_batch, max_step_tokens=settings.max_step_tokens,
                         temperature=settings.temperature, seed=settings.seed, **kw)
