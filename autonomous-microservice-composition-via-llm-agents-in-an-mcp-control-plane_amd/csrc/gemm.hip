@@ -161,13 +161,16 @@ int gemm_tn_check(int M, int N, int K) {
 // workgroup per CU (256 concurrent tiles), the 128x128 kernel ~1.04 PF/s with
 // two per CU (512 concurrent tiles).  Predicted time = full waves of tiles x
 // per-wave time; pick the smaller.
+double gemm256_waves(int M, int N, int K);
+int gemm256_num_cus();
+
 int gemm_select(int M, int N, int K) {
   if (M < 256 || N < 256 || K < 128) return 0;
-  const double t256 = (double)(((M + 255) / 256) * ((N + 255) / 256));
+  const double G = (double)gemm256_num_cus();
   const double t128 = (double)(((M + 127) / 128) * ((N + 127) / 128));
-  const double w256 = ceil(t256 / 256.0), w128 = ceil(t128 / 512.0);
-  const double cost256 = w256 * 256.0 * 4.0 / 1.22;     // in 128^2-tile units / PF
-  const double cost128 = w128 * 512.0 / 1.04;
+  // 256^2 waves (stream-K hybrid where it pays) vs 128^2 waves at 2 blocks/CU
+  const double cost256 = gemm256_waves(M, N, K) * G * 4.0 / 1.22;   // 128^2-tile units / PF
+  const double cost128 = ceil(t128 / (2.0 * G)) * 2.0 * G / 1.04;
   return cost256 < cost128 ? 1 : 0;
 }
 

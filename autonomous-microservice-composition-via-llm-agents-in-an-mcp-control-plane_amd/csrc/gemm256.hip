@@ -65,27 +65,24 @@ DEV void sched_barrier_full() {
 }
 using V256Default = V256<false, false, false, true>;   // variant 8: best of the 16-way sweep
 
-template <int EPI, class VAR = V256Default>   // EPI: 0 plain, 1 +residual, 2 SwiGLU
-__global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X,
-                                                      const bf16* __restrict__ W,
-                                                      bf16* __restrict__ Y,
-                                                      const bf16* __restrict__ R, int M, int N,
-                                                      int K) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[8 * PIECE];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const int nwg = nm * nn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+// Grouped tile order: GROUP M-tiles share each W column panel in L2.
+DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
   constexpr int GROUP = 4;
   const int per_group = GROUP * nn;
-  const int g = wg / per_group;
+  const int g = t / per_group;
   const int first_m = g * GROUP;
   const int gsz = min(nm - first_m, GROUP);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
+  m0 = (first_m + (t % per_group) % gsz) * BM;
+  n0 = ((t % per_group) / gsz) * BN;
+}
 
+// K-tiles [kt0, kt1) of the 256x256 tile at (m0, n0) accumulated into acc.
+// Starts with a barrier (the LDS ring may still be read by a previous tile).
+template <class VAR>
+DEV void mainloop(const bf16* __restrict__ X, const bf16* __restrict__ W, int M, int N, int K,
+                  int m0, int n0, int kt0, int kt1, bf16* smem, f32x4 (&acc)[2][4][4]) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   // ---- staging: wave w writes 1 KiB instructions 2w, 2w+1 of every piece
   //      (rows (2w+j)*16 + lane/4, 16-B chunk lane%4 of the 64-B row)
   const bf16* srcA[2];
@@ -107,7 +104,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
 
   const int wm = wave >> 2, wn = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  f32x4 acc[2][4][4];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -130,10 +126,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
     offB[nt] = row * KH + swz(row, fq) * 8;
   }
 
-  const int nk = K / BK;
-  // prologue: K-tile 0 fully resident
+  barrier();
+  // prologue: K-tile kt0 fully resident
 #pragma unroll
-  for (int i = 0; i < 4; ++i) stage(0, i);
+  for (int i = 0; i < 4; ++i) stage(kt0, i);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   barrier();
 
@@ -196,22 +192,30 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
   };
 
   if (VAR::pp && wm == 1) sched_barrier_full();    // stagger the two wave groups
-  for (int t = 0; t + 1 < nk; ++t) {
+  for (int t = kt0; t + 1 < kt1; ++t) {
     phase(t, 0, true, false);
     phase(t, 1, true, false);
     phase(t, 2, true, false);
     phase(t, 3, true, false);
   }
   {
-    const int t = nk - 1;
+    const int t = kt1 - 1;
     phase(t, 0, false, true);
     phase(t, 1, false, true);
     phase(t, 2, false, true);
     phase(t, 3, false, true);
   }
   if (VAR::pp && wm == 0) sched_barrier_full();
+}
 
-  // ---- epilogue: lane holds Y[m][n .. n+3]
+// lane holds Y[m][n .. n+3] of each 16x16 fragment
+template <int EPI>
+DEV void epilogue(bf16* __restrict__ Y, const bf16* __restrict__ R, int M, int N, int m0, int n0,
+                  const f32x4 (&acc)[2][4][4]) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
@@ -250,6 +254,108 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
     }
 }
 
+template <int EPI, class VAR = V256Default>   // EPI: 0 plain, 1 +residual, 2 SwiGLU
+__global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X,
+                                                      const bf16* __restrict__ W,
+                                                      bf16* __restrict__ Y,
+                                                      const bf16* __restrict__ R, int M, int N,
+                                                      int K) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[8 * PIECE];
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  int m0, n0;
+  tile_coords(xcd_remap(blockIdx.x, nm * nn), nm, nn, m0, n0);
+  f32x4 acc[2][4][4];
+  mainloop<VAR>(X, W, M, N, K, m0, n0, 0, K / BK, smem, acc);
+  epilogue<EPI>(Y, R, M, N, m0, n0, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Stream-K hybrid (fixes wave quantisation: 336 tiles on 256 CUs run as 2
+// waves at 66 % occupancy).  A persistent grid of G workgroups (one per CU)
+// first runs `dp_waves` full waves of whole tiles, then splits the remaining
+// tiles' K-iterations evenly: workgroup b owns iterations
+// [b*S/G, (b+1)*S/G) of the S = sk_tiles * nk remaining ones.  A tile split
+// across workgroups is finished by the LAST contributor to arrive: every
+// contributor stores its fp32 partial (register order, coalesced float4) to
+// its own workspace slot, releases it (agent-scope fence: the 8 XCD L2s are
+// not coherent) and bumps the tile's arrival counter; the one that sees
+// count == contributors - 1 sums all partials in contributor order
+// (deterministic), applies the epilogue and re-arms the counter.
+struct SkPlan {
+  int G, dp_waves, dp_tiles, sk_tiles, nk;
+  long long S;
+};
+
+DEV long long sk_begin(int b, const SkPlan& p) { return (long long)b * p.S / p.G; }
+
+template <int EPI, class VAR = V256Default>
+__global__ __launch_bounds__(512, 1) void gemm_tn_256_sk(const bf16* __restrict__ X,
+                                                         const bf16* __restrict__ W,
+                                                         bf16* __restrict__ Y,
+                                                         const bf16* __restrict__ R, int M, int N,
+                                                         int K, SkPlan plan,
+                                                         float* __restrict__ ws,
+                                                         int* __restrict__ cnt) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[8 * PIECE];
+  __shared__ int s_last;
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const int b = xcd_remap(blockIdx.x, plan.G);
+  f32x4 acc[2][4][4];
+  int m0, n0;
+  for (int w = 0; w < plan.dp_waves; ++w) {
+    tile_coords(w * plan.G + b, nm, nn, m0, n0);
+    mainloop<VAR>(X, W, M, N, K, m0, n0, 0, plan.nk, smem, acc);
+    epilogue<EPI>(Y, R, M, N, m0, n0, acc);
+  }
+  const long long it_end = sk_begin(b + 1, plan);
+  long long it = sk_begin(b, plan);
+  f32x4* wsv = reinterpret_cast<f32x4*>(ws);
+  while (it < it_end) {
+    const int st = (int)(it / plan.nk);                 // stream-K tile index
+    const long long t_start = (long long)st * plan.nk, t_end = t_start + plan.nk;
+    const int k0 = (int)(it - t_start);
+    const int k1 = (int)(min(it_end, t_end) - t_start);
+    tile_coords(plan.dp_tiles + st, nm, nn, m0, n0);
+    mainloop<VAR>(X, W, M, N, K, m0, n0, k0, k1, smem, acc);
+    if (k0 == 0 && k1 == plan.nk) {                     // whole tile in one workgroup
+      epilogue<EPI>(Y, R, M, N, m0, n0, acc);
+      it = t_end;
+      continue;
+    }
+    // contributors: workgroups whose ranges intersect [t_start, t_end)
+    int c0 = (int)(t_start * plan.G / plan.S);
+    while (c0 > 0 && sk_begin(c0, plan) > t_start) --c0;
+    while (sk_begin(c0 + 1, plan) <= t_start) ++c0;
+    int c1 = c0;
+    while (c1 + 1 < plan.G && sk_begin(c1 + 1, plan) < t_end) ++c1;
+    const int slot = sk_begin(b, plan) < t_start ? 1 : 0;
+    f32x4* mine = wsv + (size_t)(b * 2 + slot) * 32 * 512;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) mine[q * 512 + threadIdx.x] = (&acc[0][0][0])[q];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(cnt + st, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+               c1 - c0;
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      f32x4 tot[2][4][4];
+#pragma unroll
+      for (int q = 0; q < 32; ++q) (&tot[0][0][0])[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int c = c0; c <= c1; ++c) {
+        const int cs = sk_begin(c, plan) < t_start ? 1 : 0;
+        const f32x4* src = wsv + (size_t)(c * 2 + cs) * 32 * 512;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) (&tot[0][0][0])[q] += src[q * 512 + threadIdx.x];
+      }
+      epilogue<EPI>(Y, R, M, N, m0, n0, tot);
+      if (threadIdx.x == 0) cnt[st] = 0;
+    }
+    it = min(it_end, t_end);
+  }
+}
+
 template <class VAR>
 void launch_var(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
@@ -268,6 +374,9 @@ int launch_gemm_tn_256w4(const void* X, const void* W, void* Y, const void* R, i
 int launch_gemm_tn_256w4m16(const void* X, const void* W, void* Y, const void* R, int M, int N,
                             int K, int stages, hipStream_t s);
 
+int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N, int K, int mode,
+                            int pingpong, hipStream_t s);
+
 // tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
                                hipStream_t s) {
@@ -285,27 +394,107 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 24: launch_var<V256PingPong>(X, W, Y, M, N, K, s); return 0;
     case 25: launch_var<V256<false, false, false, true, true>>(X, W, Y, M, N, K, s); return 0;
     case 26: launch_var<V256<false, true, true, true, true>>(X, W, Y, M, N, K, s); return 0;
+    case 30: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 1, 0, s);   // data-parallel
+    case 31: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 0, s);   // stream-K forced
+    case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 0, s);   // auto
+    case 33: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 1, s);   // stream-K + ping-pong
     default: return 1;
   }
 }
 
+namespace {
+
+struct SkDevice {
+  int G = 0;
+  float* ws = nullptr;
+  int* cnt = nullptr;
+};
+
+// persistent-grid size and stream-K workspace of the current device (allocated
+// on first use, outside any graph capture)
+SkDevice& sk_device() {
+  static SkDevice devs[64];
+  int d = 0;
+  (void)hipGetDevice(&d);
+  SkDevice& sd = devs[d & 63];
+  if (sd.G == 0) {
+    hipDeviceProp_t prop;
+    sd.G = hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0
+               ? prop.multiProcessorCount : 256;
+    (void)hipMalloc(&sd.ws, (size_t)sd.G * 2 * 32 * 512 * sizeof(f32x4));
+    (void)hipMalloc(&sd.cnt, sizeof(int) * 4 * sd.G);
+    (void)hipMemset(sd.cnt, 0, sizeof(int) * 4 * sd.G);
+    (void)hipDeviceSynchronize();
+  }
+  return sd;
+}
+
+// Whole waves run data-parallel; the last partial wave plus one full wave are
+// split in K across the persistent grid (each workgroup: 1..2 tiles of work).
+bool sk_plan(int M, int N, int K, int G, int mode, SkPlan& p) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int waves = tiles / G, rem = tiles % G;
+  if (mode == 0) {                                   // auto
+    if (rem == 0) return false;
+    const double eff = (double)tiles / ((double)(waves + 1) * G);
+    if (eff >= 0.92) return false;
+  }
+  p.G = G;
+  p.nk = K / BK;
+  p.dp_waves = waves > 0 ? waves - 1 : 0;
+  p.dp_tiles = p.dp_waves * G;
+  p.sk_tiles = tiles - p.dp_tiles;
+  p.S = (long long)p.sk_tiles * p.nk;
+  return p.sk_tiles <= 4 * G;
+}
+
+template <int EPI, class VAR = V256Default>
+void launch_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                int mode, hipStream_t s) {
+  // mode: 0 auto, 1 data-parallel, 2 stream-K hybrid
+  SkPlan plan;
+  if (mode != 1) {
+    SkDevice& sd = sk_device();
+    if (sk_plan(M, N, K, sd.G, mode == 2 ? 1 : 0, plan)) {
+      gemm_tn_256_sk<EPI, VAR><<<plan.G, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                      (const bf16*)R, M, N, K, plan, sd.ws, sd.cnt);
+      return;
+    }
+  }
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  gemm_tn_256<EPI, VAR><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                      (const bf16*)R, M, N, K);
+}
+
+}  // namespace
+
+// effective waves of the 256^2 kernel (stream-K removes the quantisation of the last wave)
+double gemm256_waves(int M, int N, int K) {
+  SkDevice& sd = sk_device();
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  SkPlan p;
+  if (sk_plan(M, N, K, sd.G, 0, p)) return (double)tiles / sd.G * 1.04 + 0.05;
+  return ceil((double)tiles / sd.G);
+}
+
+int gemm256_num_cus() { return sk_device().G; }
+
 void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         hipStream_t s) {
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const dim3 grid(nm * nn);
-  if (R)
-    gemm_tn_256<1><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                        (const bf16*)R, M, N, K);
-  else
-    gemm_tn_256<0><<<grid, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N,
-                                        K);
+  if (R) launch_256<1>(X, W, Y, R, M, N, K, 0, s);
+  else launch_256<0>(X, W, Y, nullptr, M, N, K, 0, s);
 }
 
 void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N, int K,
                              hipStream_t s) {
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  gemm_tn_256<2><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr,
-                                               M, N, K);
+  launch_256<2>(X, W, Y, nullptr, M, N, K, 0, s);
+}
+
+int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N, int K, int mode,
+                            int pingpong, hipStream_t s) {
+  if (pingpong) launch_256<0, V256PingPong>(X, W, Y, nullptr, M, N, K, mode, s);
+  else launch_256<0>(X, W, Y, nullptr, M, N, K, mode, s);
+  return 0;
 }
 
 // ============================================================================

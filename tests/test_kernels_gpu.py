@@ -273,3 +273,34 @@ def test_gemm_silu_fused(M, F, K):
     y = ops.gemm_silu(X, W)
     exp = (torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t()))
     assert rel_err(y, exp) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(3584, 6144, 4096), (3584, 4096, 14336), (1000, 1024, 4096),
+                                   (700, 520, 320)])
+def test_gemm_stream_k(M, N, K):
+    """Stream-K hybrid (partial tiles reduced by the last-arriving workgroup)
+    against fp32, forced and auto-selected, plain / ping-pong / residual / SwiGLU."""
+    torch.manual_seed(4)
+    L = ops.lib()
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    exp = ref.gemm(X, W)
+    for v in (31, 33, 32, 30):
+        Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        L.gemm_variant(X, W, Y, v)
+        assert rel_err(Y, exp) < 1e-2, v
+    Y1 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    Y2 = torch.empty_like(Y1)
+    L.gemm_variant(X, W, Y1, 31)
+    L.gemm_variant(X, W, Y2, 31)
+    assert torch.equal(Y1, Y2)          # fixed reduction order: deterministic
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    R2 = R.clone()
+    ops.gemm(X, W, R=R2, out=R2, algo=1)
+    assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+    if N % 64 == 0:
+        g, u = W[: N // 2], W[N // 2:]
+        Wi = ref.interleave_gate_up(g, u).contiguous()
+        y = ops.gemm_silu(X, Wi)
+        e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+        assert rel_err(y, e) < 2e-2
