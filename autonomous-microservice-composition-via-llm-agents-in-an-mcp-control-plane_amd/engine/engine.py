@@ -64,6 +64,7 @@ class Sequence:
         self.t_first = None
         self.t_done = None
         self.is_prefix_job = decoder is None
+        self.cohort = 0                        # launch cohort (pipelined engine)
         if decoder is not None:
             self.pending += decoder.advance()
 
@@ -72,15 +73,31 @@ class Sequence:
         return self.decoder is not None and not self.decoder.done
 
 
+@dataclasses.dataclass
+class _Launch:
+    """One forward in flight: what to update once its sampled tokens land."""
+    batch_seqs: list
+    sample_seqs: list
+    tokens: Optional[torch.Tensor]      # host (pinned) copy of the sampled tokens
+    event: Optional[object]             # completion of the D2H copy
+    T: int
+
+
 class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
-                 seed: int = 0, bcast=None, cascade: bool = True):
+                 seed: int = 0, bcast=None, cascade: bool = True, pipeline: Optional[bool] = None):
         self.model = model
         cfg = model.cfg
         self.device = model.device
         self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
         self.cascade = cascade      # shared-prefix (cascade) attention
+        # two launch cohorts in flight: the host schedules / updates one cohort
+        # while the GPU runs the other's forward (no idle GPU between steps)
+        self.pipeline = (self.device.type == "cuda") if pipeline is None else pipeline
+        self.inflight: Dict[int, _Launch] = {}
+        self._turn = 0
+        self._next_cohort = 0
         self.stager = HostStager(self.device)
         if num_blocks is not None:
             self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
@@ -97,7 +114,7 @@ class LLMEngine:
         self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
         self.max_prefixes = 64
         self.steps = 0
-        self.stats = {"tokens": 0, "samples": 0, "forward_s": 0.0, "steps": 0,
+        self.stats = {"tokens": 0, "samples": 0, "steps": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
@@ -155,11 +172,13 @@ class LLMEngine:
             seq = Sequence(decoder, list(prompt_tokens), prefix, on_done)
         else:
             seq = Sequence(decoder, list(prefix_tokens or []) + list(prompt_tokens), None, on_done)
+        seq.cohort = self._next_cohort
+        self._next_cohort ^= 1
         self.waiting.append(seq)
         return seq
 
     def has_work(self) -> bool:
-        return bool(self.running or self.waiting)
+        return bool(self.running or self.waiting or self.inflight)
 
     # ---------------------------------------------------------------- step
     def _admit(self):
@@ -188,13 +207,39 @@ class LLMEngine:
             seq.on_done(seq)
 
     def step(self) -> int:
-        """One forward over the runnable batch.  Returns tokens processed."""
+        """Advance the engine by one launch.  Returns the tokens launched plus
+        the tokens retired (0 = no progress).
+
+        Pipelined: cohort c's previous launch is retired (its sampled tokens
+        fed to the grammar) while the GPU is still busy with cohort c^1's
+        forward, then cohort c is scheduled and launched asynchronously."""
+        if not self.pipeline:
+            L = self._schedule_launch(None)
+            if L is None:
+                return 0
+            self._retire(L)
+            return L.T
+        c = self._turn
+        self._turn ^= 1
+        done = 0
+        L = self.inflight.pop(c, None)
+        if L is not None:
+            self._retire(L)
+            done = L.T
+        nxt = self._schedule_launch(c)
+        if nxt is not None:
+            self.inflight[c] = nxt
+            return done + nxt.T
+        return done
+
+    def _schedule_launch(self, cohort: Optional[int]) -> Optional[_Launch]:
         t_sched = time.perf_counter()
         self._admit()
         if not self.running:
-            return 0
+            return None
+        pool = self.running if cohort is None else [q for q in self.running if q.cohort == cohort]
         copies = []
-        for seq in self.running:
+        for seq in pool:
             if not seq.materialized and seq.prefix.computed:
                 self._materialize(seq, copies)
         budget = self.max_step_tokens
@@ -208,17 +253,17 @@ class LLMEngine:
         casc = None
         if self.cascade:
             counts = {}
-            for seq in self.running:
+            for seq in pool:
                 e = seq.prefix
                 if e is not None and seq.materialized and seq.pending and e.length >= BLOCK_SIZE:
                     counts[id(e)] = counts.get(id(e), 0) + 1
             if counts:
                 best = max(counts, key=counts.get)
-                casc = next(q.prefix for q in self.running if q.prefix is not None and id(q.prefix) == best)
-        order = self.running
+                casc = next(q.prefix for q in pool if q.prefix is not None and id(q.prefix) == best)
+        order = pool
         if casc is not None:
-            order = [q for q in self.running if q.prefix is casc and q.materialized] + \
-                    [q for q in self.running if not (q.prefix is casc and q.materialized)]
+            order = [q for q in pool if q.prefix is casc and q.materialized] + \
+                    [q for q in pool if not (q.prefix is casc and q.materialized)]
         pre_tokens, kv_begin = 0, []
         casc_keys = (casc.length // BLOCK_SIZE) * BLOCK_SIZE if casc is not None else 0
         for seq in order:
@@ -255,7 +300,7 @@ class LLMEngine:
         if T == 0:
             if copies:     # copy-on-write blocks still have to land before later steps
                 self._launch(None, copies)
-            return 0
+            return None
         S = len(batch_seqs)
         maxb = max(len(t) for t in tables)
         bt = np.zeros((S, maxb), np.int32)
@@ -282,15 +327,22 @@ class LLMEngine:
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
         hidden, dstep = self._launch(step, copies)
-        t1 = time.perf_counter()
-        new_tokens = self._sample(hidden, dstep, len(sample_seqs))
-        t2 = time.perf_counter()
-        self.stats["launch_s"] += t1 - t0
-        self.stats["sample_s"] += t2 - t1
-        self.stats["forward_s"] += t2 - t0
+        tokens, event = self._sample(hidden, dstep, len(sample_seqs))
+        self.stats["launch_s"] += time.perf_counter() - t0
         self.stats["tokens"] += T
         self.stats["steps"] += 1
         self.steps += 1
+        return _Launch(batch_seqs, sample_seqs, tokens, event, T)
+
+    def _retire(self, L: _Launch):
+        """Wait for a launch's sampled tokens and advance its sequences."""
+        t1 = time.perf_counter()
+        if L.event is not None:
+            L.event.synchronize()
+        new_tokens = L.tokens.tolist() if L.tokens is not None else []
+        t2 = time.perf_counter()
+        self.stats["sample_s"] += t2 - t1
+        batch_seqs, sample_seqs = L.batch_seqs, L.sample_seqs
         # ---- bookkeeping
         for seq, take in batch_seqs:
             seq.num_cached += take
@@ -310,7 +362,6 @@ class LLMEngine:
         self.stats["update_s"] += time.perf_counter() - t2
         METRICS.set("batch_occupancy", len(self.running))
         METRICS.set("kv_block_utilization", self.alloc.utilization())
-        return T
 
     def _launch(self, step: Optional[StepInputs], copies):
         """Pack -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
@@ -334,21 +385,29 @@ class LLMEngine:
         if self.bcast is not None:
             self.bcast.stop()
 
-    def _sample(self, hidden: torch.Tensor, dstep, n: int) -> List[int]:
+    def _sample(self, hidden: torch.Tensor, dstep, n: int):
         """Fused LM-head-rows + grammar mask + Gumbel-max sampling (K9) on the
-        allowed sets that travelled with the step descriptor."""
+        allowed sets that travelled with the step descriptor.  Returns the
+        host tensor the tokens land in and the event that marks their arrival
+        (asynchronous D2H into pinned memory)."""
         if n == 0:
-            return []
+            return None, None
         tok = ops.sample_allowed(hidden, self.model.w.lm_head, dstep.allow_ptr, dstep.allow_ids,
                                  dstep.sample_ctr, self.temperature, self.seed + self.steps)
         self.stats["samples"] += n
-        return tok.cpu().tolist()
+        if not tok.is_cuda:
+            return tok, None
+        host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        host.copy_(tok, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
 
     # -------------------------------------------------------------- driver
     def run(self, max_steps: int = 1_000_000):
         n = 0
         while self.has_work() and n < max_steps:
-            if self.step() == 0 and not self.waiting:
+            if self.step() == 0 and not self.waiting and not self.inflight:
                 # nothing runnable: sequences blocked on nothing -> bug guard
                 stuck = [s for s in self.running if not s.pending]
                 if stuck:

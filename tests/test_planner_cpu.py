@@ -156,3 +156,19 @@ def test_gate_up_interleave_roundtrip():
     assert torch.equal(g, g2) and torch.equal(u, u2)
     X = torch.randn(3, 8)
     assert torch.allclose(ref.gemm_silu(X, w), torch.nn.functional.silu(X @ g.t()) * (X @ u.t()), atol=1e-5)
+
+
+def test_pipelined_engine_matches_synchronous():
+    """Two launch cohorts in flight (host updates one while the device runs the
+    other) produce the same greedy plans as the synchronous engine."""
+    reg = MemoryRegistry(synthetic_registry(6, seed=4))
+    intents = [synthetic_intent(i) for i in range(5)]
+    out = []
+    for pipe in (False, True):
+        torch.manual_seed(0)
+        model = LlamaModel.random("tiny", "cpu", seed=1)
+        eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, pipeline=pipe)
+        planner = LocalPlanner(eng, reg, max_nodes=3)
+        out.append(planner.plan_many(intents))
+        assert eng.alloc.num_free == eng.kv.num_blocks and not eng.inflight
+    assert out[0] == out[1]
