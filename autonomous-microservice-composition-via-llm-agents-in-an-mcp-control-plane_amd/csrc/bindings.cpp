@@ -254,6 +254,61 @@ void car_run(int64_t h, const at::Tensor& inp, at::Tensor& out, int64_t mode, in
   TORCH_CHECK(rc == 0, "custom all-reduce launch failed (", rc, ")");
 }
 
+// ---- K13 direct RCCL communicator: opaque int64 handle on the Python side
+int rccl_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return 0;
+    case at::kFloat: return 1;
+    case at::kInt: return 2;
+    case at::kHalf: return 3;
+    default: TORCH_CHECK(false, "rccl: unsupported dtype");
+  }
+  return -1;
+}
+
+at::Tensor nccl_unique_id() {
+  auto t = at::empty({(int64_t)rccl_unique_id_bytes()}, at::TensorOptions().dtype(at::kByte));
+  TORCH_CHECK(rccl_get_unique_id(t.data_ptr()) == 0, "ncclGetUniqueId failed");
+  return t;
+}
+
+int64_t nccl_init(int64_t world, int64_t rank, const at::Tensor& uid) {
+  TORCH_CHECK(uid.device().is_cpu() && uid.numel() == (int64_t)rccl_unique_id_bytes(), "uid");
+  void* c = rccl_init(world, rank, uid.data_ptr());
+  TORCH_CHECK(c != nullptr, "ncclCommInitRank failed");
+  return (int64_t)(intptr_t)c;
+}
+
+void nccl_all_reduce(int64_t comm, at::Tensor& t, int64_t op) {
+  CHECK_DEV(t); CHECK_CONTIG(t);
+  TORCH_CHECK(rccl_all_reduce((void*)(intptr_t)comm, t.data_ptr(), t.data_ptr(), t.numel(),
+                              rccl_dtype(t), op, stream()) == 0,
+              "ncclAllReduce: ", rccl_last_error((void*)(intptr_t)comm));
+}
+
+void nccl_all_gather(int64_t comm, const at::Tensor& in, at::Tensor& out) {
+  CHECK_DEV(in); CHECK_CONTIG(in); CHECK_DEV(out); CHECK_CONTIG(out);
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && out.numel() % in.numel() == 0, "shapes");
+  TORCH_CHECK(rccl_all_gather((void*)(intptr_t)comm, in.data_ptr(), out.data_ptr(), in.numel(),
+                              rccl_dtype(in), stream()) == 0,
+              "ncclAllGather: ", rccl_last_error((void*)(intptr_t)comm));
+}
+
+void nccl_reduce_scatter(int64_t comm, const at::Tensor& in, at::Tensor& out, int64_t op) {
+  CHECK_DEV(in); CHECK_CONTIG(in); CHECK_DEV(out); CHECK_CONTIG(out);
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && in.numel() % out.numel() == 0, "shapes");
+  TORCH_CHECK(rccl_reduce_scatter((void*)(intptr_t)comm, in.data_ptr(), out.data_ptr(),
+                                  out.numel(), rccl_dtype(in), op, stream()) == 0,
+              "ncclReduceScatter: ", rccl_last_error((void*)(intptr_t)comm));
+}
+
+void nccl_broadcast(int64_t comm, at::Tensor& t, int64_t root) {
+  CHECK_DEV(t); CHECK_CONTIG(t);
+  TORCH_CHECK(rccl_broadcast((void*)(intptr_t)comm, t.data_ptr(), t.numel(), rccl_dtype(t), root,
+                             stream()) == 0,
+              "ncclBroadcast: ", rccl_last_error((void*)(intptr_t)comm));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -291,4 +346,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("car_run", &car_run);
   m.def("car_error", [](int64_t h) { return car_error((void*)(intptr_t)h); });
   m.def("car_destroy", [](int64_t h) { car_destroy((void*)(intptr_t)h); });
+  m.def("nccl_unique_id", &nccl_unique_id);
+  m.def("nccl_init", &nccl_init);
+  m.def("nccl_all_reduce", &nccl_all_reduce);
+  m.def("nccl_all_gather", &nccl_all_gather);
+  m.def("nccl_reduce_scatter", &nccl_reduce_scatter);
+  m.def("nccl_broadcast", &nccl_broadcast);
+  m.def("nccl_destroy", [](int64_t c) { rccl_destroy((void*)(intptr_t)c); });
 }

@@ -91,7 +91,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
     if force or jobs_list or not KERNELS_SO.exists():
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o",
               str(KERNELS_SO), f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip",
-              "-ltorch_hip", "-ltorch_python", f"-Wl,-rpath,{tlib}"], verbose)
+              "-ltorch_hip", "-ltorch_python", "-L/opt/rocm/lib", "-lrccl", f"-Wl,-rpath,{tlib}",
+              "-Wl,-rpath,/opt/rocm/lib"], verbose)
     build_runtime(force, verbose)
     return KERNELS_SO
 

@@ -69,3 +69,17 @@ int car_allreduce(void* state, const void* inp, void* out, long long n_elems, in
                   int blocks, hipStream_t s);
 int car_error(void* state);
 void car_destroy(void* state);
+
+// rccl_comm.hip (K13): direct rccl.h wrapper; dtype 0 bf16, 1 f32, 2 i32, 3 f16; op 0 sum, 1 max, 2 min
+size_t rccl_unique_id_bytes();
+int rccl_get_unique_id(void* out);
+void* rccl_init(int world, int rank, const void* unique_id);
+int rccl_all_reduce(void* comm, const void* send, void* recv, size_t count, int dtype, int op,
+                    hipStream_t s);
+int rccl_all_gather(void* comm, const void* send, void* recv, size_t count, int dtype,
+                    hipStream_t s);
+int rccl_reduce_scatter(void* comm, const void* send, void* recv, size_t count, int dtype, int op,
+                        hipStream_t s);
+int rccl_broadcast(void* comm, void* buf, size_t count, int dtype, int root, hipStream_t s);
+const char* rccl_last_error(void* comm);
+void rccl_destroy(void* comm);

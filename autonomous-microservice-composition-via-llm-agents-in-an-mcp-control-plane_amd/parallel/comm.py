@@ -5,10 +5,15 @@ ROCm and runs over xGMI between the 8 MI355X of a node.  The CPU test tier
 uses ``gloo`` with the same code paths.
 
 * ``init_distributed``  – env:// rendezvous (torchrun), binds the local GPU.
+* ``NativeComm``        – K13: an RCCL communicator driven directly through
+  ``rccl.h`` (``csrc/rccl_comm.hip``) on the caller's HIP stream; the
+  ncclUniqueId is bootstrapped over the torch process group (C5).
 * ``make_allreduce``    – in-place sum for the row-parallel projections
-  (C1 after Wo, C2 after Wdown).  GPU: RCCL all-reduce, or the one-shot xGMI
-  peer-to-peer kernel of ``parallel.custom_allreduce`` for decode-sized
-  messages when enabled (``MCP_CUSTOM_ALLREDUCE=1``); CPU: gloo in fp32.
+  (C1 after Wo, C2 after Wdown).  GPU: the xGMI peer-to-peer kernel of
+  ``parallel.custom_allreduce`` for decode-sized messages when enabled
+  (``MCP_CUSTOM_ALLREDUCE=1``), else the native RCCL communicator
+  (``MCP_COMM=native``, default) or torch.distributed's (``MCP_COMM=torch``);
+  CPU: gloo in fp32.
 * ``StepBroadcaster``   – C4: the driver rank broadcasts each step's packed
   int32 descriptor (tokens, positions, slots, block tables, work lists, KV
   copy-on-write pairs) to the TP worker ranks.
@@ -39,6 +44,48 @@ def init_distributed(backend: Optional[str] = None):
     return rank, world, local_rank, device
 
 
+class NativeComm:
+    """Direct RCCL communicator over the ranks of ``group``."""
+
+    OPS = {"sum": 0, "max": 1, "min": 2}
+
+    def __init__(self, group, device):
+        from .. import ops
+        self._lib = ops.lib()
+        self.device = torch.device(device)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        obj = [self._lib.nccl_unique_id().numpy().tobytes() if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None
+                                   else 0, group=group)
+        uid = torch.frombuffer(bytearray(obj[0]), dtype=torch.uint8).clone()
+        with torch.cuda.device(self.device):
+            self._comm = self._lib.nccl_init(self.world, self.rank, uid)
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        self._lib.nccl_all_reduce(self._comm, t, self.OPS[op])
+        return t
+
+    def all_gather(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        out = t.new_empty((self.world,) + tuple(t.shape)) if out is None else out
+        self._lib.nccl_all_gather(self._comm, t.contiguous(), out)
+        return out
+
+    def reduce_scatter(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        out = t.new_empty((t.numel() // self.world,))
+        self._lib.nccl_reduce_scatter(self._comm, t.contiguous(), out, self.OPS[op])
+        return out
+
+    def broadcast(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        self._lib.nccl_broadcast(self._comm, t, root)
+        return t
+
+    def close(self):
+        if self._comm:
+            self._lib.nccl_destroy(self._comm)
+            self._comm = 0
+
+
 def make_allreduce(group, device) -> Callable[[torch.Tensor], None]:
     device = torch.device(device)
     if device.type != "cuda":
@@ -51,10 +98,13 @@ def make_allreduce(group, device) -> Callable[[torch.Tensor], None]:
     if os.environ.get("MCP_CUSTOM_ALLREDUCE", "0") == "1":
         from .custom_allreduce import CustomAllReduce
         custom = CustomAllReduce(group, device)
+    native = NativeComm(group, device) if os.environ.get("MCP_COMM", "native") == "native" else None
 
     def gpu_allreduce(t: torch.Tensor):
         if custom is not None and custom.eligible(t):
             custom(t)
+        elif native is not None:
+            native.all_reduce(t)
         else:
             dist.all_reduce(t, group=group)
     return gpu_allreduce
