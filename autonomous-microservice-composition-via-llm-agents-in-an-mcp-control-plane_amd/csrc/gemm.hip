@@ -196,6 +196,7 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
 
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s) {
+  if (M <= SKINNY_MAX_M && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;
   if (gemm_select(M, N, K) == 1)
     launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
   else
@@ -205,6 +206,7 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                          int algo, hipStream_t s) {
   if (algo < 0) launch_gemm_tn(X, W, Y, R, M, N, K, s);
+  else if (algo == 2 && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;
   else if (algo == 1) launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
   else launch_gemm_tn_128(X, W, Y, R, M, N, K, s);
 }
@@ -214,6 +216,7 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
                              hipStream_t s);
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (N % 64) return 1;
+  if (M <= SKINNY_MAX_M && launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0) return 0;
   if (gemm_select(M, N, K) == 1) {
     launch_gemm_tn_256_silu(X, W, Y, M, N, K, s);
   } else {

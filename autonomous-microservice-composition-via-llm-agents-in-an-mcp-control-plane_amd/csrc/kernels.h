@@ -19,13 +19,19 @@ void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
 void launch_copy_blocks(void* data, const int* src, const int* dst, int npairs, int layers2,
                         int nb, int block_elems, hipStream_t s);
 
+// gemm_skinny.hip (K2): decode-sized M, weight-streaming; epi 0 plain, 1 +R, 2 SwiGLU
+#define SKINNY_MAX_M 128
+int skinny_ok(int M, int N, int K, int epi);
+int launch_gemm_skinny(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                       int epi, hipStream_t s);
+
 // gemm.hip
 int gemm_tn_check(int M, int N, int K);
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s);
 void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         hipStream_t s);
-// algo: -1 auto, 0 = 128x128 two-barrier kernel, 1 = 256x256 multi-phase kernel
+// algo: -1 auto, 0 = 128x128 two-barrier kernel, 1 = 256x256 multi-phase kernel, 2 = skinny (K2)
 int gemm_select(int M, int N, int K);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);

@@ -304,3 +304,23 @@ def test_gemm_stream_k(M, N, K):
         y = ops.gemm_silu(X, Wi)
         e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
         assert rel_err(y, e) < 2e-2
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100, 128])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1280, 8192), (512, 384)])
+def test_gemm_skinny(M, N, K):
+    """K2 weight-streaming GEMM (decode-sized M) against fp32: plain, in-place
+    residual and fused SwiGLU."""
+    torch.manual_seed(5)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    assert rel_err(ops.gemm(X, W, algo=2), ref.gemm(X, W)) < 1e-2
+    assert rel_err(ops.gemm(X, W), ref.gemm(X, W)) < 1e-2
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    R2 = R.clone()
+    ops.gemm(X, W, R=R2, out=R2, algo=2)
+    assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+    g, u = W[: N // 2], W[N // 2:]
+    Wi = ref.interleave_gate_up(g, u).contiguous()
+    e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+    assert rel_err(ops.gemm_silu(X, Wi), e) < 2e-2
