@@ -131,9 +131,11 @@ class HostStager:
         self._ev = [None, None]
         self._i = 0
 
-    def to_device(self, host: np.ndarray) -> torch.Tensor:
+    def to_device(self, host: np.ndarray, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Async H2D of ``host``; into ``out`` (a static device buffer) when given."""
         if self.device is None or self.device.type != "cuda":
-            return torch.from_numpy(host)
+            t = torch.from_numpy(host)
+            return t if out is None else out[:t.numel()].copy_(t)
         i = self._i
         self._i ^= 1
         n = int(host.size)
@@ -145,7 +147,11 @@ class HostStager:
                             pin_memory=True)
             self._buf[i] = b
         np.copyto(b.numpy()[:n], host)
-        d = b[:n].to(self.device, non_blocking=True)
+        if out is not None:
+            d = out[:n]
+            d.copy_(b[:n], non_blocking=True)
+        else:
+            d = b[:n].to(self.device, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._ev[i] = ev

@@ -86,7 +86,8 @@ class _Launch:
 class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
-                 seed: int = 0, bcast=None, cascade: bool = True, pipeline: Optional[bool] = None):
+                 seed: int = 0, bcast=None, cascade: bool = True, pipeline: Optional[bool] = None,
+                 graphs: Optional[bool] = None):
         self.model = model
         cfg = model.cfg
         self.device = model.device
@@ -99,6 +100,9 @@ class LLMEngine:
         self._turn = 0
         self._next_cohort = 0
         self.stager = HostStager(self.device)
+        self._graphs_wanted = (self.device.type == "cuda" and bcast is None
+                               and getattr(model, "tp", 1) == 1) if graphs is None else graphs
+        self.graphs = None          # engine.graphs.GraphRunner, created after the KV cache
         if num_blocks is not None:
             self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
         else:
@@ -114,7 +118,10 @@ class LLMEngine:
         self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
         self.max_prefixes = 64
         self.steps = 0
-        self.stats = {"tokens": 0, "samples": 0, "steps": 0,
+        if self._graphs_wanted:
+            from .graphs import GraphRunner
+            self.graphs = GraphRunner(model, self.kv, temperature, seed)
+        self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
@@ -320,14 +327,22 @@ class LLMEngine:
                                          count=int(ptr[-1]))
             step.sample_ctr = np.asarray([(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF
                                           for q in sample_seqs], np.int32)
-        if pre_tokens > 0:
+        use_graph = (self.graphs is not None and not copies and T <= self.graphs.buckets[-1]
+                     and self.temperature == self.graphs.temperature)
+        if pre_tokens > 0 and not use_graph:
             step.kv_begin = np.asarray(kv_begin, np.int32)
             step.pre_bt = np.asarray(casc.blocks[:casc_keys // BLOCK_SIZE], np.int32)
             step.pre_tokens = pre_tokens
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
-        hidden, dstep = self._launch(step, copies)
-        tokens, event = self._sample(hidden, dstep, len(sample_seqs))
+        tok_dev = self.graphs.run(step) if use_graph else None
+        if tok_dev is not None:            # replayed hipGraph: forward + sampling
+            self.stats["graph_steps"] += 1
+            self.stats["samples"] += len(sample_seqs)
+            tokens, event = self._fetch(tok_dev[:len(sample_seqs)])
+        else:
+            hidden, dstep = self._launch(step, copies)
+            tokens, event = self._sample(hidden, dstep, len(sample_seqs))
         self.stats["launch_s"] += time.perf_counter() - t0
         self.stats["tokens"] += T
         self.stats["steps"] += 1
@@ -387,17 +402,24 @@ class LLMEngine:
 
     def _sample(self, hidden: torch.Tensor, dstep, n: int):
         """Fused LM-head-rows + grammar mask + Gumbel-max sampling (K9) on the
-        allowed sets that travelled with the step descriptor.  Returns the
-        host tensor the tokens land in and the event that marks their arrival
-        (asynchronous D2H into pinned memory)."""
+        allowed sets that travelled with the step descriptor.  The RNG counter
+        (request uid, sample index) makes every draw unique, so the seed is
+        constant (the same kernel runs inside captured hipGraphs)."""
         if n == 0:
             return None, None
         tok = ops.sample_allowed(hidden, self.model.w.lm_head, dstep.allow_ptr, dstep.allow_ids,
-                                 dstep.sample_ctr, self.temperature, self.seed + self.steps)
+                                 dstep.sample_ctr, self.temperature, self.seed)
         self.stats["samples"] += n
+        return self._fetch(tok)
+
+    @staticmethod
+    def _fetch(tok: torch.Tensor):
+        """Async D2H of sampled tokens into pinned memory + completion event."""
+        if tok.numel() == 0:
+            return None, None
         if not tok.is_cuda:
             return tok, None
-        host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        host = torch.empty(tok.numel(), dtype=torch.int32, pin_memory=True)
         host.copy_(tok, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()

@@ -155,11 +155,14 @@ def sample_allowed(hidden, W, allow_ptr, allow_ids, ctr, temperature, seed, out_
         lib().sample_allowed(hidden, W, allow_ptr, allow_ids, ctr, temperature, seed, out_tok,
                              out_logit)
         return out_tok
-    # CPU: same Gumbel-max semantics with torch's RNG
+    # CPU: same Gumbel-max semantics with torch's RNG, one stream per (seed, counter)
     toks = []
-    g = torch.Generator().manual_seed(int(seed))
-    for ids, logits in ref.sample_allowed_logits(hidden, W, allow_ptr, allow_ids):
+    for i, (ids, logits) in enumerate(ref.sample_allowed_logits(hidden, W, allow_ptr, allow_ids)):
+        if len(ids) == 0:
+            toks.append(-1)
+            continue
         if temperature > 0:
+            g = torch.Generator().manual_seed(int(seed) * 1_000_003 + int(ctr[i]))
             u = torch.rand(logits.shape, generator=g).clamp_(1e-7, 1 - 1e-7)
             sc = logits / temperature - torch.log(-torch.log(u))
         else:

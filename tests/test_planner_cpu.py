@@ -172,3 +172,49 @@ def test_pipelined_engine_matches_synchronous():
         out.append(planner.plan_many(intents))
         assert eng.alloc.num_free == eng.kv.num_blocks and not eng.inflight
     assert out[0] == out[1]
+
+
+def test_graph_static_layout_matches_dynamic():
+    """The fixed per-bucket layout used by captured hipGraphs (padding tokens,
+    empty dummy sequences, padded work lists and allowed sets) computes the same
+    hidden states and samples as the dynamic layout (CPU reference ops)."""
+    from mcp_amd import ops
+    from mcp_amd.engine.batch import StepInputs, pack, views
+    from mcp_amd.engine.graphs import GraphRunner
+    torch.manual_seed(0)
+    model = LlamaModel.random("tiny", "cpu", seed=2)
+    eng = LLMEngine(model, num_blocks=64, max_batch=8, temperature=0.0, graphs=False)
+    gr = GraphRunner(model, eng.kv, 0.0, 0)
+    rng = np.random.default_rng(0)
+    q_lens, ctx = [3, 1, 9], [3, 40, 9]
+    T = sum(q_lens)
+    blocks = [[0], [1], [2]]
+    ids = rng.integers(0, 1000, T).astype(np.int32)
+    pos = np.concatenate([np.arange(c - q, c) for q, c in zip(q_lens, ctx)]).astype(np.int32)
+    slots = np.concatenate([np.asarray(b)[p // 64] * 64 + p % 64 for b, p in
+                            zip(blocks, np.split(pos, np.cumsum(q_lens)[:-1]))]).astype(np.int32)
+    qs = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    rows = (qs + np.asarray(q_lens) - 1).astype(np.int32)
+    allowed = [[5, 9, 11], [7, 8], [1, 2, 3, 4]]
+    ptr = np.concatenate([[0], np.cumsum([len(a) for a in allowed])]).astype(np.int32)
+    step = StepInputs(token_ids=ids, positions=pos, slots=slots, q_start=qs,
+                      q_len=np.asarray(q_lens, np.int32), ctx_len=np.asarray(ctx, np.int32),
+                      block_table=np.asarray(blocks, np.int32), logit_rows=rows,
+                      allow_ptr=ptr, allow_ids=np.concatenate(allowed).astype(np.int32),
+                      sample_ctr=np.asarray([1, 2, 3], np.int32))
+    # make the cached context (positions before the new tokens) deterministic
+    eng.kv.data.normal_()
+    kv0 = eng.kv.data.clone()
+    d = pack(step, model.cfg.group, "cpu")
+    h_dyn = model.forward(d, eng.kv)
+    t_dyn = ops.sample_allowed(h_dyn, model.w.lm_head, d.allow_ptr, d.allow_ids, d.sample_ctr, 0.0, 0)
+    eng.kv.data.copy_(kv0)
+    b = gr.bucket_for(step)
+    assert b == 16
+    host = gr.pack_static(step, b)
+    ds = views(torch.from_numpy(host), gr._sizes(b) + [gr._caps(b)[0], 0])[0]
+    h_st = model.forward(ds, eng.kv)
+    t_st = ops.sample_allowed(h_st, model.w.lm_head, ds.allow_ptr, ds.allow_ids, ds.sample_ctr, 0.0, 0)
+    assert torch.allclose(h_st[:3].float(), h_dyn.float(), atol=1e-5)
+    assert t_st[:3].tolist() == t_dyn.tolist()
+    assert (t_st[3:] == -1).all()          # padded rows have empty allowed sets
