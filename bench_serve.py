@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Serving benchmarks (BASELINE.json configs 2 and 5).
+
+* ``single`` (config 2): Llama-3-8B TP=1, 10-service registry, ONE intent at a
+  time, intent -> DAG latency.  Reported twice: with the registry prompt's
+  prefix KV cached (the steady state of a server whose registry did not change)
+  and cold (registry prefix recomputed for every intent).
+* ``qps`` (config 5): open-loop Poisson arrivals at a fixed rate per GPU into
+  the continuously-batching engine (requests join and leave the running batch
+  every step; small steps replay captured hipGraphs).  Reports achieved
+  plans/s, p50 / p99 intent -> DAG latency (arrival to DAG) and batch stats.
+  For N GPUs run it under torchrun: every rank serves ``--qps`` on its own
+  replica (data parallel), the JSON line aggregates the node.
+
+Synthetic intents, random-init weights (no checkpoints offline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import mcp_amd  # noqa: E402,F401
+from mcp_amd.engine.engine import LLMEngine  # noqa: E402
+from mcp_amd.models.llama import LlamaModel  # noqa: E402
+from mcp_amd.orchestrator import validate_dag  # noqa: E402
+from mcp_amd.planner.local import LocalPlanner  # noqa: E402
+from mcp_amd.planner.prompt import synthetic_intent  # noqa: E402
+from mcp_amd.registry import MemoryRegistry, synthetic_registry  # noqa: E402
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def pct(xs, q):
+    return float(np.percentile(np.asarray(xs), q)) if xs else float("nan")
+
+
+def run_single(planner, n, warm):
+    lat = []
+    for i in range(n):
+        t = time.perf_counter()
+        planner.plan_many([synthetic_intent(10_000 + i)], fresh_prefix=not warm)
+        lat.append(time.perf_counter() - t)
+    return lat
+
+
+def run_qps(planner, engine, qps, duration, seed, rank):
+    rng = np.random.default_rng(seed + 7919 * rank)
+    n = max(1, int(qps * duration))
+    arrivals = np.cumsum(rng.exponential(1.0 / qps, n))
+    services = planner.registry.list_services()
+    lat, dags = [], []
+    done_at = {}
+    t0 = time.perf_counter()
+    i = 0
+    batch_sizes = []
+    while i < n or engine.has_work():
+        now = time.perf_counter() - t0
+        while i < n and arrivals[i] <= now:
+            dec, ptoks, stoks = planner.prepare(synthetic_intent(rank * 1_000_000 + i), services)
+            arr = arrivals[i]
+
+            def on_done(seq, arr=arr):
+                done_at[seq.uid] = (time.perf_counter() - t0, arr, seq.result)
+            engine.submit(dec, stoks, prefix_tokens=ptoks, on_done=on_done)
+            i += 1
+        if engine.has_work():
+            batch_sizes.append(len(engine.running))
+            engine.step()
+        elif i < n:
+            time.sleep(max(0.0, min(arrivals[i] - (time.perf_counter() - t0), 0.002)))
+    elapsed = time.perf_counter() - t0
+    for t_done, arr, res in done_at.values():
+        lat.append(t_done - arr)
+        dags.append(res)
+    return lat, dags, elapsed, n, batch_sizes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["single", "qps"])
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--services", type=int, default=10)
+    ap.add_argument("--n", type=int, default=20, help="single: intents per measurement")
+    ap.add_argument("--qps", type=float, default=20.0, help="qps: arrival rate per GPU")
+    ap.add_argument("--duration", type=float, default=20.0)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--min-nodes", type=int, default=5)
+    ap.add_argument("--max-nodes", type=int, default=5)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    model = LlamaModel.random(args.model, dev, seed=args.seed)
+    engine = LLMEngine(model, max_batch=512, max_step_tokens=16384, temperature=0.2,
+                       seed=args.seed + rank, graphs=False if args.no_graphs else None)
+    reg = MemoryRegistry(synthetic_registry(args.services, seed=1))
+    names = [s.name for s in reg.list_services()]
+    planner = LocalPlanner(engine, reg, max_nodes=args.max_nodes, min_nodes=args.min_nodes)
+    planner.plan_many([synthetic_intent(-1 - i) for i in range(max(1, args.warmup))])
+
+    out = {"n_gpus": world, "model": args.model, "services": args.services, "dtype": "bf16",
+           "data": "synthetic intents, random-init weights",
+           "nodes_per_plan": [args.min_nodes, args.max_nodes]}
+    if args.mode == "single":
+        run_single(planner, args.warmup, warm=True)         # warms the hipGraph buckets too
+        warm = run_single(planner, args.n, warm=True)
+        cold = run_single(planner, args.n, warm=False)
+        out.update(metric="single-intent intent->DAG latency (config 2)",
+                   p50_warm_prefix_ms=round(statistics.median(warm) * 1e3, 2),
+                   p90_warm_prefix_ms=round(pct(warm, 90) * 1e3, 2),
+                   p50_cold_prefix_ms=round(statistics.median(cold) * 1e3, 2),
+                   graph_steps=engine.stats["graph_steps"], steps=engine.stats["steps"])
+    else:
+        if world > 1:
+            dist.barrier()
+        lat, dags, elapsed, n, bs = run_qps(planner, engine, args.qps, args.duration, args.seed, rank)
+        for d in dags:
+            validate_dag(d, names)
+        v = torch.tensor([len(lat) / elapsed, statistics.median(lat), pct(lat, 99),
+                          float(np.mean(bs)) if bs else 0.0], dtype=torch.float64, device=dev)
+        if world > 1:
+            tot = v.clone()
+            dist.all_reduce(tot)
+            mx = v.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            plans_s, p50, p99, mean_b = float(tot[0]), float(mx[1]), float(mx[2]), float(tot[3]) / world
+        else:
+            plans_s, p50, p99, mean_b = (float(x) for x in v)
+        out.update(metric="plans/sec at fixed QPS (config 5)", offered_qps=args.qps * world,
+                   value=round(plans_s, 2), unit="plans/s", p50_latency_ms=round(p50 * 1e3, 1),
+                   p99_latency_ms=round(p99 * 1e3, 1), mean_running_batch=round(mean_b, 1),
+                   graph_steps=engine.stats["graph_steps"], steps=engine.stats["steps"],
+                   duration_s=args.duration)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
