@@ -23,7 +23,7 @@ import logging
 from typing import Optional
 
 import httpx
-from fastapi import FastAPI
+from fastapi import FastAPI, HTTPException
 from fastapi.responses import PlainTextResponse
 from pydantic import BaseModel
 
@@ -96,9 +96,17 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
     app.state.settings = settings
     app.state.components = state
 
+    async def _plan(intent: str) -> dict:
+        try:
+            return await state["planner"].plan(intent)
+        except RuntimeError as e:
+            if type(e).__name__ == "EngineStalled":       # hung GPU step: retry elsewhere
+                raise HTTPException(status_code=503, detail=str(e))
+            raise
+
     @app.post("/plan", response_model=PlanResponse)
     async def plan_intent(req: PlanRequest):
-        return PlanResponse(graph=await state["planner"].plan(req.intent))
+        return PlanResponse(graph=await _plan(req.intent))
 
     @app.post("/execute", response_model=ExecuteResponse)
     async def run_graph(req: ExecuteRequest):
@@ -106,7 +114,7 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
 
     @app.post("/plan_and_execute", response_model=ExecuteResponse)
     async def plan_and_run(req: PlanRequest):
-        graph = PlanResponse(graph=await state["planner"].plan(req.intent)).graph
+        graph = PlanResponse(graph=await _plan(req.intent)).graph
         return ExecuteResponse(**await state["orch"].execute(graph, {}))
 
     @app.get("/metrics", response_class=PlainTextResponse)
@@ -115,6 +123,8 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
 
     @app.get("/healthz")
     async def healthz():
+        if getattr(state["planner"], "stalled", False):
+            raise HTTPException(status_code=503, detail="planner engine stalled")
         return {"ok": True, "services": len(registry.list_services())}
 
     return app

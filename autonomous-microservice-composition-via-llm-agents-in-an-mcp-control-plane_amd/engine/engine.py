@@ -31,6 +31,7 @@ import torch
 
 from .. import ops
 from ..utils.metrics import METRICS
+from ..utils.tracing import span
 from .batch import BLOCK_SIZE, HostStager, StepInputs, pack_host, views
 from .kv_cache import KVCache
 
@@ -61,6 +62,7 @@ class Sequence:
         self.error: Optional[str] = None
         self.on_done = on_done
         self.t_submit = time.perf_counter()
+        self.t_admit = None
         self.t_first = None
         self.t_done = None
         self.is_prefix_job = decoder is None
@@ -97,6 +99,7 @@ class LLMEngine:
         # while the GPU runs the other's forward (no idle GPU between steps)
         self.pipeline = (self.device.type == "cuda") if pipeline is None else pipeline
         self.inflight: Dict[int, _Launch] = {}
+        self.last_progress = time.perf_counter()   # watched by the planner's stall watchdog
         self._turn = 0
         self._next_cohort = 0
         self.stager = HostStager(self.device)
@@ -181,6 +184,8 @@ class LLMEngine:
             seq = Sequence(decoder, list(prefix_tokens or []) + list(prompt_tokens), None, on_done)
         seq.cohort = self._next_cohort
         self._next_cohort ^= 1
+        if not self.has_work():
+            self.last_progress = time.perf_counter()
         self.waiting.append(seq)
         return seq
 
@@ -190,7 +195,9 @@ class LLMEngine:
     # ---------------------------------------------------------------- step
     def _admit(self):
         while self.waiting and len(self.running) < self.max_batch:
-            self.running.append(self.waiting.pop(0))
+            seq = self.waiting.pop(0)
+            seq.t_admit = time.perf_counter()
+            self.running.append(seq)
 
     def _ensure_blocks(self, seq: Sequence, total_tokens: int):
         need = (total_tokens + BLOCK_SIZE - 1) // BLOCK_SIZE - len(seq.blocks)
@@ -210,6 +217,12 @@ class LLMEngine:
             except Exception as e:  # pragma: no cover - grammar guarantees JSON
                 seq.error = repr(e)
             METRICS.plan_done(seq.t_done - seq.t_submit)
+            # per-request phases: queue (submit -> admitted), first sampled token, total
+            if seq.t_admit is not None:
+                METRICS.observe("queue_s", seq.t_admit - seq.t_submit)
+            if seq.t_first is not None:
+                METRICS.observe("ttft_s", seq.t_first - seq.t_submit)
+            METRICS.inc("sampled_tokens", seq.n_samples)
         if seq.on_done is not None:
             seq.on_done(seq)
 
@@ -221,19 +234,25 @@ class LLMEngine:
         fed to the grammar) while the GPU is still busy with cohort c^1's
         forward, then cohort c is scheduled and launched asynchronously."""
         if not self.pipeline:
-            L = self._schedule_launch(None)
+            with span("engine.launch"):
+                L = self._schedule_launch(None)
             if L is None:
                 return 0
-            self._retire(L)
+            with span("engine.retire"):
+                self._retire(L)
+            self.last_progress = time.perf_counter()
             return L.T
         c = self._turn
         self._turn ^= 1
         done = 0
         L = self.inflight.pop(c, None)
         if L is not None:
-            self._retire(L)
+            with span("engine.retire"):
+                self._retire(L)
             done = L.T
-        nxt = self._schedule_launch(c)
+            self.last_progress = time.perf_counter()
+        with span("engine.launch"):
+            nxt = self._schedule_launch(c)
         if nxt is not None:
             self.inflight[c] = nxt
             return done + nxt.T

@@ -33,9 +33,15 @@ from .prompt import build_prompt_parts
 from .tokenizer import get_tokenizer
 
 
+class EngineStalled(RuntimeError):
+    """The engine made no progress for ``watchdog_s`` with requests pending
+    (e.g. a hung GPU step); the API answers 503 and the router drains the replica."""
+
+
 class LocalPlanner(Planner):
     def __init__(self, engine, registry, tokenizer=None, max_nodes: int = 6, retriever=None,
-                 retrieval_threshold: int = 48, topk: int = 32, min_nodes: int = 1):
+                 retrieval_threshold: int = 48, topk: int = 32, min_nodes: int = 1,
+                 watchdog_s: Optional[float] = None):
         self.engine = engine
         self.registry = registry
         self.tok = tokenizer or get_tokenizer()
@@ -50,6 +56,12 @@ class LocalPlanner(Planner):
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self._lock = threading.Lock()
+        self.watchdog_s = float(os.environ.get("MCP_WATCHDOG_S", "60")) if watchdog_s is None \
+            else watchdog_s
+        self._pending: Dict[int, tuple] = {}        # id -> (loop, future), async requests in flight
+        self._pending_lock = threading.Lock()
+        self._watchdog: Optional[threading.Thread] = None
+        self.stalled = False
 
     # ----------------------------------------------------------- factory
     @classmethod
@@ -120,6 +132,27 @@ class LocalPlanner(Planner):
         if self._thread is None or not self._thread.is_alive():
             self._thread = threading.Thread(target=self._loop, name="mcp-engine", daemon=True)
             self._thread.start()
+        if self.watchdog_s > 0 and (self._watchdog is None or not self._watchdog.is_alive()):
+            self._watchdog = threading.Thread(target=self._watch, name="mcp-watchdog", daemon=True)
+            self._watchdog.start()
+
+    def _watch(self):
+        """Fail every pending request if the engine stops making progress."""
+        period = min(1.0, self.watchdog_s / 4)
+        while not self._stop.wait(period):
+            with self._pending_lock:
+                busy = bool(self._pending)
+            if not busy or self.stalled:
+                continue
+            idle = time.perf_counter() - self.engine.last_progress
+            if idle > self.watchdog_s:
+                self.stalled = True
+                METRICS.inc("engine_stalls")
+                with self._pending_lock:
+                    items, self._pending = list(self._pending.values()), {}
+                err = EngineStalled(f"planner engine made no progress for {idle:.1f}s")
+                for loop, fut in items:
+                    loop.call_soon_threadsafe(_set_exc, fut, err)
 
     def _loop(self):
         eng = self.engine
@@ -137,6 +170,8 @@ class LocalPlanner(Planner):
 
                     def done(seq, loop=loop, fut=fut, t0=t0):
                         METRICS.observe("engine_latency_s", time.perf_counter() - t0)
+                        with self._pending_lock:
+                            self._pending.pop(id(fut), None)
                         if seq.error:
                             loop.call_soon_threadsafe(_set_exc, fut, RuntimeError(seq.error))
                         else:
@@ -153,9 +188,13 @@ class LocalPlanner(Planner):
                     eng.step()
 
     async def plan(self, intent: str) -> dict:
+        if self.stalled:
+            raise EngineStalled("planner engine is stalled")
         self._ensure_thread()
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
+        with self._pending_lock:
+            self._pending[id(fut)] = (loop, fut)
         self._q.put((intent, loop, fut))
         return await fut
 

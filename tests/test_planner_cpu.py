@@ -218,3 +218,28 @@ def test_graph_static_layout_matches_dynamic():
     assert torch.allclose(h_st[:3].float(), h_dyn.float(), atol=1e-5)
     assert t_st[:3].tolist() == t_dyn.tolist()
     assert (t_st[3:] == -1).all()          # padded rows have empty allowed sets
+
+
+def test_engine_stall_watchdog_returns_503():
+    """A step that stops making progress (hung GPU) fails pending requests with
+    EngineStalled -> HTTP 503, and /healthz reports the replica unhealthy."""
+    import time as _time
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    eng = LLMEngine(model, num_blocks=128, max_batch=4)
+    reg = MemoryRegistry(synthetic_registry(3, seed=5))
+    planner = LocalPlanner(eng, reg, max_nodes=2, watchdog_s=0.3)
+    real_step = eng.step
+
+    def hung_step():
+        _time.sleep(1.5)
+        return real_step()
+    eng.step = hung_step
+
+    def h(request):
+        return httpx.Response(200, json={})
+    app = create_app(Settings(), registry=reg, planner=planner, transport=httpx.MockTransport(h))
+    with TestClient(app) as c:
+        r = c.post("/plan", json={"intent": "charge the order"})
+        assert r.status_code == 503
+        assert c.get("/healthz").status_code == 503
+    planner._stop.set()
