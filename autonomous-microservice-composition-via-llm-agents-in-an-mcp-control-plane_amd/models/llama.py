@@ -160,7 +160,7 @@ class LlamaModel:
     """Stateless forward over weights + an external paged KV cache."""
 
     def __init__(self, cfg: LlamaConfig, weights: LlamaWeights, device, tp_rank: int = 0,
-                 tp: int = 1, tp_group=None):
+                 tp: int = 1, tp_group=None, allreduce=None):
         self.cfg = cfg
         self.w = weights
         self.device = torch.device(device)
@@ -170,8 +170,8 @@ class LlamaModel:
         self.hq, self.hkv = cfg.heads // tp, cfg.kv_heads // tp
         self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
-        self._allreduce = None
-        if tp > 1:
+        self._allreduce = allreduce      # injectable (simulated ranks in tests)
+        if tp > 1 and allreduce is None:
             from ..parallel.comm import make_allreduce
             self._allreduce = make_allreduce(tp_group, self.device)
 
