@@ -80,6 +80,7 @@ class GrammarSpec:
         self.names = [s["name"] for s in self.services]
         self.keys = [self._input_keys(s) for s in self.services]
         self._trie_cache: Dict[Tuple[str, ...], Trie] = {}
+        self._enc_cache: Dict[str, List[int]] = {}      # forced spans repeat across requests
         self.name_trie = self.trie(tuple(json.dumps(n) for n in self.names))
 
     @staticmethod
@@ -90,7 +91,12 @@ class GrammarSpec:
         return [k for k in sch.keys() if k not in ("type", "required", "$schema", "title")]
 
     def encode(self, text: str) -> List[int]:
-        return self.tok.encode(text)
+        t = self._enc_cache.get(text)
+        if t is None:
+            t = self.tok.encode(text)
+            if len(self._enc_cache) < 65536:
+                self._enc_cache[text] = t
+        return list(t)
 
     def trie(self, alts: Tuple[str, ...]) -> Trie:
         t = self._trie_cache.get(alts)
