@@ -445,6 +445,10 @@ bool sk_plan(int M, int N, int K, int G, int mode, SkPlan& p) {
   p.dp_tiles = p.dp_waves * G;
   p.sk_tiles = tiles - p.dp_tiles;
   p.S = (long long)p.sk_tiles * p.nk;
+  // every workgroup of the stream-K phase must own >= 1 iteration (an empty
+  // range would be counted as a contributor and the tile never completes);
+  // S >= G whenever a data-parallel wave exists, so this only shrinks tiny grids
+  if (p.S < p.G) p.G = (int)p.S;
   return p.sk_tiles <= 4 * G;
 }
 
