@@ -63,7 +63,9 @@ DEV void sched_barrier_full() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
-using V256Default = V256<false, false, false, true>;   // variant 8: best of the 16-way sweep
+// production default: ping-pong (variant 24), +4-10 % over the best non-staggered
+// variant 8 on the Llama-3-8B projection shapes (profiles/gemm_tuning.md)
+using V256Default = V256<false, false, true, true, true>;
 
 // Grouped tile order: GROUP M-tiles share each W column panel in L2.
 DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
@@ -301,58 +303,66 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256_sk(const bf16* __restrict_
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   const int b = xcd_remap(blockIdx.x, plan.G);
   f32x4 acc[2][4][4];
-  int m0, n0;
-  for (int w = 0; w < plan.dp_waves; ++w) {
-    tile_coords(w * plan.G + b, nm, nn, m0, n0);
-    mainloop<VAR>(X, W, M, N, K, m0, n0, 0, plan.nk, smem, acc);
-    epilogue<EPI>(Y, R, M, N, m0, n0, acc);
-  }
-  const long long it_end = sk_begin(b + 1, plan);
-  long long it = sk_begin(b, plan);
   f32x4* wsv = reinterpret_cast<f32x4*>(ws);
-  while (it < it_end) {
-    const int st = (int)(it / plan.nk);                 // stream-K tile index
-    const long long t_start = (long long)st * plan.nk, t_end = t_start + plan.nk;
-    const int k0 = (int)(it - t_start);
-    const int k1 = (int)(min(it_end, t_end) - t_start);
-    tile_coords(plan.dp_tiles + st, nm, nn, m0, n0);
-    mainloop<VAR>(X, W, M, N, K, m0, n0, k0, k1, smem, acc);
-    if (k0 == 0 && k1 == plan.nk) {                     // whole tile in one workgroup
-      epilogue<EPI>(Y, R, M, N, m0, n0, acc);
-      it = t_end;
-      continue;
+  // one loop over this workgroup's work units (whole data-parallel tiles, then
+  // its stream-K range) with a single mainloop / epilogue instance each
+  int w = 0;
+  long long it = sk_begin(b, plan);
+  const long long it_end = sk_begin(b + 1, plan);
+  while (true) {
+    int t, k0, k1, st = 0;
+    long long t_start = 0, t_end = 0;
+    if (w < plan.dp_waves) {
+      t = w * plan.G + b;
+      k0 = 0;
+      k1 = plan.nk;
+      ++w;
+    } else if (it < it_end) {
+      st = (int)(it / plan.nk);
+      t_start = (long long)st * plan.nk;
+      t_end = t_start + plan.nk;
+      k0 = (int)(it - t_start);
+      k1 = (int)(min(it_end, t_end) - t_start);
+      t = plan.dp_tiles + st;
+      it = min(it_end, t_end);
+    } else {
+      break;
     }
-    // contributors: workgroups whose ranges intersect [t_start, t_end)
-    int c0 = (int)(t_start * plan.G / plan.S);
-    while (c0 > 0 && sk_begin(c0, plan) > t_start) --c0;
-    while (sk_begin(c0 + 1, plan) <= t_start) ++c0;
-    int c1 = c0;
-    while (c1 + 1 < plan.G && sk_begin(c1 + 1, plan) < t_end) ++c1;
-    const int slot = sk_begin(b, plan) < t_start ? 1 : 0;
-    f32x4* mine = wsv + (size_t)(b * 2 + slot) * 32 * 512;
+    int m0, n0;
+    tile_coords(t, nm, nn, m0, n0);
+    mainloop<VAR>(X, W, M, N, K, m0, n0, k0, k1, smem, acc);
+    if (k0 != 0 || k1 != plan.nk) {
+      // contributors: workgroups whose ranges intersect [t_start, t_end)
+      int c0 = (int)(t_start * plan.G / plan.S);
+      while (c0 > 0 && sk_begin(c0, plan) > t_start) --c0;
+      while (sk_begin(c0 + 1, plan) <= t_start) ++c0;
+      int c1 = c0;
+      while (c1 + 1 < plan.G && sk_begin(c1 + 1, plan) < t_end) ++c1;
+      const int slot = sk_begin(b, plan) < t_start ? 1 : 0;
+      f32x4* mine = wsv + (size_t)(b * 2 + slot) * 32 * 512;
 #pragma unroll
-    for (int q = 0; q < 32; ++q) mine[q * 512 + threadIdx.x] = (&acc[0][0][0])[q];
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
-      s_last = __hip_atomic_fetch_add(cnt + st, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-               c1 - c0;
-    __syncthreads();
-    if (s_last) {
+      for (int q = 0; q < 32; ++q) mine[q * 512 + threadIdx.x] = (&acc[0][0][0])[q];
       __threadfence();
-      f32x4 tot[2][4][4];
+      __syncthreads();
+      if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(cnt + st, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                 c1 - c0;
+      __syncthreads();
+      if (!s_last) continue;
+      __threadfence();
+      // sum every contributor's partial (own included) in contributor order,
+      // reusing acc as the accumulator (no second 128-register array)
 #pragma unroll
-      for (int q = 0; q < 32; ++q) (&tot[0][0][0])[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < 32; ++q) (&acc[0][0][0])[q] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int c = c0; c <= c1; ++c) {
         const int cs = sk_begin(c, plan) < t_start ? 1 : 0;
         const f32x4* src = wsv + (size_t)(c * 2 + cs) * 32 * 512;
 #pragma unroll
-        for (int q = 0; q < 32; ++q) (&tot[0][0][0])[q] += src[q * 512 + threadIdx.x];
+        for (int q = 0; q < 32; ++q) (&acc[0][0][0])[q] += src[q * 512 + threadIdx.x];
       }
-      epilogue<EPI>(Y, R, M, N, m0, n0, tot);
       if (threadIdx.x == 0) cnt[st] = 0;
     }
-    it = min(it_end, t_end);
+    epilogue<EPI>(Y, R, M, N, m0, n0, acc);
   }
 }
 
@@ -394,9 +404,9 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 24: launch_var<V256PingPong>(X, W, Y, M, N, K, s); return 0;
     case 25: launch_var<V256<false, false, false, true, true>>(X, W, Y, M, N, K, s); return 0;
     case 26: launch_var<V256<false, true, true, true, true>>(X, W, Y, M, N, K, s); return 0;
-    case 30: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 1, 0, s);   // data-parallel
-    case 31: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 0, s);   // stream-K forced
-    case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 0, s);   // auto
+    case 30: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 1, 1, s);   // data-parallel
+    case 31: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 0, s);   // stream-K, variant 8 body
+    case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 1, s);   // auto (production)
     case 33: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 1, s);   // stream-K + ping-pong
     default: return 1;
   }
@@ -497,7 +507,7 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
 int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N, int K, int mode,
                             int pingpong, hipStream_t s) {
   if (pingpong) launch_256<0, V256PingPong>(X, W, Y, nullptr, M, N, K, mode, s);
-  else launch_256<0>(X, W, Y, nullptr, M, N, K, mode, s);
+  else launch_256<0, V256<false, false, false, true>>(X, W, Y, nullptr, M, N, K, mode, s);
   return 0;
 }
 

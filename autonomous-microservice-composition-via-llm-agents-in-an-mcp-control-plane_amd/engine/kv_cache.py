@@ -71,7 +71,7 @@ class KVCache:
                  dtype=torch.bfloat16):
         self.layers, self.kv_heads, self.head_dim = layers, kv_heads, head_dim
         self.num_blocks = num_blocks
-        self.data = torch.empty(layers, 2, num_blocks, kv_heads, BLOCK_SIZE, head_dim,
+        self.data = torch.zeros(layers, 2, num_blocks, kv_heads, BLOCK_SIZE, head_dim,
                                 device=device, dtype=dtype)
         self.allocator = make_allocator(num_blocks)
 

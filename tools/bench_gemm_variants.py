@@ -8,7 +8,7 @@ L = ops.lib()
 dev = 'cuda'
 shapes = [(3584, 6144, 4096), (3584, 4096, 4096), (3584, 28672, 4096), (3584, 4096, 14336),
           (4096, 4096, 4096), (1792, 6144, 4096)]
-variants = [int(v) for v in sys.argv[1].split(',')] if len(sys.argv) > 1 else [8, 24, 30, 31, 32, 33]
+variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [8, 24, 30, 31, 32, 33]
 rounds = 3
 res = {}
 for (M, N, K) in shapes:
