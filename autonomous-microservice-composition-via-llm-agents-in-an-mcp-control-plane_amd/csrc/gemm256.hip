@@ -96,10 +96,15 @@ DEV void mainloop(const bf16* __restrict__ X, const bf16* __restrict__ W, int M,
     srcA[j] = X + (size_t)min(m0 + row, M - 1) * K + ch * 8;
     srcB[j] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
   }
-  auto stage = [&](int t, int i) {          // piece i of K-tile t
+  // t counts K-tiles from kt0 (slot parity t & 1 is then static after the
+  // compiler's unrolling, which keeps its LDS-DMA alias tracking from adding a
+  // vmcnt(0) before every ds_read)
+  const bf16* const kbaseA[2] = {srcA[0] + (size_t)kt0 * BK, srcA[1] + (size_t)kt0 * BK};
+  const bf16* const kbaseB[2] = {srcB[0] + (size_t)kt0 * BK, srcB[1] + (size_t)kt0 * BK};
+  auto stage = [&](int t, int i) {          // piece i of K-tile kt0 + t
     const int koff = t * BK + (i >> 1) * KH;
     bf16* slot = smem + ((t & 1) * 4 + i) * PIECE;
-    const bf16* const* src = (i & 1) ? srcB : srcA;
+    const bf16* const* src = (i & 1) ? kbaseB : kbaseA;
 #pragma unroll
     for (int j = 0; j < 2; ++j) glds16(src[j] + koff, slot + (2 * wave + j) * 512);
   };
@@ -131,7 +136,7 @@ DEV void mainloop(const bf16* __restrict__ X, const bf16* __restrict__ W, int M,
   barrier();
   // prologue: K-tile kt0 fully resident
 #pragma unroll
-  for (int i = 0; i < 4; ++i) stage(kt0, i);
+  for (int i = 0; i < 4; ++i) stage(0, i);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   barrier();
 
@@ -194,14 +199,15 @@ DEV void mainloop(const bf16* __restrict__ X, const bf16* __restrict__ W, int M,
   };
 
   if (VAR::pp && wm == 1) sched_barrier_full();    // stagger the two wave groups
-  for (int t = kt0; t + 1 < kt1; ++t) {
+  const int nt = kt1 - kt0;
+  for (int t = 0; t + 1 < nt; ++t) {
     phase(t, 0, true, false);
     phase(t, 1, true, false);
     phase(t, 2, true, false);
     phase(t, 3, true, false);
   }
   {
-    const int t = kt1 - 1;
+    const int t = nt - 1;
     phase(t, 0, false, true);
     phase(t, 1, false, true);
     phase(t, 2, false, true);
@@ -272,98 +278,67 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_256(const bf16* __restrict__ X
 }
 
 // ---------------------------------------------------------------------------
-// Stream-K hybrid (fixes wave quantisation: 336 tiles on 256 CUs run as 2
-// waves at 66 % occupancy).  A persistent grid of G workgroups (one per CU)
-// first runs `dp_waves` full waves of whole tiles, then splits the remaining
-// tiles' K-iterations evenly: workgroup b owns iterations
-// [b*S/G, (b+1)*S/G) of the S = sk_tiles * nk remaining ones.  A tile split
-// across workgroups is finished by the LAST contributor to arrive: every
-// contributor stores its fp32 partial (register order, coalesced float4) to
-// its own workspace slot, releases it (agent-scope fence: the 8 XCD L2s are
-// not coherent) and bumps the tile's arrival counter; the one that sees
-// count == contributors - 1 sums all partials in contributor order
+// Split-K for wave quantisation: 336 tiles on 256 CUs run as 2 waves at 66 %
+// occupancy.  Splitting every tile's K range into s parts gives tiles*s
+// workgroups of 1/s tile each; s is chosen to minimise ceil(tiles*s/G)/s
+// (3 for 336 tiles: 1.33 tile-times instead of 2).  Each workgroup runs ONE
+// mainloop (a loop around it makes the compiler's LDS-DMA alias tracking put
+// a vmcnt(0) before every ds_read), stores its fp32 partial (register order,
+// coalesced float4) to its workspace slot, releases it (agent-scope fence:
+// the 8 XCD L2s are not coherent) and bumps the tile's arrival counter; the
+// last of the s contributors to arrive sums the partials in split order
 // (deterministic), applies the epilogue and re-arms the counter.
-struct SkPlan {
-  int G, dp_waves, dp_tiles, sk_tiles, nk;
-  long long S;
-};
-
-DEV long long sk_begin(int b, const SkPlan& p) { return (long long)b * p.S / p.G; }
-
 template <int EPI, class VAR = V256Default>
-__global__ __launch_bounds__(512, 1) void gemm_tn_256_sk(const bf16* __restrict__ X,
-                                                         const bf16* __restrict__ W,
-                                                         bf16* __restrict__ Y,
-                                                         const bf16* __restrict__ R, int M, int N,
-                                                         int K, SkPlan plan,
-                                                         float* __restrict__ ws,
-                                                         int* __restrict__ cnt) {
+__global__ __launch_bounds__(512, 1) void gemm_tn_256_splitk(const bf16* __restrict__ X,
+                                                             const bf16* __restrict__ W,
+                                                             bf16* __restrict__ Y,
+                                                             const bf16* __restrict__ R, int M,
+                                                             int N, int K, int splits,
+                                                             float* __restrict__ ws,
+                                                             int* __restrict__ cnt) {
+  // ONE __shared__ array: a second LDS object (even the 4-byte last-arriver
+  // flag) makes hipcc put vmcnt(0) before every ds_read of the K-loop
+  // (cdna_hip_programming.md §5 "Three .s-level traps" (a))
   __shared__ __attribute__((aligned(16))) bf16 smem[8 * PIECE];
-  __shared__ int s_last;
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const int b = xcd_remap(blockIdx.x, plan.G);
+  // splits of one tile are consecutive logical ids -> same XCD (shared L2 for the fixup)
+  const int lid = xcd_remap(blockIdx.x, nm * nn * splits);
+  const int t = lid / splits, sp = lid % splits;
+  const int nk = K / BK;
+  const int k0 = (int)((long long)sp * nk / splits), k1 = (int)((long long)(sp + 1) * nk / splits);
+  int m0, n0;
+  tile_coords(t, nm, nn, m0, n0);
   f32x4 acc[2][4][4];
-  f32x4* wsv = reinterpret_cast<f32x4*>(ws);
-  // one loop over this workgroup's work units (whole data-parallel tiles, then
-  // its stream-K range) with a single mainloop / epilogue instance each
-  int w = 0;
-  long long it = sk_begin(b, plan);
-  const long long it_end = sk_begin(b + 1, plan);
-  while (true) {
-    int t, k0, k1, st = 0;
-    long long t_start = 0, t_end = 0;
-    if (w < plan.dp_waves) {
-      t = w * plan.G + b;
-      k0 = 0;
-      k1 = plan.nk;
-      ++w;
-    } else if (it < it_end) {
-      st = (int)(it / plan.nk);
-      t_start = (long long)st * plan.nk;
-      t_end = t_start + plan.nk;
-      k0 = (int)(it - t_start);
-      k1 = (int)(min(it_end, t_end) - t_start);
-      t = plan.dp_tiles + st;
-      it = min(it_end, t_end);
-    } else {
-      break;
+  mainloop<VAR>(X, W, M, N, K, m0, n0, k0, k1, smem, acc);
+  f32x4* wsv = reinterpret_cast<f32x4*>(ws) + (size_t)t * splits * 32 * 512;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) wsv[((size_t)sp * 32 + q) * 512 + threadIdx.x] = (&acc[0][0][0])[q];
+  // publish (guide §5 "Projection GEMM at M = 256" item 2): drain, one agent
+  // release by lane 0, ticket; the last arriver acquires once and reduces
+  int* flag = reinterpret_cast<int*>(smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == splits - 1;
+    if (prev == splits - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cnt[t] = 0;                               // re-arm for the next launch
     }
-    int m0, n0;
-    tile_coords(t, nm, nn, m0, n0);
-    mainloop<VAR>(X, W, M, N, K, m0, n0, k0, k1, smem, acc);
-    if (k0 != 0 || k1 != plan.nk) {
-      // contributors: workgroups whose ranges intersect [t_start, t_end)
-      int c0 = (int)(t_start * plan.G / plan.S);
-      while (c0 > 0 && sk_begin(c0, plan) > t_start) --c0;
-      while (sk_begin(c0 + 1, plan) <= t_start) ++c0;
-      int c1 = c0;
-      while (c1 + 1 < plan.G && sk_begin(c1 + 1, plan) < t_end) ++c1;
-      const int slot = sk_begin(b, plan) < t_start ? 1 : 0;
-      f32x4* mine = wsv + (size_t)(b * 2 + slot) * 32 * 512;
-#pragma unroll
-      for (int q = 0; q < 32; ++q) mine[q * 512 + threadIdx.x] = (&acc[0][0][0])[q];
-      __threadfence();
-      __syncthreads();
-      if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(cnt + st, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-                 c1 - c0;
-      __syncthreads();
-      if (!s_last) continue;
-      __threadfence();
-      // sum every contributor's partial (own included) in contributor order,
-      // reusing acc as the accumulator (no second 128-register array)
-#pragma unroll
-      for (int q = 0; q < 32; ++q) (&acc[0][0][0])[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int c = c0; c <= c1; ++c) {
-        const int cs = sk_begin(c, plan) < t_start ? 1 : 0;
-        const f32x4* src = wsv + (size_t)(c * 2 + cs) * 32 * 512;
-#pragma unroll
-        for (int q = 0; q < 32; ++q) (&acc[0][0][0])[q] += src[q * 512 + threadIdx.x];
-      }
-      if (threadIdx.x == 0) cnt[st] = 0;
-    }
-    epilogue<EPI>(Y, R, M, N, m0, n0, acc);
   }
+  __syncthreads();
+  if (!*flag) return;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) (&acc[0][0][0])[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < splits; ++c) {
+#pragma unroll
+    for (int q = 0; q < 32; ++q)
+      (&acc[0][0][0])[q] += wsv[((size_t)c * 32 + q) * 512 + threadIdx.x];
+  }
+  epilogue<EPI>(Y, R, M, N, m0, n0, acc);
 }
 
 template <class VAR>
@@ -418,10 +393,15 @@ struct SkDevice {
   int G = 0;
   float* ws = nullptr;
   int* cnt = nullptr;
+  size_t ws_tiles = 0;     // partial-tile slots in ws
+  int cnt_tiles = 0;
 };
 
-// persistent-grid size and stream-K workspace of the current device (allocated
-// on first use, outside any graph capture)
+constexpr int SPLIT_MAX = 8;
+constexpr size_t TILE_PARTIAL_BYTES = 32 * 512 * sizeof(f32x4);   // 256 KiB fp32
+
+// CU count and split-K workspace of the current device (allocated on first
+// use / growth, outside any graph capture)
 SkDevice& sk_device() {
   static SkDevice devs[64];
   int d = 0;
@@ -431,64 +411,81 @@ SkDevice& sk_device() {
     hipDeviceProp_t prop;
     sd.G = hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0
                ? prop.multiProcessorCount : 256;
-    (void)hipMalloc(&sd.ws, (size_t)sd.G * 2 * 32 * 512 * sizeof(f32x4));
-    (void)hipMalloc(&sd.cnt, sizeof(int) * 4 * sd.G);
-    (void)hipMemset(sd.cnt, 0, sizeof(int) * 4 * sd.G);
-    (void)hipDeviceSynchronize();
   }
   return sd;
 }
 
-// Whole waves run data-parallel; the last partial wave plus one full wave are
-// split in K across the persistent grid (each workgroup: 1..2 tiles of work).
-bool sk_plan(int M, int N, int K, int G, int mode, SkPlan& p) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const int waves = tiles / G, rem = tiles % G;
-  if (mode == 0) {                                   // auto
-    if (rem == 0) return false;
-    const double eff = (double)tiles / ((double)(waves + 1) * G);
-    if (eff >= 0.92) return false;
+bool sk_reserve(SkDevice& sd, int tiles, int splits) {
+  const size_t need = (size_t)tiles * splits;
+  if (need > sd.ws_tiles) {
+    if (sd.ws) (void)hipFree(sd.ws);
+    if (hipMalloc(&sd.ws, need * TILE_PARTIAL_BYTES) != hipSuccess) {
+      sd.ws = nullptr;
+      sd.ws_tiles = 0;
+      return false;
+    }
+    sd.ws_tiles = need;
   }
-  p.G = G;
-  p.nk = K / BK;
-  p.dp_waves = waves > 0 ? waves - 1 : 0;
-  p.dp_tiles = p.dp_waves * G;
-  p.sk_tiles = tiles - p.dp_tiles;
-  p.S = (long long)p.sk_tiles * p.nk;
-  // every workgroup of the stream-K phase must own >= 1 iteration (an empty
-  // range would be counted as a contributor and the tile never completes);
-  // S >= G whenever a data-parallel wave exists, so this only shrinks tiny grids
-  if (p.S < p.G) p.G = (int)p.S;
-  return p.sk_tiles <= 4 * G;
+  if (tiles > sd.cnt_tiles) {
+    if (sd.cnt) (void)hipFree(sd.cnt);
+    const int n = tiles * 2;
+    if (hipMalloc(&sd.cnt, sizeof(int) * n) != hipSuccess) {
+      sd.cnt = nullptr;
+      sd.cnt_tiles = 0;
+      return false;
+    }
+    (void)hipMemset(sd.cnt, 0, sizeof(int) * n);
+    (void)hipDeviceSynchronize();
+    sd.cnt_tiles = n;
+  }
+  return true;
+}
+
+// waves per split factor, with a 3 % per-extra-split charge for the partial
+// traffic and the shorter pipelines
+double split_cost(int tiles, int G, int s) {
+  return ceil((double)tiles * s / G) / s * (1.0 + 0.03 * (s - 1));
+}
+
+int choose_splits(int M, int N, int K, int G) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int nk = K / BK;
+  int best = 1;
+  double bc = split_cost(tiles, G, 1);
+  for (int s = 2; s <= SPLIT_MAX && nk / s >= 4; ++s) {
+    const double c = split_cost(tiles, G, s);
+    if (c < bc - 1e-9) {
+      bc = c;
+      best = s;
+    }
+  }
+  return best;
 }
 
 template <int EPI, class VAR = V256Default>
 void launch_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                int mode, hipStream_t s) {
-  // mode: 0 auto, 1 data-parallel, 2 stream-K hybrid
-  SkPlan plan;
-  if (mode != 1) {
-    SkDevice& sd = sk_device();
-    if (sk_plan(M, N, K, sd.G, mode == 2 ? 1 : 0, plan)) {
-      gemm_tn_256_sk<EPI, VAR><<<plan.G, 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                      (const bf16*)R, M, N, K, plan, sd.ws, sd.cnt);
-      return;
-    }
+                int splits, hipStream_t s) {
+  // splits: 0 auto, 1 data-parallel, >1 forced split-K
+  SkDevice& sd = sk_device();
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (splits <= 0) splits = choose_splits(M, N, K, sd.G);
+  splits = min(splits, max(1, K / BK));
+  if (splits > 1 && sk_reserve(sd, tiles, splits)) {
+    gemm_tn_256_splitk<EPI, VAR><<<tiles * splits, 512, 0, s>>>(
+        (const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, splits, sd.ws, sd.cnt);
+    return;
   }
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  gemm_tn_256<EPI, VAR><<<dim3(nm * nn), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                      (const bf16*)R, M, N, K);
+  gemm_tn_256<EPI, VAR><<<dim3(tiles), 512, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                    (const bf16*)R, M, N, K);
 }
 
 }  // namespace
 
-// effective waves of the 256^2 kernel (stream-K removes the quantisation of the last wave)
+// effective waves of the 256^2 kernel (split-K trims the quantisation of the last wave)
 double gemm256_waves(int M, int N, int K) {
   SkDevice& sd = sk_device();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  SkPlan p;
-  if (sk_plan(M, N, K, sd.G, 0, p)) return (double)tiles / sd.G * 1.04 + 0.05;
-  return ceil((double)tiles / sd.G);
+  return split_cost(tiles, sd.G, choose_splits(M, N, K, sd.G));
 }
 
 int gemm256_num_cus() { return sk_device().G; }
@@ -506,8 +503,10 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
 
 int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N, int K, int mode,
                             int pingpong, hipStream_t s) {
-  if (pingpong) launch_256<0, V256PingPong>(X, W, Y, nullptr, M, N, K, mode, s);
-  else launch_256<0, V256<false, false, false, true>>(X, W, Y, nullptr, M, N, K, mode, s);
+  // mode: 0 auto split, 1 data-parallel, 2 forced 3-way split
+  const int splits = mode == 0 ? 0 : mode == 1 ? 1 : 3;
+  if (pingpong) launch_256<0, V256PingPong>(X, W, Y, nullptr, M, N, K, splits, s);
+  else launch_256<0, V256<false, false, false, true>>(X, W, Y, nullptr, M, N, K, splits, s);
   return 0;
 }
 
