@@ -22,6 +22,8 @@
 // whose last read precedes the barrier that ends tile t-1.
 // LDS rows are 64 B (32 bf16); swizzle chunk ^= ((row>>2)&1)<<1 on the glds
 // SOURCE and the ds_read address (conflict-free, tools/lds_banks.py).
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -447,7 +449,21 @@ double split_cost(int tiles, int G, int s) {
   return ceil((double)tiles * s / G) / s * (1.0 + 0.03 * (s - 1));
 }
 
+// Auto split-K is OFF by default: with 256 KiB fp32 slabs per split and tile
+// the publish + last-arriver reduction costs more than the quantisation it
+// removes on every Llama-3 shape measured (profiles/gemm_tuning.md); forced
+// splits stay available (gemm_variant 31/33) and MCP_GEMM_SPLITK=1 enables auto.
+static bool splitk_auto() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("MCP_GEMM_SPLITK");
+    on = e && e[0] == '1';
+  }
+  return on == 1;
+}
+
 int choose_splits(int M, int N, int K, int G) {
+  if (!splitk_auto()) return 1;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int nk = K / BK;
   int best = 1;

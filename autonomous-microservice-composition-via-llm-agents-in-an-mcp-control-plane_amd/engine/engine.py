@@ -22,6 +22,7 @@ async frontend (planner.local) talks to it through queues.
 from __future__ import annotations
 
 import dataclasses
+import os
 import itertools
 import time
 from typing import Callable, Dict, List, Optional, Sequence as Seq
@@ -97,7 +98,10 @@ class LLMEngine:
         self.cascade = cascade      # shared-prefix (cascade) attention
         # two launch cohorts in flight: the host schedules / updates one cohort
         # while the GPU runs the other's forward (no idle GPU between steps)
-        self.pipeline = (self.device.type == "cuda") if pipeline is None else pipeline
+        if pipeline is None:
+            env = os.environ.get("MCP_PIPELINE", "auto")
+            pipeline = self.device.type == "cuda" if env == "auto" else env == "1"
+        self.pipeline = pipeline
         self.inflight: Dict[int, _Launch] = {}
         self.last_progress = time.perf_counter()   # watched by the planner's stall watchdog
         self._turn = 0
