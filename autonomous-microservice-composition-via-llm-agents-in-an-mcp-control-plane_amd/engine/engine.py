@@ -237,7 +237,10 @@ class LLMEngine:
         Pipelined: cohort c's previous launch is retired (its sampled tokens
         fed to the grammar) while the GPU is still busy with cohort c^1's
         forward, then cohort c is scheduled and launched asynchronously."""
-        if not self.pipeline:
+        if not self.pipeline or self._big_step():
+            while self.inflight:                  # drain the cohorts before a full-batch step
+                c, L = self.inflight.popitem()
+                self._retire(L)
             with span("engine.launch"):
                 L = self._schedule_launch(None)
             if L is None:
@@ -261,6 +264,20 @@ class LLMEngine:
             self.inflight[c] = nxt
             return done + nxt.T
         return done
+
+    PIPELINE_MAX_TOKENS = 1024
+
+    def _big_step(self) -> bool:
+        """Large batches run as ONE launch: halving the GEMM M per cohort costs
+        more in MFMA wave quantisation (e.g. 112 tiles on 256 CUs) than the
+        host time the two-cohort overlap hides (measured: 166 vs 156 plans/s at
+        256 concurrent intents)."""
+        n = 0
+        for q in self.running:
+            n += len(q.pending)
+            if n > self.PIPELINE_MAX_TOKENS:
+                return True
+        return False
 
     def _schedule_launch(self, cohort: Optional[int]) -> Optional[_Launch]:
         t_sched = time.perf_counter()
