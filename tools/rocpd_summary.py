@@ -1,0 +1,49 @@
+"""Summarise a rocprofv3 SQLite output (``-d DIR -o run`` -> run_results.db):
+per-kernel calls / total / mean time and a per-category breakdown.
+
+    python tools/rocpd_summary.py gpurun_out/prof11/run_results.db > profiles/x.md
+"""
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+CATS = [("gemm (MFMA 256x256)", r"gemm_tn_256"), ("gemm (MFMA 128x128)", r"gemm_tn_128"),
+        ("gemm (skinny K2)", r"gemm_skinny"), ("attention", r"attn_"),
+        ("sampling", r"sample_"), ("rmsnorm", r"rmsnorm"), ("rope+kv write", r"rope"),
+        ("embedding", r"embedding"), ("top-k", r"topk|l2norm"), ("kv copy", r"copy_blocks"),
+        ("all-reduce", r"car_|nccl|rccl"), ("torch/other", r".")]
+
+
+def short(name):
+    n = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)
+    m = re.match(r"(\w+?)I(.*)E(vPK|v)", n)
+    return (m.group(1) + "<" + m.group(2)[:40] + ">") if m else n[:80]
+
+
+def main(db):
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, count(*), sum(duration), avg(duration) from kernels "
+                          "group by name order by sum(duration) desc"))
+    span = c.execute("select max(end) - min(start) from kernels").fetchone()[0]
+    total = sum(r[2] for r in rows)
+    cats = defaultdict(float)
+    for name, n, tot, avg in rows:
+        for cat, pat in CATS:
+            if re.search(pat, name):
+                cats[cat] += tot
+                break
+    print(f"# rocprofv3 kernel summary: `{db}`\n")
+    print(f"GPU kernel time {total / 1e6:.1f} ms over a {span / 1e6:.1f} ms window "
+          f"(busy {100 * total / span:.1f} %)\n")
+    print("| category | ms | % of kernel time |\n|---|---|---|")
+    for cat, _ in CATS:
+        if cats.get(cat):
+            print(f"| {cat} | {cats[cat] / 1e6:.1f} | {100 * cats[cat] / total:.1f} |")
+    print("\n| kernel | calls | total ms | mean us | % |\n|---|---|---|---|---|")
+    for name, n, tot, avg in rows[:25]:
+        print(f"| `{short(name)}` | {n} | {tot / 1e6:.2f} | {avg / 1e3:.1f} | {100 * tot / total:.1f} |")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
