@@ -57,7 +57,8 @@ def main():
                     help="plans have between min and max nodes; min == max fixes the DAG size so "
                          "the work per plan does not depend on the random weights' choices")
     ap.add_argument("--max-nodes", type=int, default=5)
-    ap.add_argument("--max-step-tokens", type=int, default=16384)
+    ap.add_argument("--max-step-tokens", type=int, default=4096,
+                    help="token budget per engine step; 4096 = 16 M-tiles of 256 -> whole waves on 256 CUs")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 

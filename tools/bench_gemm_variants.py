@@ -6,8 +6,8 @@ sys.path.insert(0, '.')
 import mcp_amd.ops as ops
 L = ops.lib()
 dev = 'cuda'
-shapes = [(3584, 6144, 4096), (3584, 4096, 4096), (3584, 28672, 4096), (3584, 4096, 14336),
-          (4096, 4096, 4096), (1792, 6144, 4096)]
+shapes = [(4096, 6144, 4096), (4096, 4096, 4096), (4096, 28672, 4096), (4096, 4096, 14336),
+          (3584, 6144, 4096), (1792, 6144, 4096)]
 variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [8, 24, 30, 31, 32, 33]
 rounds = 3
 res = {}
