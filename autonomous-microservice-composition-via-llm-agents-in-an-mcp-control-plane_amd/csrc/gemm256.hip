@@ -65,9 +65,10 @@ DEV void sched_barrier_full() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
-// production default: ping-pong (variant 24), +4-10 % over the best non-staggered
-// variant 8 on the Llama-3-8B projection shapes (profiles/gemm_tuning.md)
-using V256Default = V256<false, false, true, true, true>;
+// production default: ping-pong without s_setprio (variant 25), +5-12 % over the
+// best non-staggered variant 8 on the Llama-3-8B projection shapes
+// (profiles/gemm_tuning.md, profiles/gemm_variants_m4096.jsonl)
+using V256Default = V256<false, false, false, true, true>;
 
 // Grouped tile order: GROUP M-tiles share each W column panel in L2.
 DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
