@@ -19,6 +19,8 @@
 //      operand") and V^T read with ds_read_b64_tr_b16 (T10).
 // K/V tiles: global_load_lds_dwordx4 into a double-buffered LDS ring with the
 // 256-B-row XOR swizzle chunk ^= row&15 on source and read (tools/lds_banks.py).
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -260,11 +262,29 @@ void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s) {
     attn_kernel<4, G, 0><<<grid, 256, 0, s>>>(a);
 }
 
+int prefix_nw() {
+  static int nw = 0;
+  if (!nw) {
+    const char* e = getenv("MCP_ATTN_PREFIX_NW");
+    nw = e ? atoi(e) : 8;
+    if (nw != 4 && nw != 8) nw = 8;
+  }
+  return nw;
+}
+
+// Shared-prefix pass: 8 waves per block (32 tokens x G heads) -> half the K/V
+// tile staging per query of the 4-wave item and 4 waves per SIMD at 2 blocks/CU
 template <int G>
 void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s) {
-  constexpr int QT = 4 * (16 / G);
-  const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
-  attn_kernel<4, G, 1><<<grid, 256, 0, s>>>(a);
+  if (prefix_nw() == 4) {
+    constexpr int QT = 4 * (16 / G);
+    const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
+    attn_kernel<4, G, 1><<<grid, 256, 0, s>>>(a);
+  } else {
+    constexpr int QT = 8 * (16 / G);
+    const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
+    attn_kernel<8, G, 1><<<grid, 512, 0, s>>>(a);
+  }
 }
 
 }  // namespace
