@@ -365,6 +365,9 @@ int launch_gemm_tn_256w4m16(const void* X, const void* W, void* Y, const void* R
 int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N, int K, int mode,
                             int pingpong, hipStream_t s);
 
+int launch_gemm_tn_256i(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        int epi, hipStream_t s);
+
 // tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
                                hipStream_t s) {
@@ -386,6 +389,7 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 31: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 0, s);   // stream-K, variant 8 body
     case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 1, s);   // auto (production)
     case 33: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 1, s);   // stream-K + ping-pong
+    case 40: return launch_gemm_tn_256i(X, W, Y, nullptr, M, N, K, 0, s);  // one barrier per K-tile
     default: return 1;
   }
 }

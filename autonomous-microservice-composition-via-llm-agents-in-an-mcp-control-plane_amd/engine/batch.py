@@ -158,6 +158,89 @@ class HostStager:
         return d
 
 
+def pack_step_py(entries, block_size: int, group: int, copies=None, pre_bt=None, pre_tokens: int = 0,
+                 allowed=None, ctr=None):
+    """Python reference of the native ``pack_step`` (csrc/runtime/runtime.cpp).
+
+    ``entries``: (tokens, take, start, blocks, kv_begin, sample) per sequence;
+    the first ``take`` tokens enter at positions [start, start + take).
+    Returns ``(host, layout)`` like ``pack_host``."""
+    ids, pos, slots, rows = [], [], [], []
+    q_start, q_len, ctx_len, kvb, tables = [], [], [], [], []
+    T = 0
+    for toks, take, start, blocks, kv_begin, sample in entries:
+        if take <= 0 or take > len(toks):
+            raise ValueError("pack_step: bad span")
+        if start + take > len(blocks) * block_size:
+            raise ValueError("pack_step: sequence has too few KV blocks")
+        ids += list(toks[:take])
+        p = np.arange(start, start + take, dtype=np.int32)
+        pos.append(p)
+        blk = np.asarray(blocks, dtype=np.int32)
+        slots.append(blk[p // block_size] * block_size + p % block_size)
+        q_start.append(T)
+        q_len.append(take)
+        ctx_len.append(start + take)
+        kvb.append(kv_begin)
+        tables.append(blocks)
+        T += take
+        if sample:
+            rows.append(T - 1)
+    S = len(entries)
+    maxb = max([len(t) for t in tables] + [1])
+    bt = np.zeros((S, maxb), np.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = t
+    z = np.zeros(0, np.int32)
+    step = StepInputs(token_ids=np.asarray(ids, np.int32),
+                      positions=np.concatenate(pos) if pos else z,
+                      slots=np.concatenate(slots).astype(np.int32) if slots else z,
+                      q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
+                      ctx_len=np.asarray(ctx_len, np.int32), block_table=bt,
+                      logit_rows=np.asarray(rows, np.int32))
+    if pre_bt is not None and pre_tokens > 0 and len(pre_bt):
+        step.kv_begin = np.asarray(kvb, np.int32)
+        step.pre_bt = np.asarray(pre_bt, np.int32)
+        step.pre_tokens = pre_tokens
+    if allowed is not None:
+        ptr = np.zeros(len(allowed) + 1, np.int32)
+        ptr[1:] = np.cumsum([len(a) for a in allowed])
+        step.allow_ptr = ptr
+        step.allow_ids = np.asarray([t for a in allowed for t in a], np.int32)
+        step.sample_ctr = np.asarray(ctr, np.int32)
+        if len(step.sample_ctr) != len(rows) or len(allowed) != len(rows):
+            raise ValueError("pack_step: allowed sets / counters do not match sampled rows")
+    return pack_host(step, group, copies or ())
+
+
+def pack_step(entries, block_size: int, group: int, copies=None, pre_bt=None, pre_tokens: int = 0,
+              allowed=None, ctr=None):
+    """One step's packed int32 descriptor: the native C++ packer when built."""
+    from . import native
+    if native.available():
+        return native.pack_step(entries, block_size, group, list(copies) if copies else None,
+                                pre_bt, pre_tokens, allowed, ctr)
+    return pack_step_py(entries, block_size, group, copies, pre_bt, pre_tokens, allowed, ctr)
+
+
+def step_from_host(host: np.ndarray, layout) -> StepInputs:
+    """``StepInputs`` of numpy views into a packed host buffer (the inverse of
+    ``pack_host`` on the host side; used by the hipGraph bucket packer)."""
+    sizes, S, pre_tokens = layout[:-2], layout[-2], layout[-1]
+    vs, off = [], 0
+    for n in sizes:
+        vs.append(host[off:off + n])
+        off += n
+    bt = vs[7].reshape(S, -1) if S else vs[7].reshape(0, 1)
+    step = StepInputs(token_ids=vs[0], positions=vs[1], slots=vs[2], q_start=vs[4], q_len=vs[5],
+                      ctx_len=vs[6], block_table=bt, logit_rows=vs[3])
+    if pre_tokens > 0:
+        step.kv_begin, step.pre_bt, step.pre_tokens = vs[14], vs[15], pre_tokens
+    if sizes[16]:
+        step.allow_ptr, step.allow_ids, step.sample_ctr = vs[16], vs[17], vs[18]
+    return step
+
+
 def to_device(host: np.ndarray, device, pin: bool = True) -> torch.Tensor:
     t = torch.from_numpy(host)
     if device is not None and torch.device(device).type == "cuda":

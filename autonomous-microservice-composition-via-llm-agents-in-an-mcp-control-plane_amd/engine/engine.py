@@ -33,7 +33,7 @@ import torch
 from .. import ops
 from ..utils.metrics import METRICS
 from ..utils.tracing import span
-from .batch import BLOCK_SIZE, HostStager, StepInputs, pack_host, views
+from .batch import BLOCK_SIZE, HostStager, pack_step, step_from_host, views
 from .kv_cache import KVCache
 
 _uid = itertools.count(1)
@@ -290,10 +290,7 @@ class LLMEngine:
             if not seq.materialized and seq.prefix.computed:
                 self._materialize(seq, copies)
         budget = self.max_step_tokens
-        ids, pos, slots = [], [], []
-        q_start, q_len, ctx_len, tables = [], [], [], []
-        logit_rows, sample_seqs = [], []
-        batch_seqs = []
+        entries, sample_seqs, batch_seqs = [], [], []
         T = 0
         # cascade: requests that share the most common computed prefix go first,
         # so their tokens form the leading range [0, pre_tokens) of the batch
@@ -311,7 +308,7 @@ class LLMEngine:
         if casc is not None:
             order = [q for q in pool if q.prefix is casc and q.materialized] + \
                     [q for q in pool if not (q.prefix is casc and q.materialized)]
-        pre_tokens, kv_begin = 0, []
+        pre_tokens = 0
         casc_keys = (casc.length // BLOCK_SIZE) * BLOCK_SIZE if casc is not None else 0
         for seq in order:
             if not seq.materialized:           # waiting for its prefix job
@@ -324,64 +321,39 @@ class LLMEngine:
                 break
             start = seq.num_cached
             self._ensure_blocks(seq, start + take)
-            toks = seq.pending[:take]
-            q_start.append(T)
-            q_len.append(take)
-            ctx_len.append(start + take)
-            tables.append(seq.blocks)
-            ids += toks
-            p = np.arange(start, start + take, dtype=np.int32)
-            pos.append(p)
-            blk = np.asarray(seq.blocks, dtype=np.int32)
-            slots.append(blk[p // BLOCK_SIZE] * BLOCK_SIZE + p % BLOCK_SIZE)
-            if casc is not None and seq.prefix is casc and seq.materialized:
-                pre_tokens = T + take
-                kv_begin.append(casc_keys)
-            else:
-                kv_begin.append(0)
+            in_casc = casc is not None and seq.prefix is casc
             T += take
+            if in_casc:
+                pre_tokens = T
+            sample = take == n and seq.wants_sample
+            entries.append((seq.pending, take, start, seq.blocks, casc_keys if in_casc else 0, sample))
             batch_seqs.append((seq, take))
-            if take == n and seq.wants_sample:
-                logit_rows.append(T - 1)
+            if sample:
                 sample_seqs.append(seq)
+        group = self.model.cfg.group
         if T == 0:
             if copies:     # copy-on-write blocks still have to land before later steps
-                self._launch(None, copies)
+                self._launch(*pack_step([], BLOCK_SIZE, group, copies))
             return None
-        S = len(batch_seqs)
-        maxb = max(len(t) for t in tables)
-        bt = np.zeros((S, maxb), np.int32)
-        for i, t in enumerate(tables):
-            bt[i, :len(t)] = t
-        step = StepInputs(token_ids=np.asarray(ids, np.int32), positions=np.concatenate(pos),
-                          slots=np.concatenate(slots).astype(np.int32),
-                          q_start=np.asarray(q_start, np.int32), q_len=np.asarray(q_len, np.int32),
-                          ctx_len=np.asarray(ctx_len, np.int32), block_table=bt,
-                          logit_rows=np.asarray(logit_rows, np.int32))
+        allowed = ctr = None
         if sample_seqs:            # grammar masks go in the same single H2D copy
             allowed = [q.decoder.allowed() for q in sample_seqs]
-            ptr = np.zeros(len(allowed) + 1, np.int32)
-            ptr[1:] = np.cumsum([len(a) for a in allowed])
-            step.allow_ptr = ptr
-            step.allow_ids = np.fromiter(itertools.chain.from_iterable(allowed), dtype=np.int32,
-                                         count=int(ptr[-1]))
-            step.sample_ctr = np.asarray([(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF
-                                          for q in sample_seqs], np.int32)
+            ctr = [(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF for q in sample_seqs]
         use_graph = (self.graphs is not None and not copies and T <= self.graphs.buckets[-1]
                      and self.temperature == self.graphs.temperature)
-        if pre_tokens > 0 and not use_graph:
-            step.kv_begin = np.asarray(kv_begin, np.int32)
-            step.pre_bt = np.asarray(casc.blocks[:casc_keys // BLOCK_SIZE], np.int32)
-            step.pre_tokens = pre_tokens
+        cascade = pre_tokens > 0 and not use_graph
+        host, layout = pack_step(entries, BLOCK_SIZE, group, copies,
+                                 casc.blocks[:casc_keys // BLOCK_SIZE] if cascade else None,
+                                 pre_tokens if cascade else 0, allowed, ctr)
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
-        tok_dev = self.graphs.run(step) if use_graph else None
+        tok_dev = self.graphs.run(step_from_host(host, layout)) if use_graph else None
         if tok_dev is not None:            # replayed hipGraph: forward + sampling
             self.stats["graph_steps"] += 1
             self.stats["samples"] += len(sample_seqs)
             tokens, event = self._fetch(tok_dev[:len(sample_seqs)])
         else:
-            hidden, dstep = self._launch(step, copies)
+            hidden, dstep = self._launch(host, layout)
             tokens, event = self._sample(hidden, dstep, len(sample_seqs))
         self.stats["launch_s"] += time.perf_counter() - t0
         self.stats["tokens"] += T
@@ -418,14 +390,8 @@ class LLMEngine:
         METRICS.set("batch_occupancy", len(self.running))
         METRICS.set("kv_block_utilization", self.alloc.utilization())
 
-    def _launch(self, step: Optional[StepInputs], copies):
-        """Pack -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
-        if step is None:
-            empty = np.zeros(0, np.int32)
-            step = StepInputs(token_ids=empty, positions=empty, slots=empty, q_start=empty,
-                              q_len=empty, ctx_len=empty, block_table=np.zeros((0, 1), np.int32),
-                              logit_rows=empty)
-        host, layout = pack_host(step, self.model.cfg.group, copies)
+    def _launch(self, host, layout):
+        """(packed step) -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
         payload = self.stager.to_device(host)
         if self.bcast is not None:
             self.bcast.send(payload, layout)

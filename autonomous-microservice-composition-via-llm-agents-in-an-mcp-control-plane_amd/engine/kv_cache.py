@@ -15,15 +15,20 @@ from typing import List, Optional
 
 import torch
 
+from . import native
 from .batch import BLOCK_SIZE
 
-
-class OutOfBlocks(RuntimeError):
-    pass
+if native.available():
+    OutOfBlocks = native.OutOfBlocks
+else:
+    class OutOfBlocks(RuntimeError):
+        pass
 
 
 class BlockAllocator:
-    """Free-list allocator with refcounts (native C++ variant: engine/_runtime)."""
+    """Free-list allocator with refcounts.  The engine uses the C++ one
+    (``native.NativeBlockAllocator``, csrc/runtime/runtime.cpp) when built;
+    this is the reference implementation and CPU fallback."""
 
     def __init__(self, num_blocks: int):
         self.num_blocks = num_blocks
@@ -44,26 +49,29 @@ class BlockAllocator:
 
     def incref(self, blocks: List[int]):
         for b in blocks:
+            if self._ref[b] <= 0:
+                raise RuntimeError(f"incref of free block {b}")
             self._ref[b] += 1
 
     def free(self, blocks: List[int]):
         for b in blocks:
+            if self._ref[b] <= 0:
+                raise RuntimeError(f"double free of block {b}")
             self._ref[b] -= 1
             if self._ref[b] == 0:
                 self._free.append(b)
-            elif self._ref[b] < 0:
-                raise RuntimeError(f"double free of block {b}")
+
+    def refcount(self, b: int) -> int:
+        return self._ref[b]
 
     def utilization(self) -> float:
         return 1.0 - len(self._free) / max(1, self.num_blocks)
 
 
 def make_allocator(num_blocks: int):
-    try:
-        from . import native
+    if native.available():
         return native.NativeBlockAllocator(num_blocks)
-    except Exception:  # native runtime not built (CPU tier without compiler)
-        return BlockAllocator(num_blocks)
+    return BlockAllocator(num_blocks)
 
 
 class KVCache:

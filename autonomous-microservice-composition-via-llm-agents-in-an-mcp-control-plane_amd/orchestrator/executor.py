@@ -170,13 +170,28 @@ class Orchestrator:
             METRICS.observe("execute_latency_s", time.perf_counter() - t0)
         return {"results": results, "errors": errors}
 
+    @staticmethod
+    def generations(G: nx.DiGraph) -> List[List[str]]:
+        """Topological generations in networkx's generational-Kahn order (T3):
+        the native runtime's ``topo_generations`` when built, else networkx.
+        A cycle raises ``NetworkXUnfeasible`` either way (HTTP 500, as the
+        reference's ``nx.topological_sort``)."""
+        from ..engine import native
+        if not native.available():
+            return [list(g) for g in nx.topological_generations(G)]
+        names = list(G.nodes)
+        idx = {n: i for i, n in enumerate(names)}
+        try:
+            gens = native.topo_generations(len(names), [(idx[u], idx[v]) for u, v in G.edges])
+        except RuntimeError as e:
+            raise nx.NetworkXUnfeasible(str(e)) from None
+        return [[names[i] for i in g] for g in gens]
+
     async def _execute_generations(self, G, payload, results, errors):
-        order = list(nx.topological_sort(G))    # raises on cycles exactly like serial
+        gens = self.generations(G)
+        order = [n for g in gens for n in g]
         pos = {n: i for i, n in enumerate(order)}
-        gen_of: Dict[str, int] = {}
-        for g, names in enumerate(nx.topological_generations(G)):
-            for n in names:
-                gen_of[n] = g
+        gen_of: Dict[str, int] = {n: g for g, names in enumerate(gens) for n in names}
         i = 0
         while i < len(order):
             g = gen_of[order[i]]
