@@ -369,6 +369,8 @@ int launch_gemm_tn_256i(const void* X, const void* W, void* Y, const void* R, in
                         int epi, hipStream_t s);
 int launch_gemm_tn_256a(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         int epi, hipStream_t s);
+int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        int epi, hipStream_t s);
 
 // tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
@@ -392,8 +394,9 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 1, s);   // auto (production)
     case 33: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 1, s);   // stream-K + ping-pong
     case 40: return launch_gemm_tn_256i(X, W, Y, nullptr, M, N, K, 0, s);  // one barrier per K-tile
-    case 41: case 42: case 43: case 44:    // 4 waves, AGPR accumulators, schedule v - 41
+    case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48:   // 4 waves, AGPR acc, structure v - 41
       return launch_gemm_tn_256a(X, W, Y, nullptr, M, N, K, 10 + v - 41, s);
+    case 49: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);   // 1 wave/SIMD, 128-B DMA rows
     default: return 1;
   }
 }

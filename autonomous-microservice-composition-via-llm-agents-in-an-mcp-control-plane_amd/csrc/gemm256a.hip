@@ -16,14 +16,19 @@
 // LDS-DMA: with one wave per SIMD nothing hides the LDS-DMA issue cost
 // (MI355X_MICROARCH.md: ~60 cycles per 1 KiB piece among MFMAs).
 //
-// Pipeline over 32-deep k-steps, 4 LDS slots of {A 256x32, B 256x32} (32 KiB):
-//   step s computes from slot s%4 with fragments F[s&1] (read during step s-1)
-//     * buffer_load step s+3 -> staging G[s&1]           (start of step s)
-//     * ds_read fragments of step s+1 -> F[(s+1)&1]       (interleaved)
-//     * ds_write G[(s+1)&1] (= step s+2) -> slot (s+2)%4  (end of step s)
-//     * s_waitcnt; s_barrier
-// WAR: slot (s+2)%4 was last read during step s-3 (fragments of step s-2).
-// RAW: slot (s+2)%4 is written before barrier s and read after it (step s+1).
+// Pipeline over 32-deep k-steps; a ring of S slots {A 256x32, B 256x32}
+// (32 KiB each); step s computes from fragments F[s&1] read during step s-1:
+//   S = 4: barrier after every step;  step s loads step s+3 into registers,
+//          writes step s+2 (loaded in step s-1) to slot (s+2)%4, reads the
+//          fragments of step s+1 from slot (s+1)%4.
+//          WAR: slot (s+2)%4 was last read in step s-3; RAW: step s+1 was
+//          written in step s-1, before barrier s-1.
+//   S = 5: barrier after odd steps only (160 KiB LDS, half the barriers);
+//          step s loads s+4, writes s+3 to slot (s+3)%5, reads s+1.
+//          RAW: step s+1 was written in step s-2 and a barrier (end of s-1
+//          or s-2, whichever is odd) lies between; WAR: slot (s+3)%5 was
+//          last read in step s-3, and one of steps s-3..s-1 ends in a barrier.
+// Every wave drains its LDS ops (lgkmcnt(0)) before each barrier.
 // LDS rows are 64 B (32 bf16), chunk swizzle ^= ((row >> 2) & 1) << 1 applied
 // on the ds_write and ds_read addresses (conflict-free, tools/lds_banks.py).
 #include <type_traits>
@@ -33,7 +38,7 @@
 
 namespace {
 
-constexpr int BM = 256, BN = 256, KS = 32, SLOTS = 4;
+constexpr int BM = 256, BN = 256, KS = 32;
 constexpr int PIECE = 256 * KS;                     // bf16 elements per operand piece (16 KiB)
 constexpr int SLOT_BYTES = 2 * PIECE * 2;           // A + B = 32 KiB
 
@@ -56,13 +61,23 @@ struct Frags {
   bf16x8 b[8];
 };
 
-template <int EPI, int SCHED = 1>
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+
+// SCHED: 0 = one staging / fragment op after every MFMA pair, spread over the
+// step; 1 = the same ops bunched into the first 20 pairs.  S: LDS ring slots.
+// DMA: stage with buffer_load ... lds straight into the ring (no staging
+// registers, no ds_write), loop unrolled by S so every slot index is static.
+template <int EPI, int SCHED = 0, int S = 4, bool DMA = false, int DMAPOS = 0>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256a(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
                                                        int K) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[SLOTS * 2 * PIECE];
+  static_assert(S == 4 || S == 5, "ring of 4 or 5 slots");
+  static_assert(!DMA || (S == 4 && SCHED == 0), "LDS-DMA staging: 4 slots, spread schedule");
+  constexpr int LA = S - 1;          // a step loads step s + LA into registers ...
+  constexpr int WA = S - 2;          // ... and writes step s + WA to the LDS ring
+  __shared__ __attribute__((aligned(16))) bf16 smem[S * 2 * PIECE];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -96,68 +111,27 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256a(const bf16* __restrict__ 
   // LDS byte offset of this thread's chunk i inside a piece: rows srow + 64 i
   // share bit 2 of the row, hence the swizzle; +4 KiB per i
   const int wofs = (srow * KS + swz(srow, sch) * 8) * 2;
-
-  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
-  u32x4_t G[2][8];                                   // [set][A0..3 | B0..3]
-  auto gload = [&](int s, u32x4_t (&g)[8]) {
-    const int soff = s * KS * 2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      g[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsA, goffA[i], soff, 0));
-      g[4 + i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsB, goffB[i], soff, 0));
-    }
-  };
   char* const lds = reinterpret_cast<char*>(smem);
-  auto lwrite = [&](int slot, const u32x4_t (&g)[8]) {
-    char* base = lds + slot * SLOT_BYTES + wofs;
+  // LDS-DMA: instruction i (0..3) of this wave fills rows (4 wave + i) * 16 +
+  // lane / 4 of a piece lane-linearly; the chunk swizzle moves to the source
+  unsigned doffA[4], doffB[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<u32x4_t*>(base + i * 4096) = g[i];
-      *reinterpret_cast<u32x4_t*>(base + PIECE * 2 + i * 4096) = g[4 + i];
-    }
+  for (int i = 0; i < 4; ++i) {
+    // DMAPOS 3 (timing-only probe, wrong results): 8 rows x 128 B per instruction
+    const int row = DMAPOS == 3 ? (4 * wave + i) * 8 + (lane >> 3) : (4 * wave + i) * 16 + (lane >> 2);
+    const int ch = DMAPOS == 3 ? (lane & 7) : swz(row, lane & 3);
+    doffA[i] = (unsigned)(((size_t)min(m0 + row, M - 1) * K + ch * 8) * 2);
+    doffB[i] = (unsigned)(((size_t)min(n0 + row, N - 1) * K + ch * 8) * 2);
+  }
+  auto dma1 = [&](int st, int slot, int i) {           // i < 4: A instruction i, else B i-4
+    const int soff = st * KS * 2;
+    auto* dst = (__attribute__((address_space(3))) void*)(
+        smem + slot * 2 * PIECE + (i < 4 ? 0 : PIECE) + (4 * wave + (i & 3)) * 512);
+    if (i < 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, doffA[i], soff, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, doffB[i - 4], soff, 0, 0);
   };
 
-  // ---- fragment reads: wave (wm, wn) owns rows wm*128.., cols wn*128..
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int rowA = wm * 128 + fr, rowB = wn * 128 + fr;
-  const int rA = (rowA * KS + swz(rowA, fq) * 8) * 2;   // fragment mt: + mt * 1 KiB
-  const int rB = (rowB * KS + swz(rowB, fq) * 8) * 2 + PIECE * 2;
-  auto fread = [&](int slot, Frags& f) {
-    const char* pa = lds + slot * SLOT_BYTES + rA;
-    const char* pb = lds + slot * SLOT_BYTES + rB;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) f.b[i] = *reinterpret_cast<const bf16x8*>(pb + i * 1024);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) f.a[i] = *reinterpret_cast<const bf16x8*>(pa + i * 1024);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int ns = K / KS;                             // even, >= 4 (launcher)
-  Frags F[2];
-  // prologue: steps 0, 1 in LDS, step 2 staged in G[0]... (G set = step & 1 of the loading step)
-  gload(0, G[0]);
-  gload(1, G[1]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lwrite(0, G[0]);
-  lwrite(1, G[1]);
-  gload(2, G[0]);                                    // consumed (written) at the end of step 0
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  raw_barrier();
-  fread(0, F[0]);
-  __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): clean waitcnt state at the loop head
-
-  // one k-step; P = s & 1 and which of load / write / read happen are all
-  // static (no branches in the loop body: a conditional load makes hipcc's
-  // waitcnt analysis fall back to draining every outstanding load)
-  // single staging / fragment operations, so the step can interleave them
-  // one per two MFMAs (with one wave per SIMD nothing else fills the MFMA
-  // pipe while a VMEM / LDS instruction issues)
+  u32x4_t G[2][8];                                   // [set][A0..3 | B0..3], set = step & 1
   auto gload1 = [&](int st, u32x4_t (&g)[8], int i) {      // i < 4: A chunk i, else B chunk i-4
     const int soff = st * KS * 2;
     if (i < 4)
@@ -170,52 +144,106 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256a(const bf16* __restrict__ 
     char* base = lds + slot * SLOT_BYTES + wofs + (i < 4 ? 0 : PIECE * 2);
     *reinterpret_cast<u32x4_t*>(base + (i & 3) * 4096) = g[i];
   };
+  auto gload = [&](int st, u32x4_t (&g)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gload1(st, g, i);
+  };
+  auto lwrite = [&](int slot, const u32x4_t (&g)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lwrite1(slot, g, i);
+  };
+
+  // ---- fragment reads: wave (wm, wn) owns rows wm*128.., cols wn*128..
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rowA = wm * 128 + fr, rowB = wn * 128 + fr;
+  const int rA = (rowA * KS + swz(rowA, fq) * 8) * 2;   // fragment mt: + mt * 1 KiB
+  const int rB = (rowB * KS + swz(rowB, fq) * 8) * 2 + PIECE * 2;
   auto fread1 = [&](int slot, Frags& f, int i) {           // i < 8: B[i], else A[i-8]
     if (i < 8)
       f.b[i] = *reinterpret_cast<const bf16x8*>(lds + slot * SLOT_BYTES + rB + i * 1024);
     else
       f.a[i - 8] = *reinterpret_cast<const bf16x8*>(lds + slot * SLOT_BYTES + rA + (i - 8) * 1024);
   };
-  auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
 
-  // one k-step; P = s & 1 and which of load / write / read happen are all
-  // static (no branches in the loop body: a conditional load makes hipcc's
-  // waitcnt analysis fall back to draining every outstanding load).
-  // 64 MFMAs in pairs, staging / fragment operations between the pairs
-  auto step = [&](int s, auto p_c, auto ld_c, auto wr_c, auto rd_c) {
-    constexpr int P = decltype(p_c)::value;
-    constexpr bool LD = decltype(ld_c)::value, WR = decltype(wr_c)::value,
-                   RD = decltype(rd_c)::value;
-    Frags& cur = F[P];
-    Frags& nxt = F[P ^ 1];
-    const int rslot = (s + 1) % SLOTS, wslot = (s + 2) % SLOTS;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = K / KS;                             // even, >= 4 (launcher)
+  Frags F[2];
+  if constexpr (DMA) {
+    // prologue: steps 0, 1, 2 in flight into slots 0, 1, 2; step 0 landed
+#pragma unroll
+    for (int st = 0; st < 3; ++st)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dma1(st, st, i);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+  // prologue: steps 0 .. WA-1 in the ring, step WA loaded into G[WA & 1]
+  gload(0, G[0]);
+  gload(1, G[1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lwrite(0, G[0]);
+  lwrite(1, G[1]);
+  if constexpr (S == 5) {
+    gload(2, G[0]);
+    gload(3, G[1]);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    lwrite(2, G[0]);
+  } else {
+    gload(2, G[0]);
+  }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) fread1(0, F[0], i);
+  __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): clean waitcnt state at the loop head
+
+  auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+  // one k-step; P = s & 1 static (the loop is unrolled by two), no branches in
+  // the body (a conditional load makes hipcc's waitcnt analysis fall back to
+  // draining every outstanding load).  64 MFMAs in pairs with the staging /
+  // fragment operations placed between the pairs (one wave per SIMD: nothing
+  // else fills the MFMA pipe while a VMEM / LDS instruction issues)
+  auto step = [&](int s, auto p_c) {
+    constexpr int P = decltype(p_c)::value;         // DMA: s % 4, else s & 1
+    constexpr int GL = (LA & 1) ? (P & 1) ^ 1 : (P & 1);   // register set of step s + LA
+    Frags& cur = F[P & 1];
+    Frags& nxt = F[(P & 1) ^ 1];
+    const int rslot = DMA ? (P + 1) % S : (s + 1) % S, wslot = (s + WA) % S;
     fence();
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
       const int i0 = 2 * j, i1 = 2 * j + 1;
       mfma_a(acc[i0 >> 3][i0 & 7], cur.b[i0 & 7], cur.a[i0 >> 3]);
       mfma_a(acc[i1 >> 3][i1 & 7], cur.b[i1 & 7], cur.a[i1 >> 3]);
-      // which operations follow pair j (SCHED, A/B-tested: tools/bench_gemm_variants.py)
-      constexpr int L0 = 0, R0 = SCHED == 3 ? 8 : 0, W0 = SCHED == 1 ? 12 : SCHED == 2 ? 4 : 0;
-      if constexpr (SCHED == 0) {               // spread over the whole step
+      if constexpr (DMA) {                      // DMA of step s+3 into the slot of step s-1
+        // DMAPOS (tuning): 0 one DMA per 4 pairs, 1 all 8 after pair 0,
+        // 2 none (timing-only upper bound: wrong results)
         const int k = j >> 2;
-        if ((j & 3) == 0) {
-          if constexpr (LD) gload1(s + 3, G[P ^ 1], k);   // G[P^1] went to LDS in step s-1
-        } else if ((j & 3) == 3) {
-          if constexpr (WR) lwrite1(wslot, G[P], k);      // step s+2
-        } else {
-          if constexpr (RD) fread1(rslot, nxt, 2 * k + (j & 3) - 1);
+        if ((DMAPOS == 0 || DMAPOS == 3) && (j & 3) == 0) dma1(s + 3, (P + 3) % S, k);
+        if (DMAPOS == 1 && j == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dma1(s + 3, (P + 3) % S, i);
         }
-      } else {                                  // early, so everything landed by the closing wait
-        if (j >= L0 && j < L0 + 8) {
-          if constexpr (LD) gload1(s + 3, G[P ^ 1], j - L0);
-        }
-        if (j >= R0 && j < R0 + 16) {
-          if constexpr (RD) fread1(rslot, nxt, j - R0);
-        }
-        if (j >= W0 && j < W0 + 8) {
-          if constexpr (WR) lwrite1(wslot, G[P], j - W0);
-        }
+        if ((j & 3) == 1 || (j & 3) == 2)
+          fread1(rslot, nxt, 2 * k + (j & 3) - 1);
+      } else if constexpr (SCHED == 0) {        // spread over the whole step
+        const int k = j >> 2;
+        if ((j & 3) == 0)
+          gload1(s + LA, G[GL], k);             // G[GL] went to the ring in step s-1
+        else if ((j & 3) == 3)
+          lwrite1(wslot, G[GL ^ 1], k);         // step s+WA, loaded in step s-1
+        else
+          fread1(rslot, nxt, 2 * k + (j & 3) - 1);
+      } else {                                  // bunched early
+        if (j < 8) gload1(s + LA, G[GL], j);
+        if (j < 16) fread1(rslot, nxt, j);
+        if (j >= 12 && j < 20) lwrite1(wslot, G[GL ^ 1], j - 12);
       }
       fence();
     }
@@ -225,32 +253,49 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256a(const bf16* __restrict__ 
     // MFMA source, which inline asm does not pad)
 #pragma unroll
     for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(cur.a[i]), "v"(cur.b[i]));
-    // lgkmcnt(0) as a builtin (vmcnt/expcnt left at their maxima), so hipcc
-    // knows every LDS op is done and never re-waits for the fragment reads
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    raw_barrier();
+    if constexpr (DMA) {
+      // step s+2's DMA (issued in step s-1) landed; step s+3's 8 stay in flight
+      if constexpr (DMAPOS == 2) __builtin_amdgcn_s_waitcnt(0xC07F);
+      else __builtin_amdgcn_s_waitcnt(0x0078);      // vmcnt(8) lgkmcnt(0)
+      raw_barrier();
+    } else if (S == 4 || (P & 1) == 1) {
+      // lgkmcnt(0) as a builtin (vmcnt/expcnt left at their maxima), so hipcc
+      // knows every LDS op is done and never re-waits for the fragment reads
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      raw_barrier();
+    }
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using T_ = std::true_type;
   // ns is even (K % 64 == 0, launcher).  Every step runs the full body, also
-  // the last three: their loads of steps >= ns read bytes that are never used
+  // the last ones: their loads of steps >= ns read bytes that are never used
   // (in-bounds rows, or zeros past the end of the buffer descriptor) and their
   // writes go to slots that are never read again.  A peeled tail would be
   // separate code in which hipcc re-assigns the accumulators with
   // v_accvgpr_mov's - VALU writes that the inline-asm MFMAs next to them are
   // not padded against.
-  // accumulator zeroing (VALU v_accvgpr_write) -> first MFMA reading them as
+  // Accumulator zeroing (VALU v_accvgpr_write) -> first MFMA reading them as
   // srcC needs wait states: pin the writes before a nop (asm statements keep
-  // their order; the empty "+a" asms depend on the writes)
+  // their order; the empty "+a" asms depend on the writes).
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
   asm volatile("s_nop 4" ::: "memory");
-  for (int s = 0; s < ns; s += 2) {
-    step(s, I0{}, T_{}, T_{}, T_{});
-    step(s + 1, I1{}, T_{}, T_{}, T_{});
+  if constexpr (DMA) {
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    for (int s = 0; s < ns; s += 4) {               // ns % 4 == 0 (launcher)
+      step(s, I0{});
+      step(s + 1, I1{});
+      step(s + 2, I2{});
+      step(s + 3, I3{});
+    }
+  } else {
+    for (int s = 0; s < ns; s += 2) {
+      step(s, I0{});
+      step(s + 1, I1{});
+    }
   }
   // MFMA results -> VALU reads: 8-pass XDL needs its wait states (inline asm is not padded)
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -304,12 +349,28 @@ int launch_gemm_tn_256a(const void* X, const void* W, void* Y, const void* R, in
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
-  if (epi >= 10) {                                   // schedule variants (tuning), plain epilogue
+  if (epi >= 10) {                                   // structure variants (tuning), plain epilogue
     switch (epi - 10) {
-      case 0: gemm_tn_256a<0, 0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
-      case 1: gemm_tn_256a<0, 1><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
-      case 2: gemm_tn_256a<0, 2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
-      case 3: gemm_tn_256a<0, 3><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 0: gemm_tn_256a<0, 0, 4><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 1: gemm_tn_256a<0, 1, 4><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 2: gemm_tn_256a<0, 0, 5><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 3: gemm_tn_256a<0, 1, 5><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 4:
+        if (K % (4 * KS)) return 1;
+        gemm_tn_256a<0, 0, 4, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K);
+        return 0;
+      case 5:
+        if (K % (4 * KS)) return 1;
+        gemm_tn_256a<0, 0, 4, true, 2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K);
+        return 0;
+      case 6:
+        if (K % (4 * KS)) return 1;
+        gemm_tn_256a<0, 0, 4, true, 1><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K);
+        return 0;
+      case 7:
+        if (K % (4 * KS)) return 1;
+        gemm_tn_256a<0, 0, 4, true, 3><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K);
+        return 0;
       default: return 2;
     }
   }

@@ -1,0 +1,262 @@
+// K1 (large-M path), production: 256x256 tile, ONE wave per SIMD (4 waves,
+// 2x2), 128x128 outputs per wave = 8x8 v_mfma_f32_16x16x32_bf16 tiles whose
+// 256 fp32 accumulators live in AGPRs, operands staged by LDS-DMA in
+// 128-byte rows.
+//   Y[M,N] = X[M,K] . W[N,K]^T (+ R | SwiGLU)   fp32 accumulate, bf16 out
+//
+// How it got here (profiles/gemm_tuning.md): the 8-wave kernels (gemm256.hip)
+// read 12 fragments per 32 MFMAs; a 128x128 wave tile reads 16 per 64.  With
+// the MFMAs as inline asm whose accumulators are "+a" operands
+// (gemm256a.hip), hipcc keeps the 256 accumulators in AGPRs, so one wave per
+// SIMD fits.  Without any staging that loop runs at 1.6-1.8 PF/s; the cost
+// left is the LDS-DMA issue (~60 cycles per 1 KiB instruction among MFMAs,
+// MI355X_MICROARCH.md), which falls by a third when an instruction covers
+// 8 rows x 128 B instead of 16 rows x 64 B (fewer cache lines per request)
+// - hence 64-deep k-tiles stored as 128-byte rows here.
+//
+// Pipeline, per 64-deep k-tile t (LDS slot c = t & 1, 64 KiB = A | B, each
+// 256 rows x 128 B; fragments F[0] = k-half 0, F[1] = k-half 1):
+//   half 0: 64 MFMAs from F[0]          || ds_read F[1] <- (t, k1) from slot c
+//   s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier
+//           (tile t+1's DMA, issued in half 1 of tile t-1, landed for every
+//            wave; nobody reads slot c any more)
+//   half 1: 64 MFMAs from F[1]          || ds_read F[0] <- (t+1, k0) from slot c^1
+//                                       || LDS-DMA tile t+2 -> slot c
+// One barrier per 128 MFMAs.  RAW: a slot is read only after the barrier that
+// follows every wave's vmcnt(0) for its DMA.  WAR: slot c is refilled only
+// after the barrier that follows every wave's lgkmcnt(0) for its last reads.
+// LDS rows of 128 B, 16-B chunk swizzle ^= row & 7, applied on the DMA source
+// address and the ds_read address (conflict-free: tools/lds_banks.py).
+// Rows past M / N read zeros: the buffer descriptors' range check; those
+// outputs are never stored.
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int ROWB = BK * 2;                        // 128-byte LDS rows
+constexpr int PIECE_B = 256 * ROWB;                 // one operand of a slot: 32 KiB
+constexpr int SLOT_B = 2 * PIECE_B;                 // A | B: 64 KiB
+
+DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// acc (AGPR) += B-fragment x A-fragment; an opaque statement, so hipcc keeps
+// the accumulator in AGPRs and issue order is program order
+DEV void mfma_a(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+struct Frags {
+  bf16x8 a[8];
+  bf16x8 b[8];
+};
+
+// grouped tile order: GROUP M-tiles share each W column panel in L2
+DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * nn;
+  const int g = t / per_group;
+  const int first_m = g * GROUP;
+  const int gsz = min(nm - first_m, GROUP);
+  m0 = (first_m + (t % per_group) % gsz) * BM;
+  n0 = ((t % per_group) / gsz) * BN;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
+                                                       const bf16* __restrict__ W,
+                                                       bf16* __restrict__ Y,
+                                                       const bf16* __restrict__ R, int M, int N,
+                                                       int K) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT_B];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  int m0, n0;
+  tile_coords(xcd_remap(blockIdx.x, nm * nn), nm, nn, m0, n0);
+
+  // ---- LDS-DMA: instruction q (0..31) of an operand fills rows 8q..8q+7,
+  //      lane-linearly (row 8q + lane/8, LDS chunk lane%8); wave w issues
+  //      q = 8w .. 8w+7.  Per lane: a 32-bit byte offset (row-in-8, swizzled
+  //      source chunk); the row group and the k position go in soffset.
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((size_t)M * K * 2),
+                                                     0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((size_t)N * K * 2),
+                                                     0x00020000);
+  const unsigned voff = (unsigned)(((lane >> 3) * K + (((lane & 7) ^ (lane >> 3)) << 3)) * 2);
+  const int rowA0 = m0 + 64 * wave, rowB0 = n0 + 64 * wave;    // first row of this wave's q's
+  auto dma1 = [&](int t, int slot, int i) {          // i < 8: A instruction i, else B i-8
+    const bool b = i >= 8;
+    const int q = i & 7;
+    const int soff = (((b ? rowB0 : rowA0) + 8 * q) * K + t * BK) * 2;
+    auto* dst = (__attribute__((address_space(3))) void*)(
+        smem + slot * SLOT_B + (b ? PIECE_B : 0) + (8 * wave + q) * 1024);
+    if (b) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, voff, soff, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, voff, soff, 0, 0);
+  };
+
+  // ---- fragment reads: wave (wm, wn) owns rows wm*128.., cols wn*128..;
+  //      lane (fr, fq) reads row fr of fragment i, k-chunk 4 kh + fq.  Fragment
+  //      i sits i * 2 KiB after fragment 0 with the same swizzle (row & 7 = fr & 7).
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  int rbase[2][2][2];                                // [slot][kh][A|B] LDS byte offsets
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int ch = ((4 * kh + fq) ^ (fr & 7)) * 16;
+      rbase[sl][kh][0] = sl * SLOT_B + (wm * 128 + fr) * ROWB + ch;
+      rbase[sl][kh][1] = sl * SLOT_B + PIECE_B + (wn * 128 + fr) * ROWB + ch;
+    }
+  auto fread1 = [&](int slot, int kh, Frags& f, int i) {   // i < 8: B[i], else A[i-8]
+    if (i < 8)
+      f.b[i] = *reinterpret_cast<const bf16x8*>(smem + rbase[slot][kh][1] + i * 2048);
+    else
+      f.a[i - 8] = *reinterpret_cast<const bf16x8*>(smem + rbase[slot][kh][0] + (i - 8) * 2048);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // accumulator zeroing (VALU v_accvgpr_write) -> first MFMA reading them as
+  // srcC needs wait states: pin the writes before a nop (asm statements keep
+  // their order; the empty "+a" statements depend on the writes)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+
+  const int nt = K / BK;                             // >= 2, even (launcher)
+  Frags F[2];
+  // prologue: tiles 0 and 1 in flight, tile 0 landed, F[0] <- (0, k0)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma1(0, 0, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma1(1, 1, i);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  raw_barrier();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) fread1(0, 0, F[0], i);
+  __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): clean waitcnt state at the loop head
+  asm volatile("s_nop 4" ::: "memory");
+
+  auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+  auto keep = [](const Frags& f) {                   // fragments stay allocated to here: hipcc
+#pragma unroll                                       // does not know the asm MFMAs read them
+    for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(f.a[i]), "v"(f.b[i]));
+  };
+  // one 64-deep k-tile; C = t & 1 static (the loop is unrolled by two).  Every
+  // tile runs the full body, also the last two: their DMAs of tiles >= nt and
+  // their reads of tile nt are never consumed (a peeled tail would be separate
+  // code where hipcc re-assigns the accumulators with v_accvgpr_mov's, VALU
+  // writes the unpadded asm MFMAs next to them race with).
+  auto tile = [&](int t, auto c_c) {
+    constexpr int C = decltype(c_c)::value;
+    fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {                   // half 0: F[0], reads of (t, k1)
+      const int i0 = 2 * j, i1 = 2 * j + 1;
+      mfma_a(acc[i0 >> 3][i0 & 7], F[0].b[i0 & 7], F[0].a[i0 >> 3]);
+      mfma_a(acc[i1 >> 3][i1 & 7], F[0].b[i1 & 7], F[0].a[i1 >> 3]);
+      if ((j & 1) == 0) fread1(C, 1, F[1], j >> 1);
+      fence();
+    }
+    keep(F[0]);
+    // tile t+1 landed (own DMAs), and this wave's reads of slot C are done
+    __builtin_amdgcn_s_waitcnt(0x0070);              // vmcnt(0) lgkmcnt(0)
+    raw_barrier();
+    fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {                   // half 1: F[1], reads of (t+1, k0), DMA t+2
+      const int i0 = 2 * j, i1 = 2 * j + 1;
+      mfma_a(acc[i0 >> 3][i0 & 7], F[1].b[i0 & 7], F[1].a[i0 >> 3]);
+      mfma_a(acc[i1 >> 3][i1 & 7], F[1].b[i1 & 7], F[1].a[i1 >> 3]);
+      if ((j & 1) == 0) fread1(C ^ 1, 0, F[0], j >> 1);
+      else dma1(t + 2, C, j >> 1);
+      fence();
+    }
+    keep(F[1]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  for (int t = 0; t < nt; t += 2) {
+    tile(t, C0{});
+    tile(t + 1, C1{});
+  }
+  // drain the trailing (unconsumed) DMAs before the workgroup's LDS is released,
+  // and pad MFMA results -> VALU reads (inline asm is not padded)
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  // ---- epilogue: lane holds Y[m][n .. n+3] of each 16x16 tile
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    const int m = m0 + wm * 128 + mt * 16 + fr;
+    if (m >= M) continue;
+    if constexpr (EPI == 2) {
+      const int F2 = N >> 1;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int f = ((n0 + wn * 128) >> 1) + p * 16 + fq * 4;
+        if (f >= F2) continue;
+        const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
+        *reinterpret_cast<bf16x4*>(Y + (size_t)m * F2 + f) = o;
+      }
+      continue;
+    }
+#pragma unroll
+    for (int nt_ = 0; nt_ < 8; ++nt_) {
+      const int n = n0 + wn * 128 + nt_ * 16 + fq * 4;
+      if (n >= N) continue;
+      f32x4 v = acc[mt][nt_];
+      if (EPI == 1) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+      *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+    }
+  }
+}
+
+}  // namespace
+
+// 0 ok; 1 K not a multiple of 128; 3 an operand past the 2 GiB buffer range
+int gemm256d_ok(int M, int N, int K) {
+  if (K % (2 * BK)) return 1;
+  if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31)) return 3;
+  return 0;
+}
+
+int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        int epi, hipStream_t s) {
+  if (const int rc = gemm256d_ok(M, N, K)) return rc;
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const dim3 grid(nm * nn);
+  auto x = (const bf16*)X;
+  auto w = (const bf16*)W;
+  auto y = (bf16*)Y;
+  auto r = (const bf16*)R;
+  switch (epi) {
+    case 0: gemm_tn_256d<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+    case 1: gemm_tn_256d<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
+    case 2: gemm_tn_256d<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+    default: return 2;
+  }
+}
