@@ -157,11 +157,12 @@ int gemm_tn_check(int M, int N, int K) {
 }
 
 // Tile selection by a wave-quantisation time model calibrated on MI355X
-// (tools/bench_gemm.py): the 256x256 kernel sustains ~1.22 PF/s with one
-// workgroup per CU (256 concurrent tiles), the 128x128 kernel ~1.04 PF/s with
-// two per CU (512 concurrent tiles).  Predicted time = full waves of tiles x
+// (tools/bench_gemm.py): the 256x256 kernels sustain ~1.40 PF/s (AGPR kernel,
+// gemm256d.hip) / ~1.22 PF/s (ping-pong) with one workgroup per CU (256
+// concurrent tiles), the 128x128 kernel ~1.04 PF/s with two per CU (512).  Predicted time = full waves of tiles x
 // per-wave time; pick the smaller.
 double gemm256_waves(int M, int N, int K);
+double gemm256_rate(int M, int N, int K);
 int gemm256_num_cus();
 
 int gemm_select(int M, int N, int K) {
@@ -169,7 +170,7 @@ int gemm_select(int M, int N, int K) {
   const double G = (double)gemm256_num_cus();
   const double t128 = (double)(((M + 127) / 128) * ((N + 127) / 128));
   // 256^2 waves (stream-K hybrid where it pays) vs 128^2 waves at 2 blocks/CU
-  const double cost256 = gemm256_waves(M, N, K) * G * 4.0 / 1.22;   // 128^2-tile units / PF
+  const double cost256 = gemm256_waves(M, N, K) * G * 4.0 / gemm256_rate(M, N, K);   // 128^2 units / PF
   const double cost128 = ceil(t128 / (2.0 * G)) * 2.0 * G / 1.04;
   return cost256 < cost128 ? 1 : 0;
 }

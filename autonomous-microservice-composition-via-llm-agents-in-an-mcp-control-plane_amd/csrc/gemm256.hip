@@ -371,6 +371,7 @@ int launch_gemm_tn_256a(const void* X, const void* W, void* Y, const void* R, in
                         int epi, hipStream_t s);
 int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         int epi, hipStream_t s);
+int gemm256d_ok(int M, int N, int K);
 
 // tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
@@ -474,6 +475,15 @@ static bool splitk_auto() {
   return on == 1;
 }
 
+static bool use_256d() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("MCP_GEMM256");
+    on = !(e && e[0] == 'p' && e[1] == 'p');
+  }
+  return on == 1;
+}
+
 int choose_splits(int M, int N, int K, int G) {
   if (!splitk_auto()) return 1;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -494,6 +504,11 @@ template <int EPI, class VAR = V256Default>
 void launch_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                 int splits, hipStream_t s) {
   // splits: 0 auto, 1 data-parallel, >1 forced split-K
+  // production: the one-wave-per-SIMD AGPR kernel (gemm256d.hip) wherever its
+  // shape rules hold (K % 128, N % 256); MCP_GEMM256=pp keeps the ping-pong kernel
+  if (splits <= 1 && use_256d() && gemm256d_ok(M, N, K) == 0 &&
+      launch_gemm_tn_256d(X, W, Y, R, M, N, K, EPI, s) == 0)
+    return;
   SkDevice& sd = sk_device();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (splits <= 0) splits = choose_splits(M, N, K, sd.G);
@@ -517,6 +532,12 @@ double gemm256_waves(int M, int N, int K) {
 }
 
 int gemm256_num_cus() { return sk_device().G; }
+
+// sustained rate of the 256^2 path for this shape, PF/s (tools/bench_gemm.py):
+// the AGPR kernel where it applies, else the ping-pong kernel
+double gemm256_rate(int M, int N, int K) {
+  return use_256d() && gemm256d_ok(M, N, K) == 0 ? 1.40 : 1.22;
+}
 
 void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         hipStream_t s) {

@@ -27,8 +27,8 @@
 // after the barrier that follows every wave's lgkmcnt(0) for its last reads.
 // LDS rows of 128 B, 16-B chunk swizzle ^= row & 7, applied on the DMA source
 // address and the ds_read address (conflict-free: tools/lds_banks.py).
-// Rows past M / N read zeros: the buffer descriptors' range check; those
-// outputs are never stored.
+// Rows past M re-read row M-1 (clamped per-lane offsets); their outputs are
+// never stored.
 #include <type_traits>
 
 #include "common.h"
@@ -84,23 +84,33 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   tile_coords(xcd_remap(blockIdx.x, nm * nn), nm, nn, m0, n0);
 
   // ---- LDS-DMA: instruction q (0..31) of an operand fills rows 8q..8q+7,
-  //      lane-linearly (row 8q + lane/8, LDS chunk lane%8); wave w issues
-  //      q = 8w .. 8w+7.  Per lane: a 32-bit byte offset (row-in-8, swizzled
-  //      source chunk); the row group and the k position go in soffset.
+  //      lane-linearly (row 8q + lane/8, LDS chunk lane%8, swizzled source
+  //      chunk); wave w issues q = 8w .. 8w+7.  The k position goes in soffset.
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((size_t)M * K * 2),
                                                      0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((size_t)N * K * 2),
                                                      0x00020000);
-  const unsigned voff = (unsigned)(((lane >> 3) * K + (((lane & 7) ^ (lane >> 3)) << 3)) * 2);
-  const int rowA0 = m0 + 64 * wave, rowB0 = n0 + 64 * wave;    // first row of this wave's q's
+  // The buffer range check covers voffset (+ the instruction offset) but NOT
+  // soffset, so rows that can fall past the end of X (the last M-tile) are
+  // clamped in per-lane offsets; W rows are always in range (N % 256 == 0,
+  // launcher) and step through soffset.
+  const int chunk = (lane & 7) ^ (lane >> 3);
+  unsigned offA[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    offA[q] = (unsigned)(((size_t)min(m0 + 64 * wave + 8 * q + (lane >> 3), M - 1) * K + chunk * 8) * 2);
+  const unsigned offB = (unsigned)(((lane >> 3) * K + chunk * 8) * 2);
+  const int rowB0 = n0 + 64 * wave;                  // first W row of this wave's instructions
   auto dma1 = [&](int t, int slot, int i) {          // i < 8: A instruction i, else B i-8
     const bool b = i >= 8;
     const int q = i & 7;
-    const int soff = (((b ? rowB0 : rowA0) + 8 * q) * K + t * BK) * 2;
     auto* dst = (__attribute__((address_space(3))) void*)(
         smem + slot * SLOT_B + (b ? PIECE_B : 0) + (8 * wave + q) * 1024);
-    if (b) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, voff, soff, 0, 0);
-    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, voff, soff, 0, 0);
+    if (b)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, offB, ((rowB0 + 8 * q) * K + t * BK) * 2,
+                                               0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA[q], t * BK * 2, 0, 0);
   };
 
   // ---- fragment reads: wave (wm, wn) owns rows wm*128.., cols wn*128..;
@@ -237,9 +247,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
 
 }  // namespace
 
-// 0 ok; 1 K not a multiple of 128; 3 an operand past the 2 GiB buffer range
+// 0 ok; 1 K not a multiple of 128; 2 N not a multiple of 256; 3 an operand
+// past the 2 GiB buffer range
 int gemm256d_ok(int M, int N, int K) {
   if (K % (2 * BK)) return 1;
+  if (N % BN) return 2;
   if ((size_t)M * K * 2 >= (1ull << 31) || (size_t)N * K * 2 >= (1ull << 31)) return 3;
   return 0;
 }

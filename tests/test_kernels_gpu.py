@@ -324,3 +324,26 @@ def test_gemm_skinny(M, N, K):
     Wi = ref.interleave_gate_up(g, u).contiguous()
     e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
     assert rel_err(ops.gemm_silu(X, Wi), e) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(2600, 4096, 4096), (100, 512, 256), (513, 1024, 384),
+                                   (4096, 6144, 4096)])
+def test_gemm_256d_agpr(M, N, K):
+    """One-wave-per-SIMD AGPR kernel (gemm256d.hip, variant 49 / production 256 path):
+    partial last M-tile (clamped rows), plain / residual in place / SwiGLU."""
+    torch.manual_seed(6)
+    L = ops.lib()
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    L.gemm_variant(X, W, Y, 49)
+    assert rel_err(Y, ref.gemm(X, W)) < 1e-2
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    R2 = R.clone()
+    ops.gemm(X, W, R=R2, out=R2, algo=1)
+    assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+    g, u = W[: N // 2], W[N // 2:]
+    Wi = ref.interleave_gate_up(g, u).contiguous()
+    y = ops.gemm_silu(X, Wi)
+    e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+    assert rel_err(y, e) < 2e-2
