@@ -67,13 +67,16 @@ struct AttnArgs {
 //         sequence that shares one registry prefix, 16-token tiles that mix
 //         sequences (they attend to the same K/V), no mask (every query sits
 //         after the prefix).  Writes normalised O and its LSE.
-template <int NW, int G, int MODE>
+template <int NW, int G, int MODE, int NBUF_ = 0>
 __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   constexpr int TPW = 16 / G;                 // tokens per wave
   constexpr int QT = NW * TPW;                // tokens per work item
   constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
   static_assert(PIECES % NW == 0, "pieces split evenly");
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];   // [buf][K|V][64][128]
+  // 1-wave (decode) items are latency-bound: one 32 KiB K|V buffer instead of
+  // two lets 5 instead of 2 of them share a CU (LDS 160 KiB)
+  constexpr int NBUF = NBUF_ > 0 ? NBUF_ : (NW == 1 ? 1 : 2);
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * 2 * TILE];   // [buf][K|V][64][128]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kvh = blockIdx.y;
@@ -144,11 +147,16 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_part = 0.f;
 
-  if (kt0 < ntiles) stage(kt0, 0);
-  __syncthreads();
+  if (NBUF == 2 && kt0 < ntiles) stage(kt0, 0);
+  if (NBUF == 2) __syncthreads();
   for (int kt = kt0; kt < ntiles; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
+    const int cur = NBUF == 2 ? (kt - kt0) & 1 : 0;
+    if (NBUF == 1) {
+      stage(kt, 0);
+      __syncthreads();             // its fence drains the LDS-DMA (vmcnt(0))
+    } else if (kt + 1 < ntiles) {
+      stage(kt + 1, cur ^ 1);
+    }
     const bf16* Kl = smem + cur * 2 * TILE;
     const bf16* Vl = Kl + TILE;
 
@@ -256,7 +264,10 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
 template <int G>
 void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s) {
   const dim3 grid(nwork, a.Hkv);
-  if (nw == 1)
+  static const int nw1_bufs = getenv("MCP_ATTN_NW1_BUFS") ? atoi(getenv("MCP_ATTN_NW1_BUFS")) : 1;
+  if (nw == 1 && nw1_bufs == 2)
+    attn_kernel<1, G, 0, 2><<<grid, 64, 0, s>>>(a);
+  else if (nw == 1)
     attn_kernel<1, G, 0><<<grid, 64, 0, s>>>(a);
   else
     attn_kernel<4, G, 0><<<grid, 256, 0, s>>>(a);

@@ -16,7 +16,8 @@ from mcp_amd.engine.batch import StepInputs, pack  # noqa: E402
 
 dev = "cuda"
 Hq, Hkv, D = 32, 8, 128
-S, ql, prefix = 256, 16, 704
+# argv[1]: new tokens per request (16: 4-wave items; <= 8: 1-wave decode items)
+S, ql, prefix = 256, (int(sys.argv[1]) if len(sys.argv) > 1 else 16), 704
 own = 200
 nb_pre = prefix // 64
 rng = np.random.default_rng(0)
@@ -82,6 +83,6 @@ for nw, ws, wq in d.attn.work_lists():
 t_prefix()
 t_own()
 err = ((out.float() - ref.float()).norm() / ref.norm()).item()
-print(json.dumps({"prefix_us": round(tp, 1), "prefix_tflops": round(fl_pre / tp / 1e6, 1),
+print(json.dumps({"ql": ql, "prefix_us": round(tp, 1), "prefix_tflops": round(fl_pre / tp / 1e6, 1),
                   "own_us": round(to, 1), "own_tflops": round(fl_own / to / 1e6, 1),
                   "cascade_vs_plain_rel_err": err}))

@@ -1,14 +1,18 @@
 """Summarise a rocprofv3 SQLite output (``-d DIR -o run`` -> run_results.db):
 per-kernel calls / total / mean time and a per-category breakdown.
 
-    python tools/rocpd_summary.py gpurun_out/prof11/run_results.db > profiles/x.md
+    python tools/rocpd_summary.py gpurun_out/prof11/run_results.db [last_ms] > profiles/x.md
+
+``last_ms``: only kernels that start in the last ``last_ms`` milliseconds of
+the trace (e.g. the timed steps of bench.py, after model init and warm-up).
 """
 import re
 import sqlite3
 import sys
 from collections import defaultdict
 
-CATS = [("gemm (MFMA 256x256)", r"gemm_tn_256"), ("gemm (MFMA 128x128)", r"gemm_tn_128"),
+CATS = [("gemm (MFMA 256x256, AGPR 1 wave/SIMD)", r"gemm_tn_256d"),
+        ("gemm (MFMA 256x256)", r"gemm_tn_256"), ("gemm (MFMA 128x128)", r"gemm_tn_128"),
         ("gemm (skinny K2)", r"gemm_skinny"), ("attention", r"attn_"),
         ("sampling", r"sample_"), ("rmsnorm", r"rmsnorm"), ("rope+kv write", r"rope"),
         ("embedding", r"embedding"), ("top-k", r"topk|l2norm"), ("kv copy", r"copy_blocks"),
@@ -21,11 +25,14 @@ def short(name):
     return (m.group(1) + "<" + m.group(2)[:40] + ">") if m else n[:80]
 
 
-def main(db):
+def main(db, last_ms=None):
     c = sqlite3.connect(db)
+    t_end = c.execute("select max(end) from kernels").fetchone()[0]
+    t0 = t_end - int(last_ms * 1e6) if last_ms else 0
     rows = list(c.execute("select name, count(*), sum(duration), avg(duration) from kernels "
-                          "group by name order by sum(duration) desc"))
-    span = c.execute("select max(end) - min(start) from kernels").fetchone()[0]
+                          "where start >= ? group by name order by sum(duration) desc", (t0,)))
+    span = c.execute("select max(end) - min(start) from kernels where start >= ?",
+                     (t0,)).fetchone()[0]
     total = sum(r[2] for r in rows)
     cats = defaultdict(float)
     for name, n, tot, avg in rows:
@@ -46,4 +53,4 @@ def main(db):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else None)
