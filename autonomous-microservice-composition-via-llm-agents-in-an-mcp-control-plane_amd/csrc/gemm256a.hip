@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256a(const bf16* __restrict__ 
     doffB[i] = (unsigned)(((size_t)min(n0 + row, N - 1) * K + ch * 8) * 2);
   }
   auto dma1 = [&](int st, int slot, int i) {           // i < 4: A instruction i, else B i-4
-    const int soff = st * KS * 2;
+    const int soff = min(st, K / KS - 1) * KS * 2;   // soffset is not range-checked
     auto* dst = (__attribute__((address_space(3))) void*)(
         smem + slot * 2 * PIECE + (i < 4 ? 0 : PIECE) + (4 * wave + (i & 3)) * 512);
     if (i < 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, doffA[i], soff, 0, 0);
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256a(const bf16* __restrict__ 
 
   u32x4_t G[2][8];                                   // [set][A0..3 | B0..3], set = step & 1
   auto gload1 = [&](int st, u32x4_t (&g)[8], int i) {      // i < 4: A chunk i, else B chunk i-4
-    const int soff = st * KS * 2;
+    const int soff = min(st, K / KS - 1) * KS * 2;   // soffset is not range-checked
     if (i < 4)
       g[i] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsA, goffA[i], soff, 0));
     else

@@ -101,16 +101,20 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     offA[q] = (unsigned)(((size_t)min(m0 + 64 * wave + 8 * q + (lane >> 3), M - 1) * K + chunk * 8) * 2);
   const unsigned offB = (unsigned)(((lane >> 3) * K + chunk * 8) * 2);
   const int rowB0 = n0 + 64 * wave;                  // first W row of this wave's instructions
+  // k-tile t of the trailing (unconsumed) DMAs is clamped to the last one:
+  // soffset is outside the range check, so t >= nt would read past the end of
+  // the last row of X / W
+  const int nt = K / BK;                             // >= 2, even (launcher)
   auto dma1 = [&](int t, int slot, int i) {          // i < 8: A instruction i, else B i-8
     const bool b = i >= 8;
     const int q = i & 7;
+    const int kb = min(t, nt - 1) * BK * 2;
     auto* dst = (__attribute__((address_space(3))) void*)(
         smem + slot * SLOT_B + (b ? PIECE_B : 0) + (8 * wave + q) * 1024);
     if (b)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, offB, ((rowB0 + 8 * q) * K + t * BK) * 2,
-                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, offB, (rowB0 + 8 * q) * K * 2 + kb, 0, 0);
     else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA[q], t * BK * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA[q], kb, 0, 0);
   };
 
   // ---- fragment reads: wave (wm, wn) owns rows wm*128.., cols wn*128..;
@@ -147,7 +151,6 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
 
-  const int nt = K / BK;                             // >= 2, even (launcher)
   Frags F[2];
   // prologue: tiles 0 and 1 in flight, tile 0 landed, F[0] <- (0, k0)
 #pragma unroll
@@ -167,8 +170,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(f.a[i]), "v"(f.b[i]));
   };
   // one 64-deep k-tile; C = t & 1 static (the loop is unrolled by two).  Every
-  // tile runs the full body, also the last two: their DMAs of tiles >= nt and
-  // their reads of tile nt are never consumed (a peeled tail would be separate
+  // tile runs the full body, also the last two: their DMAs (clamped to the last
+  // k-tile) and their reads of tile nt are never consumed (a peeled tail would be separate
   // code where hipcc re-assigns the accumulators with v_accvgpr_mov's, VALU
   // writes the unpadded asm MFMAs next to them race with).
   auto tile = [&](int t, auto c_c) {
