@@ -372,6 +372,9 @@ int launch_gemm_tn_256a(const void* X, const void* W, void* Y, const void* R, in
 int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         int epi, hipStream_t s);
 int gemm256d_ok(int M, int N, int K);
+int launch_gemm_tn_256sk(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                         int epi, int force, hipStream_t s);
+double gemm256sk_waves(int M, int N, int K);
 
 // tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
@@ -398,6 +401,7 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48:   // 4 waves, AGPR acc, structure v - 41
       return launch_gemm_tn_256a(X, W, Y, nullptr, M, N, K, 10 + v - 41, s);
     case 49: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);   // 1 wave/SIMD, 128-B DMA rows
+    case 50: return launch_gemm_tn_256sk(X, W, Y, nullptr, M, N, K, 0, 1, s);   // its stream-K form
     default: return 1;
   }
 }
@@ -506,9 +510,11 @@ void launch_256(const void* X, const void* W, void* Y, const void* R, int M, int
   // splits: 0 auto, 1 data-parallel, >1 forced split-K
   // production: the one-wave-per-SIMD AGPR kernel (gemm256d.hip) wherever its
   // shape rules hold (K % 128, N % 256); MCP_GEMM256=pp keeps the ping-pong kernel
-  if (splits <= 1 && use_256d() && gemm256d_ok(M, N, K) == 0 &&
-      launch_gemm_tn_256d(X, W, Y, R, M, N, K, EPI, s) == 0)
-    return;
+  if (splits <= 1 && use_256d() && gemm256d_ok(M, N, K) == 0) {
+    // stream-K (gemm256sk.hip) where the data-parallel grid's last wave is mostly empty
+    if (splits <= 0 && launch_gemm_tn_256sk(X, W, Y, R, M, N, K, EPI, 0, s) == 0) return;
+    if (launch_gemm_tn_256d(X, W, Y, R, M, N, K, EPI, s) == 0) return;
+  }
   SkDevice& sd = sk_device();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (splits <= 0) splits = choose_splits(M, N, K, sd.G);
@@ -524,8 +530,9 @@ void launch_256(const void* X, const void* W, void* Y, const void* R, int M, int
 
 }  // namespace
 
-// effective waves of the 256^2 kernel (split-K trims the quantisation of the last wave)
+// effective waves of the 256^2 kernel (stream-K / split-K trim the quantisation of the last wave)
 double gemm256_waves(int M, int N, int K) {
+  if (use_256d() && gemm256d_ok(M, N, K) == 0) return gemm256sk_waves(M, N, K);
   SkDevice& sd = sk_device();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   return split_cost(tiles, sd.G, choose_splits(M, N, K, sd.G));

@@ -336,8 +336,10 @@ def test_gemm_256d_agpr(M, N, K):
     X = torch.randn(M, K, device=DEV).bfloat16()
     W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    L.gemm_variant(X, W, Y, 49)
-    assert rel_err(Y, ref.gemm(X, W)) < 1e-2
+    for v in (49, 50):                 # data-parallel, stream-K (last-arriver slab sums)
+        Y.zero_()
+        L.gemm_variant(X, W, Y, v)
+        assert rel_err(Y, ref.gemm(X, W)) < 1e-2, v
     R = torch.randn(M, N, device=DEV).bfloat16()
     R2 = R.clone()
     ops.gemm(X, W, R=R2, out=R2, algo=1)
