@@ -3,6 +3,7 @@
 // graph-capturable; every op runs on the current HIP stream of the tensor's
 // device.
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 #include <ATen/hip/HIPContext.h>
 
 #include "kernels.h"
@@ -103,6 +104,12 @@ void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64
   TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_variant: unsupported shape");
   TORCH_CHECK(launch_gemm_tn_256_variant(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, v,
                                          stream()) == 0, "bad variant");
+}
+
+void gemm_plan_set_py(int64_t N, int64_t K, const std::vector<int64_t>& codes) {
+  std::vector<int> c(codes.begin(), codes.end());
+  for (int v : c) TORCH_CHECK(v >= -1 && v <= 2, "gemm plan code must be -1..2");
+  gemm_plan_set((int)N, (int)K, c.data(), (int)c.size());
 }
 
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
@@ -322,6 +329,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("algo") = -1);
   m.def("gemm_select", &gemm_select);
   m.def("gemm_variant", &gemm_variant);
+  m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
+  m.def("gemm_plan_clear", &gemm_plan_clear);
+  m.def("gemm_plan_lookup", &gemm_plan_lookup);
   m.def("gemm_silu", &gemm_silu);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);

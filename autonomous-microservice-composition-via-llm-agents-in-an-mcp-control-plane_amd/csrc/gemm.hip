@@ -17,6 +17,8 @@
 //  * operands swapped in the MFMA (W as A, X as B) so each lane ends with 4
 //    consecutive output columns of one row -> 8-byte bf16 stores.
 //  * XCD-aware bijective block remap + grouped tile order for L2 reuse (T1).
+#include <vector>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -158,20 +160,61 @@ int gemm_tn_check(int M, int N, int K) {
 
 // Tile selection by a wave-quantisation time model calibrated on MI355X
 // (tools/bench_gemm.py): the 256x256 kernels sustain ~1.40 PF/s (AGPR kernel,
-// gemm256d.hip) / ~1.22 PF/s (ping-pong) with one workgroup per CU (256
-// concurrent tiles), the 128x128 kernel ~1.04 PF/s with two per CU (512).  Predicted time = full waves of tiles x
+// gemm256d.hip, 256- or 192-row tiles) / ~1.22 PF/s (ping-pong) with one
+// workgroup per CU (256 concurrent tiles), the 128x128 kernel ~0.9 PF/s with
+// two per CU (512).  Predicted time = full waves of tiles x
 // per-wave time; pick the smaller.
 double gemm256_waves(int M, int N, int K);
 double gemm256_rate(int M, int N, int K);
 int gemm256_num_cus();
 
+// ---- measured tile plans (tools/tune_gemm_plan.py -> profiles/gemm_plan_*.json,
+// loaded by ops.lib()): per (N, K) weight shape one code per 64-row M bucket
+// (bucket b = rows (64 b, 64 b + 64]; every tile height divides 64, so all M
+// of a bucket have the tile counts of its top row, the row that was timed):
+// 0 = 128^2 kernel, 1 = AGPR kernel with 256-row tiles, 2 = with 192-row tiles.
+// Written once at load, before any launch; read-only afterwards.
+namespace {
+struct GemmPlan {
+  int N, K;
+  std::vector<signed char> code;
+};
+std::vector<GemmPlan> g_plans;
+}  // namespace
+
+void gemm_plan_set(int N, int K, const int* codes, int n) {
+  std::vector<signed char> c(codes, codes + n);
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.code = std::move(c);
+      return;
+    }
+  g_plans.push_back({N, K, std::move(c)});
+}
+
+void gemm_plan_clear() { g_plans.clear(); }
+
+// -1 = no measured plan for this shape
+int gemm_plan_lookup(int M, int N, int K) {
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.code.size() ? p.code[b] : -1;
+    }
+  return -1;
+}
+
 int gemm_select(int M, int N, int K) {
   if (M < 256 || N < 256 || K < 128) return 0;
+  const int plan = gemm_plan_lookup(M, N, K);
+  if (plan >= 0 && (plan == 0 || gemm256d_ok(M, N, K) == 0)) return plan == 0 ? 0 : 1;
   const double G = (double)gemm256_num_cus();
   const double t128 = (double)(((M + 127) / 128) * ((N + 127) / 128));
   // 256^2 waves (stream-K hybrid where it pays) vs 128^2 waves at 2 blocks/CU
   const double cost256 = gemm256_waves(M, N, K) * G * 4.0 / gemm256_rate(M, N, K);   // 128^2 units / PF
-  const double cost128 = ceil(t128 / (2.0 * G)) * 2.0 * G / 1.04;
+  // 128^2 kernel: ~0.9 PF/s at the decode-step shapes (M ~ 2600, measured
+  // 0.68-1.07; profiles/gemm_tuning.md)
+  const double cost128 = ceil(t128 / (2.0 * G)) * 2.0 * G / 0.90;
   return cost256 < cost128 ? 1 : 0;
 }
 

@@ -375,6 +375,10 @@ int gemm256d_ok(int M, int N, int K);
 int launch_gemm_tn_256sk(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                          int epi, int force, hipStream_t s);
 double gemm256sk_waves(int M, int N, int K);
+int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                           int K, int epi, int bm, hipStream_t s);
+int gemm256d_height(int M, int N, int K);
+double gemm256d_waves_bm(int M, int N, int K, int bm);
 
 // tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
@@ -400,8 +404,10 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 40: return launch_gemm_tn_256i(X, W, Y, nullptr, M, N, K, 0, s);  // one barrier per K-tile
     case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48:   // 4 waves, AGPR acc, structure v - 41
       return launch_gemm_tn_256a(X, W, Y, nullptr, M, N, K, 10 + v - 41, s);
-    case 49: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);   // 1 wave/SIMD, 128-B DMA rows
+    case 49: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 256, s);   // 1 wave/SIMD, 128-B DMA rows
     case 50: return launch_gemm_tn_256sk(X, W, Y, nullptr, M, N, K, 0, 1, s);   // its stream-K form
+    case 51: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 192, s);   // 192-row tiles
+    case 52: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);          // height by cost model
     default: return 1;
   }
 }
@@ -532,7 +538,8 @@ void launch_256(const void* X, const void* W, void* Y, const void* R, int M, int
 
 // effective waves of the 256^2 kernel (stream-K / split-K trim the quantisation of the last wave)
 double gemm256_waves(int M, int N, int K) {
-  if (use_256d() && gemm256d_ok(M, N, K) == 0) return gemm256sk_waves(M, N, K);
+  if (use_256d() && gemm256d_ok(M, N, K) == 0)       // tile height chosen per shape (256 / 192)
+    return fmin(gemm256d_waves_bm(M, N, K, gemm256d_height(M, N, K)), gemm256sk_waves(M, N, K));
   SkDevice& sd = sk_device();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   return split_cost(tiles, sd.G, choose_splits(M, N, K, sd.G));

@@ -29,6 +29,12 @@
 // address and the ds_read address (conflict-free: tools/lds_banks.py).
 // Rows past M re-read row M-1 (clamped per-lane offsets); their outputs are
 // never stored.
+//
+// Tile height BMT = 256 or 192 (96x128 per wave, 6x8 MFMA tiles): M = 2600
+// rows (a decode step of the headline bench) are 11 M-tiles of 256 - 176
+// tiles for N = 4096, 69 % of 256 CUs - but 14 M-tiles of 192 - 224 tiles,
+// 88 %.  gemm.hip picks the height by a wave-quantisation cost model (the
+// same choice as hipBLASLt's MT192x256 kernels for these shapes).
 #include <type_traits>
 
 #include "common.h"
@@ -36,10 +42,9 @@
 
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int BN = 256, BK = 64;
 constexpr int ROWB = BK * 2;                        // 128-byte LDS rows
-constexpr int PIECE_B = 256 * ROWB;                 // one operand of a slot: 32 KiB
-constexpr int SLOT_B = 2 * PIECE_B;                 // A | B: 64 KiB
+constexpr int PIECE_BB = 256 * ROWB;                // the W operand of a slot: 32 KiB
 
 DEV void raw_barrier() {
   asm volatile("" ::: "memory");
@@ -53,39 +58,55 @@ DEV void mfma_a(f32x4& acc, const bf16x8& b, const bf16x8& a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
 
+template <int MTW>
 struct Frags {
-  bf16x8 a[8];
+  bf16x8 a[MTW];
   bf16x8 b[8];
 };
 
 // grouped tile order: GROUP M-tiles share each W column panel in L2
-DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
+DEV void tile_coords(int t, int nm, int nn, int bm, int& m0, int& n0) {
   constexpr int GROUP = 4;
   const int per_group = GROUP * nn;
   const int g = t / per_group;
   const int first_m = g * GROUP;
   const int gsz = min(nm - first_m, GROUP);
-  m0 = (first_m + (t % per_group) % gsz) * BM;
+  m0 = (first_m + (t % per_group) % gsz) * bm;
   n0 = ((t % per_group) / gsz) * BN;
 }
 
-template <int EPI>
+// ops n spread over P slots: how many start at slot j, and the first index
+constexpr int ops_at(int j, int n, int P) { return ((j + 1) * n) / P - (j * n) / P; }
+constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
+
+template <int EPI, int BMT>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
                                                        int K) {
+  static_assert(BMT == 256 || BMT == 192, "tile height");
+  constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (8 or 6)
+  constexpr int WROWS = BMT / 2;                    // rows per wave (128 or 96)
+  constexpr int PIECE_A = BMT * ROWB;               // the X operand of a slot
+  constexpr int SLOT_B = PIECE_A + PIECE_BB;
+  constexpr int QA = BMT / 32;                      // A DMA instructions per wave (8 or 6)
+  constexpr int NDMA = QA + 8;                      // DMA instructions per wave and k-tile
+  constexpr int NRD = 8 + MTW;                      // fragment reads per wave and k-half
+  constexpr int NMF = MTW * 8;                      // MFMAs per wave and k-half
+  constexpr int NP = NMF / 2;                       // MFMA pairs per k-half
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT_B];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  const int nm = (M + BMT - 1) / BMT, nn = (N + BN - 1) / BN;
   int m0, n0;
-  tile_coords(xcd_remap(blockIdx.x, nm * nn), nm, nn, m0, n0);
+  tile_coords(xcd_remap(blockIdx.x, nm * nn), nm, nn, BMT, m0, n0);
 
-  // ---- LDS-DMA: instruction q (0..31) of an operand fills rows 8q..8q+7,
+  // ---- LDS-DMA: instruction q of an operand fills rows 8q..8q+7,
   //      lane-linearly (row 8q + lane/8, LDS chunk lane%8, swizzled source
-  //      chunk); wave w issues q = 8w .. 8w+7.  The k position goes in soffset.
+  //      chunk); wave w issues A's q = QA w .. QA w + QA-1 and W's 8w .. 8w+7.
+  //      The k position goes in soffset.
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((size_t)M * K * 2),
                                                      0x00020000);
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((size_t)N * K * 2),
@@ -95,29 +116,31 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // clamped in per-lane offsets; W rows are always in range (N % 256 == 0,
   // launcher) and step through soffset.
   const int chunk = (lane & 7) ^ (lane >> 3);
+  // (sized 8, not QA: an array sized by a local constexpr and captured by the
+  // DMA lambda makes hipcc's host pass silently drop the kernel's stub)
   unsigned offA[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q)
-    offA[q] = (unsigned)(((size_t)min(m0 + 64 * wave + 8 * q + (lane >> 3), M - 1) * K + chunk * 8) * 2);
+  for (int q = 0; q < QA; ++q)
+    offA[q] = (unsigned)(((size_t)min(m0 + 8 * QA * wave + 8 * q + (lane >> 3), M - 1) * K + chunk * 8) * 2);
   const unsigned offB = (unsigned)(((lane >> 3) * K + chunk * 8) * 2);
   const int rowB0 = n0 + 64 * wave;                  // first W row of this wave's instructions
   // k-tile t of the trailing (unconsumed) DMAs is clamped to the last one:
   // soffset is outside the range check, so t >= nt would read past the end of
   // the last row of X / W
   const int nt = K / BK;                             // >= 2, even (launcher)
-  auto dma1 = [&](int t, int slot, int i) {          // i < 8: A instruction i, else B i-8
-    const bool b = i >= 8;
-    const int q = i & 7;
+  auto dma1 = [&](int t, int slot, int i) {          // i < QA: A instruction i, else B i-QA
+    const bool b = i >= QA;
+    const int q = b ? i - QA : i;
     const int kb = min(t, nt - 1) * BK * 2;
     auto* dst = (__attribute__((address_space(3))) void*)(
-        smem + slot * SLOT_B + (b ? PIECE_B : 0) + (8 * wave + q) * 1024);
+        smem + slot * SLOT_B + (b ? PIECE_A + (8 * wave + q) * 1024 : (QA * wave + q) * 1024));
     if (b)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, offB, (rowB0 + 8 * q) * K * 2 + kb, 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA[q], kb, 0, 0);
   };
 
-  // ---- fragment reads: wave (wm, wn) owns rows wm*128.., cols wn*128..;
+  // ---- fragment reads: wave (wm, wn) owns rows wm*WROWS.., cols wn*128..;
   //      lane (fr, fq) reads row fr of fragment i, k-chunk 4 kh + fq.  Fragment
   //      i sits i * 2 KiB after fragment 0 with the same swizzle (row & 7 = fr & 7).
   const int wm = wave >> 1, wn = wave & 1;
@@ -128,61 +151,66 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       const int ch = ((4 * kh + fq) ^ (fr & 7)) * 16;
-      rbase[sl][kh][0] = sl * SLOT_B + (wm * 128 + fr) * ROWB + ch;
-      rbase[sl][kh][1] = sl * SLOT_B + PIECE_B + (wn * 128 + fr) * ROWB + ch;
+      rbase[sl][kh][0] = sl * SLOT_B + (wm * WROWS + fr) * ROWB + ch;
+      rbase[sl][kh][1] = sl * SLOT_B + PIECE_A + (wn * 128 + fr) * ROWB + ch;
     }
-  auto fread1 = [&](int slot, int kh, Frags& f, int i) {   // i < 8: B[i], else A[i-8]
+  auto fread1 = [&](int slot, int kh, Frags<MTW>& f, int i) {   // i < 8: B[i], else A[i-8]
     if (i < 8)
       f.b[i] = *reinterpret_cast<const bf16x8*>(smem + rbase[slot][kh][1] + i * 2048);
     else
       f.a[i - 8] = *reinterpret_cast<const bf16x8*>(smem + rbase[slot][kh][0] + (i - 8) * 2048);
   };
 
-  f32x4 acc[8][8];
+  f32x4 acc[MTW][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MTW; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // accumulator zeroing (VALU v_accvgpr_write) -> first MFMA reading them as
   // srcC needs wait states: pin the writes before a nop (asm statements keep
   // their order; the empty "+a" statements depend on the writes)
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MTW; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
 
-  Frags F[2];
+  Frags<MTW> F[2];
   // prologue: tiles 0 and 1 in flight, tile 0 landed, F[0] <- (0, k0)
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma1(0, 0, i);
+  for (int i = 0; i < NDMA; ++i) dma1(0, 0, i);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dma1(1, 1, i);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  for (int i = 0; i < NDMA; ++i) dma1(1, 1, i);
+  if constexpr (NDMA == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   raw_barrier();
 #pragma unroll
-  for (int i = 0; i < 16; ++i) fread1(0, 0, F[0], i);
+  for (int i = 0; i < NRD; ++i) fread1(0, 0, F[0], i);
   __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): clean waitcnt state at the loop head
   asm volatile("s_nop 4" ::: "memory");
 
   auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
-  auto keep = [](const Frags& f) {                   // fragments stay allocated to here: hipcc
+  auto keep = [](const Frags<MTW>& f) {              // fragments stay allocated to here: hipcc
 #pragma unroll                                       // does not know the asm MFMAs read them
-    for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(f.a[i]), "v"(f.b[i]));
+    for (int i = 0; i < MTW; ++i) asm volatile("" :: "v"(f.a[i]));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm volatile("" :: "v"(f.b[i]));
   };
   // one 64-deep k-tile; C = t & 1 static (the loop is unrolled by two).  Every
   // tile runs the full body, also the last two: their DMAs (clamped to the last
   // k-tile) and their reads of tile nt are never consumed (a peeled tail would be separate
   // code where hipcc re-assigns the accumulators with v_accvgpr_mov's, VALU
-  // writes the unpadded asm MFMAs next to them race with).
+  // writes the unpadded asm MFMAs next to them race with).  The reads and
+  // DMAs are spread evenly over the MFMA pairs of each half.
   auto tile = [&](int t, auto c_c) {
     constexpr int C = decltype(c_c)::value;
     fence();
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {                   // half 0: F[0], reads of (t, k1)
+    for (int j = 0; j < NP; ++j) {                   // half 0: F[0], reads of (t, k1)
       const int i0 = 2 * j, i1 = 2 * j + 1;
       mfma_a(acc[i0 >> 3][i0 & 7], F[0].b[i0 & 7], F[0].a[i0 >> 3]);
       mfma_a(acc[i1 >> 3][i1 & 7], F[0].b[i1 & 7], F[0].a[i1 >> 3]);
-      if ((j & 1) == 0) fread1(C, 1, F[1], j >> 1);
+#pragma unroll
+      for (int r = 0; r < ops_at(j, NRD, NP); ++r) fread1(C, 1, F[1], op0_at(j, NRD, NP) + r);
       fence();
     }
     keep(F[0]);
@@ -191,12 +219,14 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     raw_barrier();
     fence();
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {                   // half 1: F[1], reads of (t+1, k0), DMA t+2
+    for (int j = 0; j < NP; ++j) {                   // half 1: F[1], reads of (t+1, k0), DMA t+2
       const int i0 = 2 * j, i1 = 2 * j + 1;
       mfma_a(acc[i0 >> 3][i0 & 7], F[1].b[i0 & 7], F[1].a[i0 >> 3]);
       mfma_a(acc[i1 >> 3][i1 & 7], F[1].b[i1 & 7], F[1].a[i1 >> 3]);
-      if ((j & 1) == 0) fread1(C ^ 1, 0, F[0], j >> 1);
-      else dma1(t + 2, C, j >> 1);
+#pragma unroll
+      for (int r = 0; r < ops_at(j, NRD, NP); ++r) fread1(C ^ 1, 0, F[0], op0_at(j, NRD, NP) + r);
+#pragma unroll
+      for (int d = 0; d < ops_at(j, NDMA, NP); ++d) dma1(t + 2, C, op0_at(j, NDMA, NP) + d);
       fence();
     }
     keep(F[1]);
@@ -213,8 +243,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
 
   // ---- epilogue: lane holds Y[m][n .. n+3] of each 16x16 tile
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
-    const int m = m0 + wm * 128 + mt * 16 + fr;
+  for (int mt = 0; mt < MTW; ++mt) {
+    const int m = m0 + wm * WROWS + mt * 16 + fr;
     if (m >= M) continue;
     if constexpr (EPI == 2) {
       const int F2 = N >> 1;
@@ -259,19 +289,63 @@ int gemm256d_ok(int M, int N, int K) {
   return 0;
 }
 
-int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                        int epi, hipStream_t s) {
+// Tile height by waves of tiles on the CUs (one workgroup per CU either way):
+// time ~ ceil(tiles / G) x tile time, and a 192-row tile takes 3/4 of a
+// 256-row one; MCP_GEMM_BM=256 / 192 forces it.
+static int g_cus = 0;
+double gemm256d_waves_bm(int M, int N, int K, int bm) {
+  if (!g_cus) {
+    int d = 0;
+    hipDeviceProp_t prop;
+    (void)hipGetDevice(&d);
+    g_cus = hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0
+                ? prop.multiProcessorCount : 256;
+  }
+  const double tiles = (double)((M + bm - 1) / bm) * ((N + BN - 1) / BN);
+  return ceil(tiles / g_cus) * bm / 256.0;           // in 256-row tile times
+}
+
+int gemm256d_height(int M, int N, int K) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("MCP_GEMM_BM");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 256 || forced == 192) return forced;
+  const int plan = gemm_plan_lookup(M, N, K);        // measured (gemm.hip)
+  if (plan == 1 || plan == 2) return plan == 2 ? 192 : 256;
+  // the 192 kernel runs ~4 % below the 256 one per FLOP: prefer 256 on ties
+  return gemm256d_waves_bm(M, N, K, 192) * 1.04 < gemm256d_waves_bm(M, N, K, 256) ? 192 : 256;
+}
+
+// bm: tile height 256 or 192 (0: pick by gemm256d_height)
+int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                           int K, int epi, int bm, hipStream_t s) {
   if (const int rc = gemm256d_ok(M, N, K)) return rc;
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  if (bm == 0) bm = gemm256d_height(M, N, K);
+  const int nm = (M + bm - 1) / bm, nn = (N + BN - 1) / BN;
   const dim3 grid(nm * nn);
   auto x = (const bf16*)X;
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
+  if (bm == 192) {
+    switch (epi) {
+      case 0: gemm_tn_256d<0, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 1: gemm_tn_256d<1, 192><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
+      case 2: gemm_tn_256d<2, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      default: return 2;
+    }
+  }
   switch (epi) {
-    case 0: gemm_tn_256d<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
-    case 1: gemm_tn_256d<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
-    case 2: gemm_tn_256d<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+    case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+    case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
+    case 2: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
     default: return 2;
   }
+}
+
+int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        int epi, hipStream_t s) {
+  return launch_gemm_tn_256d_bm(X, W, Y, R, M, N, K, epi, 0, s);
 }

@@ -16,6 +16,7 @@
 // The mainloop is gemm256d.hip's (see there for the pipeline, the LDS image
 // and the inline-asm rules); it is repeated here rather than shared so the
 // two kernels' register allocations cannot perturb each other.
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -359,7 +360,9 @@ int launch_gemm_tn_256sk(const void* X, const void* W, void* Y, const void* R, i
   SkState* st = sk_state(T);
   if (!st) return 3;
   if (mode == 2 && !(sk_cost(T, U, st->G) < 0.92 * ceil((double)T / st->G))) return 4;
-  const dim3 grid(st->G);
+  // never more workgroups than (tile, k-unit) iterations: an empty range
+  // would still be counted between a tile's first and last owner
+  const dim3 grid((unsigned)std::min<long long>(st->G, (long long)T * U));
   auto x = (const bf16*)X;
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;

@@ -33,6 +33,10 @@ void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, in
                         hipStream_t s);
 // algo: -1 auto, 0 = 128x128 two-barrier kernel, 1 = 256x256 multi-phase kernel, 2 = skinny (K2)
 int gemm_select(int M, int N, int K);
+int gemm_plan_lookup(int M, int N, int K);
+void gemm_plan_set(int N, int K, const int* codes, int n);
+void gemm_plan_clear();
+int gemm256d_ok(int M, int N, int K);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,

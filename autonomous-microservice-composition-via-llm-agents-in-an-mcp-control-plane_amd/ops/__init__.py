@@ -38,8 +38,30 @@ def lib():
         spec = importlib.util.spec_from_file_location("_kernels", cands[0], loader=loader)
         mod = importlib.util.module_from_spec(spec)
         loader.exec_module(mod)
+        _load_gemm_plan(mod)
         _LIB = mod
     return _LIB
+
+
+GEMM_PLAN_FILE = os.path.join(_HERE, "gemm_plan_gfx950.json")
+
+
+def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
+    """Install the measured GEMM tile plans (tools/tune_gemm_plan.py) into the
+    kernel library's selector.  MCP_GEMM_PLAN=<path> picks another file, "0"
+    disables (the analytic wave-quantisation model then decides alone).
+    Returns the number of (N, K) shapes installed."""
+    import json
+
+    path = path or os.environ.get("MCP_GEMM_PLAN", GEMM_PLAN_FILE)
+    if path == "0" or not os.path.exists(path) or not hasattr(mod, "gemm_plan_set"):
+        return 0
+    with open(path) as f:
+        plan = json.load(f)
+    mod.gemm_plan_clear()
+    for sh in plan["shapes"]:
+        mod.gemm_plan_set(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["codes"]])
+    return len(plan["shapes"])
 
 
 def library_path() -> Optional[str]:
@@ -53,6 +75,30 @@ def available() -> bool:
         return True
     except (KernelLibraryMissing, ImportError, OSError):
         return False
+
+
+# GEMM shape histogram for tile-selection tuning: MCP_GEMM_TRACE=<path> counts
+# eager (M, N, K, kind) calls and writes them as JSON lines at exit (calls made
+# while a HIP graph is being captured are counted under kind "+graph")
+_TRACE = None
+if os.environ.get("MCP_GEMM_TRACE"):
+    import atexit
+    import collections
+    import json
+
+    _TRACE = collections.Counter()
+
+    def _dump_trace(path=os.environ["MCP_GEMM_TRACE"]):
+        with open(path, "w") as f:
+            for (M, N, K, kind), c in sorted(_TRACE.items()):
+                f.write(json.dumps({"M": M, "N": N, "K": K, "kind": kind, "calls": c}) + "\n")
+
+    atexit.register(_dump_trace)
+
+
+def _trace(X, W, kind):
+    cap = torch.cuda.is_current_stream_capturing()
+    _TRACE[(X.numel() // X.shape[-1], W.shape[0], W.shape[1], kind + ("+graph" if cap else ""))] += 1
 
 
 # --------------------------------------------------------------------- ops
@@ -97,6 +143,8 @@ def embedding(ids, table, out=None):
 def gemm(X, W, R=None, out=None, algo: int = -1):
     """Y = X @ W^T (+ R).  X [M, K], W [N, K].  algo: -1 auto, 0 = 128^2, 1 = 256^2."""
     if X.is_cuda:
+        if _TRACE is not None:
+            _trace(X, W, "gemm" if R is None else "gemm+res")
         out = X.new_empty(*X.shape[:-1], W.shape[0]) if out is None else out
         lib().gemm(X, W, out, R, algo)
         return out
@@ -108,6 +156,8 @@ def gemm_silu(X, W, out=None):
     """SwiGLU projection: silu(X Wg^T) * (X Wu^T) with W = interleave_gate_up(Wg, Wu)
     ([2F, K], 16-row groups); the activation is fused into the MFMA GEMM epilogue."""
     if X.is_cuda:
+        if _TRACE is not None:
+            _trace(X, W, "swiglu")
         out = X.new_empty(*X.shape[:-1], W.shape[0] // 2) if out is None else out
         lib().gemm_silu(X, W, out)
         return out

@@ -336,7 +336,7 @@ def test_gemm_256d_agpr(M, N, K):
     X = torch.randn(M, K, device=DEV).bfloat16()
     W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    for v in (49, 50):                 # data-parallel, stream-K (last-arriver slab sums)
+    for v in (49, 50, 51):             # data-parallel, stream-K (last-arriver slab sums), 192-row tiles
         Y.zero_()
         L.gemm_variant(X, W, Y, v)
         assert rel_err(Y, ref.gemm(X, W)) < 1e-2, v

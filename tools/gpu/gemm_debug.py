@@ -7,7 +7,7 @@ for (M, N, K) in [(256, 256, 128), (256, 256, 256), (512, 512, 1024)]:
     X = torch.randn(M, K, device='cuda').bfloat16()
     W = torch.randn(N, K, device='cuda').bfloat16()
     ref = X.float() @ W.float().t()
-    for v in (45, 49):
+    for v in (49, 51):
         Y = torch.zeros(M, N, device='cuda', dtype=torch.bfloat16)
         L.gemm_variant(X, W, Y, v)
         torch.cuda.synchronize()

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/tune_gemm_plan.py gpurun_out/gemm_plan_gfx950.json 8192 > gpurun_out/tune.log 2>&1 && \
+cp gpurun_out/gemm_plan_gfx950.json autonomous-microservice-composition-via-llm-agents-in-an-mcp-control-plane_amd/ops/gemm_plan_gfx950.json && \
+MCP_GEMM_TRACE=gpurun_out/gemm_shapes.jsonl timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 300 python -u bench.py > gpurun_out/bench2.log 2>&1

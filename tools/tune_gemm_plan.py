@@ -1,0 +1,88 @@
+"""Measure the GEMM tile plan for the Llama weight shapes on this GPU and write
+it where ops.lib() loads it (ops/gemm_plan_gfx950.json).
+
+For every (N, K) weight shape and every 64-row M bucket (timed at the bucket's
+top row, which has the tile counts of the whole bucket) the three MFMA kernels
+are timed interleaved (3 rounds x 10 launches, min): code 0 = 128^2 kernel,
+1 = AGPR kernel with 256-row tiles, 2 = AGPR kernel with 192-row tiles.  The
+fastest wins unless it beats the runner-up with the smaller code by < 1 %
+(hysteresis keeps the plan stable against timing noise).
+
+    python tools/tune_gemm_plan.py [out.json] [m_max]
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import mcp_amd.ops as ops  # noqa: E402
+
+os.environ["MCP_GEMM_PLAN"] = "0"          # time the kernels, not an old plan
+L = ops.lib()
+L.gemm_plan_clear()
+out_path = sys.argv[1] if len(sys.argv) > 1 else ops.GEMM_PLAN_FILE
+m_max = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+# Llama-3-8B (TP=1): qkv, o, gate|up (SwiGLU, interleaved), down
+SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
+MSTEP = 64
+M_MIN = 256                                # below: skinny / 128 kernels (gemm_select)
+
+dev = "cuda"
+s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+
+def run(code, X, W, Y):
+    if code == 0:
+        L.gemm(X, W, Y, None, 0)
+    else:
+        L.gemm_variant(X, W, Y, 49 if code == 1 else 51)
+
+
+def time_ms(fn, reps=10):
+    fn()
+    s_ev.record()
+    for _ in range(reps):
+        fn()
+    e_ev.record()
+    torch.cuda.synchronize()
+    return s_ev.elapsed_time(e_ev) / reps
+
+
+result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
+          "mstep": MSTEP, "codes": "0=128x128, 1=AGPR 256-row tiles, 2=AGPR 192-row tiles",
+          "generated": time.strftime("%Y-%m-%d"), "shapes": []}
+t0 = time.time()
+for (N, K) in SHAPES:
+    Xf = torch.randn(m_max, K, device=dev).bfloat16()
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+    Yf = torch.empty(m_max, N, device=dev, dtype=torch.bfloat16)
+    codes, tf = [], []
+    for b in range(m_max // MSTEP):
+        M = (b + 1) * MSTEP
+        if M < M_MIN:
+            codes.append(-1)
+            tf.append(None)
+            continue
+        X, Y = Xf[:M], Yf[:M]
+        cands = [0, 1, 2] if K % 128 == 0 and N % 256 == 0 else [0]
+        best = {c: float("inf") for c in cands}
+        for _ in range(3):
+            for c in cands:
+                best[c] = min(best[c], time_ms(lambda c=c: run(c, X, W, Y)))
+        order = sorted(cands, key=lambda c: best[c])
+        win = order[0]
+        for c in order[1:]:                    # prefer the smaller code within 1 %
+            if c < win and best[c] <= best[win] * 1.01:
+                win = c
+        codes.append(win)
+        tf.append({str(c): round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
+    result["shapes"].append({"N": N, "K": K, "codes": codes, "tflops": tf})
+    print(json.dumps({"N": N, "K": K, "codes": codes, "s": round(time.time() - t0, 1)}), flush=True)
+    del Xf, W, Yf
+with open(out_path, "w") as f:
+    json.dump(result, f, indent=None, separators=(",", ":"))
+    f.write("\n")
+print(json.dumps({"written": out_path, "s": round(time.time() - t0, 1)}), flush=True)
