@@ -349,3 +349,31 @@ def test_gemm_256d_agpr(M, N, K):
     y = ops.gemm_silu(X, Wi)
     e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
     assert rel_err(y, e) < 2e-2
+
+
+@pytest.mark.parametrize("code", [0, 1, 2])
+def test_gemm_plan_codes(code):
+    """Every kernel a measured tile plan can name (0 = 128^2, 1 = AGPR 256-row,
+    2 = AGPR 192-row tiles) through the production entry points: plain, residual
+    in place, SwiGLU; M not a multiple of any tile height."""
+    torch.manual_seed(7)
+    L = ops.lib()
+    N, K = 1024, 512
+    try:
+        L.gemm_plan_set(N, K, [code] * 64)
+        for M in (300, 700):
+            assert L.gemm_select(M, N, K) == (0 if code == 0 else 1)
+            X = torch.randn(M, K, device=DEV).bfloat16()
+            W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+            assert rel_err(ops.gemm(X, W), ref.gemm(X, W)) < 1e-2
+            R = torch.randn(M, N, device=DEV).bfloat16()
+            R2 = R.clone()
+            ops.gemm(X, W, R=R2, out=R2)
+            assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+            g, u = W[: N // 2], W[N // 2:]
+            y = ops.gemm_silu(X, ref.interleave_gate_up(g, u).contiguous())
+            e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+            assert rel_err(y, e) < 2e-2
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)
