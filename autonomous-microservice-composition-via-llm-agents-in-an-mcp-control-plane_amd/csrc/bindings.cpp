@@ -332,6 +332,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_plan_lookup", &gemm_plan_lookup);
+  m.def("gemm_splitk_init", [](int64_t bytes) { return gemm_splitk_init((size_t)bytes); },
+        "allocate the split-K fp32 workspace (call outside graph capture)");
+  m.def("gemm128_splits", &gemm128_splits);
   m.def("gemm_silu", &gemm_silu);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);

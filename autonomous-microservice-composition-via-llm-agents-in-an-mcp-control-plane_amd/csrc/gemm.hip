@@ -27,7 +27,10 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_ELEMS = 128 * BK;          // one operand tile, bf16 elements (16 KiB)
 
-template <int EPI, typename OutT = bf16>     // EPI: 0 plain, 1 +residual, 2 SwiGLU
+// SPLIT: split-K partial - blockIdx.y = split s of gridDim.y, K range
+// [s K/S, (s+1) K/S), fp32 partial tile to Y + s M N (EPI 0, OutT float);
+// splitk_reduce sums the partials and applies the epilogue.
+template <int EPI, typename OutT = bf16, bool SPLIT = false>     // EPI: 0 plain, 1 +residual, 2 SwiGLU
 __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X,
                                                       const bf16* __restrict__ W,
                                                       OutT* __restrict__ Y,
@@ -48,6 +51,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
   const int tm = first_m + (wg % per_group) % gsz;
   const int tn = (wg % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
+  const int klen = SPLIT ? K / (int)gridDim.y : K;
+  const int kbeg = SPLIT ? (int)blockIdx.y * klen : 0;
+  if constexpr (SPLIT) Y += (size_t)blockIdx.y * M * N;
 
   // ---- staging addresses: wave w stages pieces 4w..4w+3 of each operand
   const int lrow = lane >> 3;                  // row inside the 8-row piece
@@ -59,8 +65,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
     const int row = (wave * 4 + i) * 8 + lrow;
     const int ra = min(m0 + row, M - 1);
     const int rb = min(n0 + row, N - 1);
-    srcA[i] = X + (size_t)ra * K + lchunk * 8;
-    srcB[i] = W + (size_t)rb * K + lchunk * 8;
+    srcA[i] = X + (size_t)ra * K + kbeg + lchunk * 8;
+    srcB[i] = W + (size_t)rb * K + kbeg + lchunk * 8;
   }
   auto stage = [&](int kt, int buf) {
     bf16* la = smem + (buf * 2 + 0) * TILE_ELEMS;
@@ -80,7 +86,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
+  const int nk = klen / BK;
   stage(0, 0);
   __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
@@ -147,6 +153,45 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
       }
     }
   }
+}
+
+// Sum of the S fp32 split-K partials [S][M][N] + the epilogue; one thread per
+// 4 outputs (EPI 2: gate column 32 j + i pairs with up column 32 j + 16 + i,
+// the interleaved SwiGLU layout, output f = 16 j + i).
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ ws, int S,
+                                                     bf16* __restrict__ Y,
+                                                     const bf16* __restrict__ R, int M, int N) {
+  const int NO = EPI == 2 ? N / 2 : N;               // output columns
+  const size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i4 >= (size_t)M * NO / 4) return;
+  const int m = (int)(i4 / (NO / 4));
+  const int c = (int)(i4 % (NO / 4)) * 4;            // first output column
+  const size_t MN = (size_t)M * N;
+  bf16x4 o;
+  if constexpr (EPI == 2) {
+    const int cg = 32 * (c / 16) + c % 16;           // gate column (up = +16)
+    const float* p = ws + (size_t)m * N + cg;
+    f32x4 g = *reinterpret_cast<const f32x4*>(p), u = *reinterpret_cast<const f32x4*>(p + 16);
+    for (int s = 1; s < S; ++s) {
+      g += *reinterpret_cast<const f32x4*>(p + s * MN);
+      u += *reinterpret_cast<const f32x4*>(p + s * MN + 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (bf16)(g[j] / (1.f + __expf(-g[j])) * u[j]);
+  } else {
+    const float* p = ws + (size_t)m * N + c;
+    f32x4 v = *reinterpret_cast<const f32x4*>(p);
+    for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(p + s * MN);
+    if (EPI == 1) {
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+  }
+  *reinterpret_cast<bf16x4*>(Y + (size_t)m * NO + c) = o;
 }
 
 }  // namespace
@@ -218,8 +263,77 @@ int gemm_select(int M, int N, int K) {
   return cost256 < cost128 ? 1 : 0;
 }
 
+// ---- split-K for the 128^2 kernel at small M: N = 4096 at M = 256 is 64
+// tiles for 256 CUs (two per CU fit), so one projection ran at a quarter of
+// the chip.  S splits of K (each >= 8 k-tiles) fill it; the fp32 partials go
+// to a workspace allocated once when the library loads (never inside a graph
+// capture), and a reduce kernel applies the epilogue.
+namespace {
+float* g_splitk_ws = nullptr;
+size_t g_splitk_ws_bytes = 0;
+}  // namespace
+
+int gemm_splitk_init(size_t bytes) {
+  if (g_splitk_ws_bytes >= bytes) return 0;
+  if (g_splitk_ws) (void)hipFree(g_splitk_ws);
+  g_splitk_ws = nullptr;
+  g_splitk_ws_bytes = 0;
+  if (hipMalloc(&g_splitk_ws, bytes) != hipSuccess) {
+    g_splitk_ws = nullptr;
+    return 1;
+  }
+  g_splitk_ws_bytes = bytes;
+  return 0;
+}
+
+// splits for the 128^2 path (1 = none): the fewest that give >= 2 workgroups
+// per CU, K / S a multiple of 64 with >= 8 k-tiles, partials within the
+// workspace.  MCP_GEMM_SPLITK128=0 disables.
+int gemm128_splits(int M, int N, int K) {
+  static int enabled = -1;
+  if (enabled < 0) {
+    const char* e = getenv("MCP_GEMM_SPLITK128");
+    enabled = e ? atoi(e) : 1;
+  }
+  if (!enabled || !g_splitk_ws) return 1;
+  const int G = gemm256_num_cus();
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (tiles > G) return 1;
+  const int nkt = K / BK;
+  for (int S = 2; S <= 16; ++S) {
+    if (nkt % S || nkt / S < 8) continue;
+    if ((size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) break;
+    if (tiles * S >= 2 * G || S == 16) return S;
+  }
+  // largest admissible S below the target
+  int best = 1;
+  for (int S = 2; S <= 16; ++S)
+    if (nkt % S == 0 && nkt / S >= 8 && (size_t)S * M * N * sizeof(float) <= g_splitk_ws_bytes)
+      best = S;
+  return best;
+}
+
+// EPI 0/1/2 through S split-K partials + the reduce; false if not split
+static bool launch_gemm_128_split(const void* X, const void* W, void* Y, const void* R, int M,
+                                  int N, int K, int epi, hipStream_t s) {
+  const int S = gemm128_splits(M, N, K);
+  if (S <= 1) return false;
+  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+  gemm_tn_128<0, float, true><<<dim3(nm * nn, S), 256, 0, s>>>(
+      (const bf16*)X, (const bf16*)W, g_splitk_ws, nullptr, M, N, K);
+  const size_t n4 = (size_t)M * (epi == 2 ? N / 2 : N) / 4;
+  const dim3 rg((unsigned)((n4 + 255) / 256));
+  switch (epi) {
+    case 0: splitk_reduce<0><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N); break;
+    case 1: splitk_reduce<1><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, (const bf16*)R, M, N); break;
+    default: splitk_reduce<2><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N); break;
+  }
+  return true;
+}
+
 static void launch_gemm_tn_128(const void* X, const void* W, void* Y, const void* R, int M, int N,
                                int K, hipStream_t s) {
+  if (launch_gemm_128_split(X, W, Y, R, M, N, K, R ? 1 : 0, s)) return;
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   const dim3 grid(nm * nn);
   if (R)
@@ -240,7 +354,11 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
 
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s) {
-  if (M <= SKINNY_MAX_M && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;
+  // M <= 128: split-K over the 128^2 kernel beats the weight-streaming skinny
+  // kernel wherever it applies (tools/bench_small_m.py: 1.5-4x at N, K >= 4096)
+  if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
+      launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0)
+    return;
   if (gemm_select(M, N, K) == 1)
     launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
   else
@@ -260,10 +378,12 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
                              hipStream_t s);
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (N % 64) return 1;
-  if (M <= SKINNY_MAX_M && launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0) return 0;
+  if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
+      launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0)
+    return 0;
   if (gemm_select(M, N, K) == 1) {
     launch_gemm_tn_256_silu(X, W, Y, M, N, K, s);
-  } else {
+  } else if (!launch_gemm_128_split(X, W, Y, nullptr, M, N, K, 2, s)) {
     const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
     gemm_tn_128<2><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
                                                  nullptr, M, N, K);

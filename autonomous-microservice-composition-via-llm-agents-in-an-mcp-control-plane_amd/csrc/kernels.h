@@ -34,6 +34,8 @@ void launch_gemm_tn_256(const void* X, const void* W, void* Y, const void* R, in
 // algo: -1 auto, 0 = 128x128 two-barrier kernel, 1 = 256x256 multi-phase kernel, 2 = skinny (K2)
 int gemm_select(int M, int N, int K);
 int gemm_plan_lookup(int M, int N, int K);
+int gemm_splitk_init(size_t bytes);
+int gemm128_splits(int M, int N, int K);
 void gemm_plan_set(int N, int K, const int* codes, int n);
 void gemm_plan_clear();
 int gemm256d_ok(int M, int N, int K);

@@ -39,6 +39,10 @@ def lib():
         mod = importlib.util.module_from_spec(spec)
         loader.exec_module(mod)
         _load_gemm_plan(mod)
+        if torch.cuda.is_available() and hasattr(mod, "gemm_splitk_init"):
+            # fp32 split-K partials of small-M projections (gemm.hip); allocated
+            # here, never inside a hipGraph capture
+            mod.gemm_splitk_init(int(os.environ.get("MCP_GEMM_SPLITK_MB", "64")) << 20)
         _LIB = mod
     return _LIB
 

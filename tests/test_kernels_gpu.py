@@ -377,3 +377,26 @@ def test_gemm_plan_codes(code):
     finally:
         L.gemm_plan_clear()
         ops._load_gemm_plan(L)
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 4096), (100, 1024, 14336), (256, 6144, 4096),
+                                   (300, 4096, 4096), (64, 2048, 1024)])
+def test_gemm_splitk128(M, N, K):
+    """Split-K over the 128^2 kernel (fp32 partials in the load-time workspace +
+    reduce with the epilogue): plain, residual in place, SwiGLU; small M."""
+    torch.manual_seed(8)
+    L = ops.lib()
+    S = L.gemm128_splits(M, N, K)
+    assert S > 1, (M, N, K)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    assert rel_err(ops.gemm(X, W), ref.gemm(X, W)) < 1e-2
+    assert rel_err(ops.gemm(X, W, algo=0), ref.gemm(X, W)) < 1e-2
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    R2 = R.clone()
+    ops.gemm(X, W, R=R2, out=R2)
+    assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+    g, u = W[: N // 2], W[N // 2:]
+    y = ops.gemm_silu(X, ref.interleave_gate_up(g, u).contiguous())
+    e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+    assert rel_err(y, e) < 2e-2
