@@ -288,7 +288,7 @@ int gemm_splitk_init(size_t bytes) {
 
 // splits for the 128^2 path (1 = none): the fewest that give >= 2 workgroups
 // per CU, K / S a multiple of 64 with >= 8 k-tiles, partials within the
-// workspace.  MCP_GEMM_SPLITK128=0 disables.
+// workspace.  MCP_GEMM_SPLITK128=0 disables, =S > 1 forces S where K allows.
 int gemm128_splits(int M, int N, int K) {
   static int enabled = -1;
   if (enabled < 0) {
@@ -298,6 +298,10 @@ int gemm128_splits(int M, int N, int K) {
   if (!enabled || !g_splitk_ws) return 1;
   const int G = gemm256_num_cus();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (enabled > 1) {                                 // MCP_GEMM_SPLITK128=S forces S (tuning)
+    const int S = enabled, nkt = K / BK;
+    return (nkt % S == 0 && (size_t)S * M * N * sizeof(float) <= g_splitk_ws_bytes) ? S : 1;
+  }
   if (tiles > G) return 1;
   const int nkt = K / BK;
   for (int S = 2; S <= 16; ++S) {

@@ -342,9 +342,10 @@ class LLMEngine:
         use_graph = (self.graphs is not None and not copies and T <= self.graphs.buckets[-1]
                      and self.temperature == self.graphs.temperature)
         cascade = pre_tokens > 0 and not use_graph
-        host, layout = pack_step(entries, BLOCK_SIZE, group, copies,
-                                 casc.blocks[:casc_keys // BLOCK_SIZE] if cascade else None,
-                                 pre_tokens if cascade else 0, allowed, ctr)
+        with span("sched.pack"):
+            host, layout = pack_step(entries, BLOCK_SIZE, group, copies,
+                                     casc.blocks[:casc_keys // BLOCK_SIZE] if cascade else None,
+                                     pre_tokens if cascade else 0, allowed, ctr)
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
         tok_dev = self.graphs.run(step_from_host(host, layout)) if use_graph else None
@@ -364,9 +365,10 @@ class LLMEngine:
     def _retire(self, L: _Launch):
         """Wait for a launch's sampled tokens and advance its sequences."""
         t1 = time.perf_counter()
-        if L.event is not None:
-            L.event.synchronize()
-        new_tokens = L.tokens.tolist() if L.tokens is not None else []
+        with span("retire.wait"):
+            if L.event is not None:
+                L.event.synchronize()
+            new_tokens = L.tokens.tolist() if L.tokens is not None else []
         t2 = time.perf_counter()
         self.stats["sample_s"] += t2 - t1
         batch_seqs, sample_seqs = L.batch_seqs, L.sample_seqs
@@ -392,7 +394,8 @@ class LLMEngine:
 
     def _launch(self, host, layout):
         """(packed step) -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
-        payload = self.stager.to_device(host)
+        with span("launch.h2d"):
+            payload = self.stager.to_device(host)
         if self.bcast is not None:
             self.bcast.send(payload, layout)
         dstep, csrc, cdst = views(payload, layout)
@@ -400,7 +403,8 @@ class LLMEngine:
             ops.copy_blocks(self.kv.data, csrc, cdst)
         if dstep.token_ids.numel() == 0:
             return None, dstep
-        return self.model.forward(dstep, self.kv), dstep
+        with span("launch.forward"):
+            return self.model.forward(dstep, self.kv), dstep
 
     def shutdown_workers(self):
         if self.bcast is not None:

@@ -81,7 +81,14 @@ class GrammarSpec:
         self.keys = [self._input_keys(s) for s in self.services]
         self._trie_cache: Dict[Tuple[str, ...], Trie] = {}
         self._enc_cache: Dict[str, List[int]] = {}      # forced spans repeat across requests
-        self.name_trie = self.trie(tuple(json.dumps(n) for n in self.names))
+        self._chain_cache: Dict[tuple, tuple] = {}       # (trie node, live mask) -> forced walk
+        self.jnames = tuple(json.dumps(n) for n in self.names)
+        self.name_trie = self.trie(self.jnames)
+        # input sources of key k: the payload key itself, then any earlier node.
+        # ONE trie per key over every candidate; the live mask selects the key
+        # plus the nodes chosen so far (a trie restricted by a mask is the trie
+        # of the live alternatives, so the allowed tokens are the same)
+        self._src_cache: Dict[str, tuple] = {}
 
     @staticmethod
     def _input_keys(s) -> List[str]:
@@ -97,6 +104,37 @@ class GrammarSpec:
             if len(self._enc_cache) < 65536:
                 self._enc_cache[text] = t
         return list(t)
+
+    def forced_chain(self, node: Trie, live: int):
+        """Tokens forced from ``node`` under the live-alternative mask: the walk
+        while exactly one live child remains, stopping at a leaf (a resolved
+        choice).  Memoised per (node, mask) - the same walks repeat across
+        requests, and the per-token Python walk was most of the engine's
+        per-step host update."""
+        key = (id(node), live)
+        r = self._chain_cache.get(key)
+        if r is None:
+            toks, n = [], node
+            while n.leaf < 0:
+                kids = [t for t, c in n.children.items() if c.mask & live]
+                if len(kids) != 1:
+                    break
+                toks.append(kids[0])
+                n = n.children[kids[0]]
+            r = (tuple(toks), n)
+            if len(self._chain_cache) < (1 << 18):
+                self._chain_cache[key] = r
+        return r
+
+    def sources(self, key: str):
+        """(source names, their JSON alternatives, trie) for input ``key``."""
+        r = self._src_cache.get(key)
+        if r is None:
+            srcs = (key,) + tuple(n for n in self.names if n != key)
+            alts = tuple(json.dumps(x) for x in srcs)
+            r = (srcs, alts, self.trie(alts), {x: i for i, x in enumerate(srcs)})
+            self._src_cache[key] = r
+        return r
 
     def trie(self, alts: Tuple[str, ...]) -> Trie:
         t = self._trie_cache.get(alts)
@@ -137,8 +175,7 @@ class DagDecoder:
         node_inputs: List[Dict[str, str]] = []
         while True:
             live = ((1 << len(sp.names)) - 1) & ~used_mask
-            alts = tuple(json.dumps(n) for n in sp.names)
-            idx = yield (None, (alts, sp.name_trie, live))
+            idx = yield (None, (sp.jnames, sp.name_trie, live))
             used_mask |= 1 << idx
             svc = sp.services[idx]
             text = ',"endpoint":' + json.dumps(svc["endpoint"]) + ',"inputs":{'
@@ -147,13 +184,16 @@ class DagDecoder:
             prev_names = [sp.names[j] for j in chosen]
             for ki, key in enumerate(sp.keys[idx]):
                 yield (("," if ki else "") + json.dumps(key) + ":", None)
-                srcs = [key] + [n for n in prev_names if n != key]
-                alts_s = tuple(json.dumps(x) for x in srcs)
-                if len(alts_s) == 1:
+                srcs, alts_s, trie_s, pos = sp.sources(key)
+                live_s = 1
+                for n in prev_names:
+                    if n != key:
+                        live_s |= 1 << pos[n]
+                if live_s == 1:
                     yield (alts_s[0], None)
                     inputs[key] = srcs[0]
                 else:
-                    si = yield (None, (alts_s, sp.trie(alts_s), (1 << len(alts_s)) - 1))
+                    si = yield (None, (alts_s, trie_s, live_s))
                     inputs[key] = srcs[si]
             if sp.allow_retries:
                 yield ('},"retries":', None)
@@ -231,10 +271,13 @@ class DagDecoder:
     def advance(self) -> List[int]:
         """Return forced tokens (jump-forward), resolving single-child trie steps."""
         while not self.done and self._choice is not None:
-            kids = self._live_children()
-            if len(kids) != 1:
+            toks, end = self.spec.forced_chain(self._node, self._choice[2])
+            if not toks:
                 break
-            self._take(kids[0])
+            self._pending_tokens += toks
+            self._node = end
+            if end.leaf >= 0:
+                self._resolve()
         out, self._pending_tokens = self._pending_tokens, []
         return out
 
@@ -250,11 +293,14 @@ class DagDecoder:
         self._pending_tokens.append(token)
         self._node = self._node.children[token]
         if self._node.leaf >= 0:
-            alts = self._choice[0]
-            idx = self._node.leaf
-            self.text_parts.append(alts[idx])
-            self._choice = None
-            self._step_gen(idx)
+            self._resolve()
+
+    def _resolve(self):
+        """The walk reached a leaf: the choice is made, run the program on."""
+        idx = self._node.leaf
+        self.text_parts.append(self._choice[0][idx])
+        self._choice = None
+        self._step_gen(idx)
 
     # -------------------------------------------------------------- result
     @property

@@ -91,6 +91,10 @@ class LocalPlanner(Planner):
 
     def prepare(self, intent: str, services: Optional[Sequence[dict]] = None):
         services = self.registry.list_services() if services is None else services
+        dec, ptoks = self._decoder_and_prefix(intent, services)
+        return dec, ptoks, self.tok.encode(self.suffix_text(intent))
+
+    def _decoder_and_prefix(self, intent: str, services: Sequence[dict]):
         cands = self.candidates(intent, services)
         key = tuple(s["name"] for s in cands) + (getattr(self.registry, "version", 0),)
         spec = self._spec_cache.get(key)
@@ -106,7 +110,11 @@ class LocalPlanner(Planner):
             if len(self._prefix_cache) > 256:
                 self._prefix_cache.clear()
             self._prefix_cache[key] = ptoks
-        return DagDecoder(spec), ptoks, self.tok.encode(f"\nUser intent: “{intent}”\n\nJSON DAG:")
+        return DagDecoder(spec), ptoks
+
+    @staticmethod
+    def suffix_text(intent: str) -> str:
+        return f"\nUser intent: “{intent}”\n\nJSON DAG:"
 
     # ------------------------------------------------------- batch (sync)
     def plan_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> List[dict]:
@@ -114,8 +122,16 @@ class LocalPlanner(Planner):
         with self._lock:
             services = self.registry.list_services()
             seqs = []
-            for it in intents:
-                dec, ptoks, stoks = self.prepare(it, services)
+            # one batched (multi-threaded) tokenizer call for the per-intent suffixes
+            batch_enc = getattr(self.tok, "encode_batch", None)
+            sufs = batch_enc([self.suffix_text(it) for it in intents]) if batch_enc else None
+            for i, it in enumerate(intents):
+                if sufs is not None and (self.retriever is None or
+                                         len(services) <= self.retrieval_threshold):
+                    dec, ptoks = self._decoder_and_prefix(it, services)
+                    stoks = sufs[i]
+                else:
+                    dec, ptoks, stoks = self.prepare(it, services)
                 seqs.append(self.engine.submit(dec, stoks, prefix_tokens=ptoks))
             if fresh_prefix:
                 self.engine.drop_prefixes()   # batch-local prefix: recomputed next batch
