@@ -200,20 +200,31 @@ class LlamaModel:
         L = cfg.layers
         h = ops.rmsnorm(x, self.w.layers[0].attn_norm, cfg.eps)
         q = torch.empty(T, self.hq, D, device=x.device, dtype=x.dtype)
+        rows = step.logit_rows
         for l in range(L):
             lw = self.w.layers[l]
             qkv = ops.gemm(h, lw.wqkv)
             kc, vc = kv.layer(l)
             ops.rope_kv(qkv, step.positions, step.slots, self.cos_sin, q, kc, vc, self.hq, self.hkv, D)
-            a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
+            if l + 1 == L:
+                # last layer: every token's K/V is in the cache now, but only the
+                # sampled rows' hidden states are read - the output projection
+                # and the MLP run on those rows alone (exact; ~1/32 of the
+                # O + MLP FLOPs of a step whose tokens are mostly prompt /
+                # jump-forward spans)
+                if rows.numel() == 0:
+                    return x.new_empty(0, cfg.hidden)
+                a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
+                ri = rows.long()
+                x = x.index_select(0, ri)
+                a = a.view(T, self.hq * D).index_select(0, ri)
+                T = ri.numel()
+            else:
+                a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
             x = self._residual_gemm(a.view(T, self.hq * D), lw.wo, x)
             h = ops.rmsnorm(x, lw.mlp_norm, cfg.eps)
             act = ops.gemm_silu(h, lw.w_gate_up)          # SwiGLU fused in the epilogue
             x = self._residual_gemm(act, lw.w_down, x)
             if l + 1 < L:
                 h = ops.rmsnorm(x, self.w.layers[l + 1].attn_norm, cfg.eps)
-        rows = step.logit_rows
-        if rows.numel() == 0:
-            return x.new_empty(0, cfg.hidden)
-        xl = x.index_select(0, rows.long())
-        return ops.rmsnorm(xl, self.w.final_norm, cfg.eps)
+        return ops.rmsnorm(x, self.w.final_norm, cfg.eps)
