@@ -45,6 +45,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _pin_cpus(local_rank: int, local_world: int):
+    """One rank per GPU: give each rank its own contiguous slice of the CPUs this
+    process may use, so the ranks' host paths (scheduler, grammar, kernel
+    launches) do not migrate onto each other's cores.  MCP_PIN_CPUS=0 disables."""
+    if os.environ.get("MCP_PIN_CPUS", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return
+    cpus = sorted(os.sched_getaffinity(0))
+    n = len(cpus) // max(1, local_world)
+    if n >= 2:
+        os.sched_setaffinity(0, cpus[local_rank * n:(local_rank + 1) * n])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -66,6 +78,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        _pin_cpus(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
