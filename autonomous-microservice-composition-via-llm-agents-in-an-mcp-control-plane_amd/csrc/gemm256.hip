@@ -408,6 +408,7 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 50: return launch_gemm_tn_256sk(X, W, Y, nullptr, M, N, K, 0, 1, s);   // its stream-K form
     case 51: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 192, s);   // 192-row tiles
     case 52: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);          // height by cost model
+    case 61: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 9, 256, s);   // direct (unstaged) epilogue
     default: return 1;
   }
 }

@@ -79,7 +79,9 @@ DEV void tile_coords(int t, int nm, int nn, int bm, int& m0, int& n0) {
 constexpr int ops_at(int j, int n, int P) { return ((j + 1) * n) / P - (j * n) / P; }
 constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 
-template <int EPI, int BMT>
+// EPS = 1: the epilogue goes through LDS (row-contiguous 16-B stores); EPS = 0:
+// every lane stores its 4-column pieces straight from the MFMA layout.
+template <int EPI, int BMT, int EPS = 1>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
@@ -241,7 +243,71 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // and pad MFMA results -> VALU reads (inline asm is not padded)
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
-  // ---- epilogue: lane holds Y[m][n .. n+3] of each 16x16 tile
+  if constexpr (EPS) {
+    // ---- staged epilogue.  The direct one below stores 8 B per lane in
+    //      32-B row pieces (the MFMA layout: lane = 4 columns of one row); at
+    //      one workgroup per CU nothing hides those stores and they cost
+    //      10-15 % of a K = 4096 projection (no-store probe, gemm_tuning.md).
+    //      Here each wave converts its tile to bf16 (bias / SwiGLU applied)
+    //      into its own LDS region - rows of OUTW columns, 16-B chunks
+    //      swizzled ^= row - and stores it back as 16 B per lane, 256 B per
+    //      row: four times fewer, fully coalesced stores.
+    constexpr int OUTW = EPI == 2 ? 64 : 128;        // output columns per wave
+    constexpr int RB = OUTW * 2;                     // staged row bytes
+    constexpr int NCH = RB / 16;                     // 16-B chunks per row
+    constexpr int RPS = 1024 / RB;                   // rows per 1 KiB wave access
+    static_assert(4 * WROWS * RB <= 2 * SLOT_B, "epilogue staging fits the operand slots");
+    __syncthreads();                                 // every wave is done with the slots
+    char* stg = smem + wave * (WROWS * RB);
+    auto put = [&](int row, int col, const bf16x4& v) {
+      const int byte = col * 2;
+      *reinterpret_cast<bf16x4*>(stg + row * RB + (((byte >> 4) ^ (row & (NCH - 1))) << 4) +
+                                 (byte & 15)) = v;
+    };
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int row = mt * 16 + fr;
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
+          put(row, p * 16 + fq * 4, o);
+        }
+      } else {
+#pragma unroll
+        for (int nt_ = 0; nt_ < 8; ++nt_) {
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[mt][nt_][j];
+          put(row, nt_ * 16 + fq * 4, o);
+        }
+      }
+    }
+    const int ldy = EPI == 2 ? N / 2 : N;
+    const int col0 = EPI == 2 ? (n0 + wn * 128) / 2 : n0 + wn * 128;
+    const int lr = lane / NCH, lc = lane % NCH;
+#pragma unroll 4
+    for (int i = 0; i < WROWS / RPS; ++i) {
+      const int row = i * RPS + lr;
+      const int m = m0 + wm * WROWS + row;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + row * RB + ((lc ^ (row & (NCH - 1))) << 4));
+      if (m < M) {
+        const size_t off = (size_t)m * ldy + col0 + lc * 8;
+        if constexpr (EPI == 1) {
+          const bf16x8 r = *reinterpret_cast<const bf16x8*>(R + off);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)r[j]);
+        }
+        *reinterpret_cast<bf16x8*>(Y + off) = v;
+      }
+    }
+    return;
+  }
+
+  // ---- direct epilogue: lane holds Y[m][n .. n+3] of each 16x16 tile
 #pragma unroll
   for (int mt = 0; mt < MTW; ++mt) {
     const int m = m0 + wm * WROWS + mt * 16 + fr;
@@ -338,6 +404,7 @@ int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R,
     }
   }
   switch (epi) {
+    case 9: gemm_tn_256d<0, 256, 0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;   // direct epilogue (A/B)
     case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
     case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
     case 2: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
