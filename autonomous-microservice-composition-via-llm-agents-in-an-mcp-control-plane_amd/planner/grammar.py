@@ -82,6 +82,7 @@ class GrammarSpec:
         self._trie_cache: Dict[Tuple[str, ...], Trie] = {}
         self._enc_cache: Dict[str, List[int]] = {}      # forced spans repeat across requests
         self._chain_cache: Dict[tuple, tuple] = {}       # (trie node, live mask) -> forced walk
+        self._kids_cache: Dict[tuple, List[int]] = {}    # (trie node, live mask) -> allowed tokens
         self.jnames = tuple(json.dumps(n) for n in self.names)
         self.name_trie = self.trie(self.jnames)
         # input sources of key k: the payload key itself, then any earlier node.
@@ -104,6 +105,16 @@ class GrammarSpec:
             if len(self._enc_cache) < 65536:
                 self._enc_cache[text] = t
         return list(t)
+
+    def live_children(self, node: Trie, live: int) -> List[int]:
+        """Allowed next tokens at ``node`` under the live mask (memoised)."""
+        key = (id(node), live)
+        r = self._kids_cache.get(key)
+        if r is None:
+            r = [t for t, c in node.children.items() if c.mask & live]
+            if len(self._kids_cache) < (1 << 18):
+                self._kids_cache[key] = r
+        return r
 
     def forced_chain(self, node: Trie, live: int):
         """Tokens forced from ``node`` under the live-alternative mask: the walk
@@ -265,8 +276,7 @@ class DagDecoder:
 
     # ------------------------------------------------------------ protocol
     def _live_children(self):
-        alts, trie, live = self._choice
-        return [t for t, c in self._node.children.items() if c.mask & live]
+        return self.spec.live_children(self._node, self._choice[2])
 
     def advance(self) -> List[int]:
         """Return forced tokens (jump-forward), resolving single-child trie steps."""
