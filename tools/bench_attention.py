@@ -17,7 +17,11 @@ from mcp_amd.engine.batch import StepInputs, pack  # noqa: E402
 dev = "cuda"
 Hq, Hkv, D = 32, 8, 128
 # argv[1]: new tokens per request (16: 4-wave items; <= 8: 1-wave decode items)
-S, ql, prefix = 256, (int(sys.argv[1]) if len(sys.argv) > 1 else 16), 704
+# "a:b" alternates requests of a and b new tokens (mixed decode / jump-forward steps)
+qls = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "16").split(":")]
+S, prefix = 256, 704
+ql_s = np.array([qls[s % len(qls)] for s in range(S)], np.int32)
+ql = int(ql_s.max())
 own = 200
 nb_pre = prefix // 64
 rng = np.random.default_rng(0)
@@ -25,7 +29,7 @@ blocks_per_seq = (prefix + own + ql + 63) // 64
 nb = nb_pre + S * (blocks_per_seq - nb_pre) + 8
 kc = torch.randn(nb, Hkv, 64, D, device=dev).bfloat16()
 vc = torch.randn(nb, Hkv, 64, D, device=dev).bfloat16()
-T = S * ql
+T = int(ql_s.sum())
 q = torch.randn(T, Hq, D, device=dev).bfloat16()
 bt = np.zeros((S, blocks_per_seq), np.int32)
 nxt = nb_pre
@@ -34,10 +38,10 @@ for s in range(S):
     for j in range(nb_pre, blocks_per_seq):
         bt[s, j] = nxt
         nxt += 1
-ctx = np.full(S, prefix + own + ql, np.int32)
-qs = (np.arange(S) * ql).astype(np.int32)
+ctx = (prefix + own + ql_s).astype(np.int32)
+qs = np.concatenate([[0], np.cumsum(ql_s)[:-1]]).astype(np.int32)
 step = StepInputs(token_ids=np.zeros(T, np.int32), positions=np.zeros(T, np.int32),
-                  slots=np.full(T, -1, np.int32), q_start=qs, q_len=np.full(S, ql, np.int32),
+                  slots=np.full(T, -1, np.int32), q_start=qs, q_len=ql_s,
                   ctx_len=ctx, block_table=bt, logit_rows=np.zeros(0, np.int32),
                   kv_begin=np.full(S, prefix, np.int32), pre_bt=np.arange(nb_pre, dtype=np.int32),
                   pre_tokens=T)
@@ -60,6 +64,10 @@ def t_own():
                           pre_o=pre_o, pre_lse=pre_lse)
 
 
+def t_full():          # the production entry point (prefix pass + work lists)
+    ops.paged_attention(q, kc, vc, d.attn, scale, out=out)
+
+
 def timeit(fn, n=20):
     fn()
     torch.cuda.synchronize()
@@ -72,7 +80,7 @@ def timeit(fn, n=20):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-tp, to = timeit(t_prefix), timeit(t_own)
+tp, to, tf = timeit(t_prefix), timeit(t_own), timeit(t_full)
 fl_pre = 4.0 * T * Hq * prefix * D
 fl_own = 4.0 * T * Hq * (own + ql / 2) * D
 # correctness of the cascade against the plain per-request pass over all keys
@@ -83,6 +91,6 @@ for nw, ws, wq in d.attn.work_lists():
 t_prefix()
 t_own()
 err = ((out.float() - ref.float()).norm() / ref.norm()).item()
-print(json.dumps({"ql": ql, "prefix_us": round(tp, 1), "prefix_tflops": round(fl_pre / tp / 1e6, 1),
+print(json.dumps({"ql": sys.argv[1] if len(sys.argv) > 1 else "16", "full_us": round(tf, 1), "prefix_us": round(tp, 1), "prefix_tflops": round(fl_pre / tp / 1e6, 1),
                   "own_us": round(to, 1), "own_tflops": round(fl_own / to / 1e6, 1),
                   "cascade_vs_plain_rel_err": err}))
