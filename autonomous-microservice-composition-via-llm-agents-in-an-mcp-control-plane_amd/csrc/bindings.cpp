@@ -69,6 +69,33 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slo
                  k_cache.size(2), stream());
 }
 
+// QKV projection + RoPE + paged K/V write: fused in the GEMM epilogue when the
+// AGPR kernel serves the shape, else GEMM into ``qkv`` (scratch) + rope_kv
+void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const at::Tensor& pos,
+              const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& q_out,
+              at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(qkv);
+  CHECK_I32_TENSOR(pos); CHECK_I32_TENSOR(slots);
+  CHECK_BF16_TENSOR(q_out); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache);
+  CHECK_DEV(cos_sin); CHECK_CONTIG(cos_sin);
+  const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.dim() == 2 && W.size(1) == K, "W must be [N, K]");
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * D, "W rows must be (Hq + 2 Hkv) * D");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 3 &&
+              cos_sin.size(1) == D / 2 && cos_sin.size(2) == 2, "cos_sin [P, D/2, 2] f32");
+  TORCH_CHECK(pos.numel() == M && slots.numel() == M, "pos / slots: one per row of X");
+  TORCH_CHECK(qkv.numel() == (int64_t)M * N, "qkv scratch [M, N]");
+  TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * D, "q_out shape");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D &&
+              v_cache.sizes() == k_cache.sizes(), "cache [nb, Hkv, BS, D]");
+  TORCH_CHECK(D == 128 || D == 64, "head_dim must be 64 or 128");
+  TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "qkv_rope: unsupported GEMM shape");
+  RopeArgs ra{pos.data_ptr<int>(), slots.data_ptr<int>(), cos_sin.data_ptr<float>(),
+              q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv,
+              (int)k_cache.size(2)};
+  launch_qkv_rope(X.data_ptr(), W.data_ptr(), qkv.data_ptr(), M, N, K, (int)D, ra, stream());
+}
+
 void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::optional<at::Tensor>& R,
           int64_t algo) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
@@ -328,6 +355,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none(),
         py::arg("algo") = -1);
   m.def("gemm_select", &gemm_select);
+  m.def("qkv_rope", &qkv_rope);
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
   m.def("gemm_plan_clear", &gemm_plan_clear);

@@ -86,8 +86,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
-                                                       int K) {
+                                                       int K, const RopeArgs ra) {
   static_assert(BMT == 256 || BMT == 192, "tile height");
+  static_assert(EPI != 3 || EPS, "the RoPE epilogue is staged");
   constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (8 or 6)
   constexpr int WROWS = BMT / 2;                    // rows per wave (128 or 96)
   constexpr int PIECE_A = BMT * ROWB;               // the X operand of a slot
@@ -264,9 +265,44 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
       *reinterpret_cast<bf16x4*>(stg + row * RB + (((byte >> 4) ^ (row & (NCH - 1))) << 4) +
                                  (byte & 15)) = v;
     };
+    // EPI 3: this wave's 128 columns are one head (n0 % 256 == 0)
+    const int head = (n0 + wn * 128) >> 7;
+    const bool rotate = EPI == 3 && head < ra.Hq + ra.Hkv;
+    int rpos[MTW];                                   // EPI 3: positions, loaded up front
+    if (EPI == 3 && rotate) {
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) rpos[mt] = ra.pos[min(m0 + wm * WROWS + mt * 16 + fr, M - 1)];
+    }
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt) {
       const int row = mt * 16 + fr;
+      if (EPI == 3 && rotate) {
+        // rotate-half RoPE on the fp32 accumulators: d and d + 64 of the
+        // head are acc[mt][nt] and acc[mt][nt + 4] of this lane; (cos, sin)
+        // of d = 16 nt + 4 fq + j .. +3 are 32 contiguous bytes: two 16-B loads
+        const f32x4* cs = reinterpret_cast<const f32x4*>(ra.cos_sin) + (size_t)rpos[mt] * 32;
+        f32x4 c4[4][2];
+#pragma unroll
+        for (int nt_ = 0; nt_ < 4; ++nt_) {
+          c4[nt_][0] = cs[nt_ * 8 + fq * 2];
+          c4[nt_][1] = cs[nt_ * 8 + fq * 2 + 1];
+        }
+#pragma unroll
+        for (int nt_ = 0; nt_ < 4; ++nt_) {
+          bf16x4 o1, o2;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 cc = c4[nt_][j >> 1];
+            const float rc = cc[(j & 1) * 2], rs = cc[(j & 1) * 2 + 1];
+            const float x1 = acc[mt][nt_][j], x2 = acc[mt][nt_ + 4][j];
+            o1[j] = (bf16)(x1 * rc - x2 * rs);
+            o2[j] = (bf16)(x2 * rc + x1 * rs);
+          }
+          put(row, nt_ * 16 + fq * 4, o1);
+          put(row, (nt_ + 4) * 16 + fq * 4, o2);
+        }
+        continue;
+      }
       if constexpr (EPI == 2) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
@@ -289,11 +325,34 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     const int ldy = EPI == 2 ? N / 2 : N;
     const int col0 = EPI == 2 ? (n0 + wn * 128) / 2 : n0 + wn * 128;
     const int lr = lane / NCH, lc = lane % NCH;
-#pragma unroll 4
+    // EPI 3, K / V heads: this lane's rows' cache slots, loaded up front (a
+    // load per row inside the loop would serialise on its latency)
+    int rslot[EPI == 3 ? WROWS / RPS : 1];
+    if (EPI == 3 && head >= ra.Hq) {
+#pragma unroll
+      for (int i = 0; i < WROWS / RPS; ++i)
+        rslot[i] = ra.slots[min(m0 + wm * WROWS + i * RPS + lr, M - 1)];
+    }
+#pragma unroll
     for (int i = 0; i < WROWS / RPS; ++i) {
       const int row = i * RPS + lr;
       const int m = m0 + wm * WROWS + row;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + row * RB + ((lc ^ (row & (NCH - 1))) << 4));
+      if (EPI == 3 && m < M) {                       // q rows / paged K and V rows
+        bf16* dst;
+        if (head < ra.Hq) {
+          dst = reinterpret_cast<bf16*>(ra.q_out) + ((size_t)m * ra.Hq + head) * 128;
+        } else {
+          const int slot = rslot[EPI == 3 ? i : 0];
+          if (slot < 0) continue;
+          const bool isk = head < ra.Hq + ra.Hkv;
+          const int hk = head - ra.Hq - (isk ? 0 : ra.Hkv);
+          dst = reinterpret_cast<bf16*>(isk ? ra.k_cache : ra.v_cache) +
+                (((size_t)(slot / ra.BS) * ra.Hkv + hk) * ra.BS + slot % ra.BS) * 128;
+        }
+        *reinterpret_cast<bf16x8*>(dst + lc * 8) = v;
+        continue;
+      }
       if (m < M) {
         const size_t off = (size_t)m * ldy + col0 + lc * 8;
         if constexpr (EPI == 1) {
@@ -384,9 +443,9 @@ int gemm256d_height(int M, int N, int K) {
   return gemm256d_waves_bm(M, N, K, 192) * 1.04 < gemm256d_waves_bm(M, N, K, 256) ? 192 : 256;
 }
 
-// bm: tile height 256 or 192 (0: pick by gemm256d_height)
-int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
-                           int K, int epi, int bm, hipStream_t s) {
+// bm: tile height 256 or 192 (0: pick by gemm256d_height); ra: EPI 3 only
+static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                            int K, int epi, int bm, const RopeArgs& ra, hipStream_t s) {
   if (const int rc = gemm256d_ok(M, N, K)) return rc;
   if (bm == 0) bm = gemm256d_height(M, N, K);
   const int nm = (M + bm - 1) / bm, nn = (N + BN - 1) / BN;
@@ -397,19 +456,40 @@ int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R,
   auto r = (const bf16*)R;
   if (bm == 192) {
     switch (epi) {
-      case 0: gemm_tn_256d<0, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
-      case 1: gemm_tn_256d<1, 192><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
-      case 2: gemm_tn_256d<2, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+      case 0: gemm_tn_256d<0, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+      case 1: gemm_tn_256d<1, 192><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
+      case 2: gemm_tn_256d<2, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+      case 3: gemm_tn_256d<3, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
       default: return 2;
     }
   }
   switch (epi) {
-    case 9: gemm_tn_256d<0, 256, 0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;   // direct epilogue (A/B)
-    case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
-    case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K); return 0;
-    case 2: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K); return 0;
+    case 9: gemm_tn_256d<0, 256, 0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;   // direct epilogue (A/B)
+    case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+    case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
+    case 2: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+    case 3: gemm_tn_256d<3, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
     default: return 2;
   }
+}
+
+int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                           int K, int epi, int bm, hipStream_t s) {
+  return launch_256d_impl(X, W, Y, R, M, N, K, epi, bm, RopeArgs{}, s);
+}
+
+// QKV + RoPE + paged K/V write (EPI 3) on the AGPR kernel when the selector
+// picks it for this shape; otherwise the plain GEMM into qkv and rope_kv
+void launch_qkv_rope(const void* X, const void* W, void* qkv, int M, int N, int K, int D,
+                     const RopeArgs& ra, hipStream_t s) {
+  static const int fused = getenv("MCP_QKV_ROPE_FUSED") ? atoi(getenv("MCP_QKV_ROPE_FUSED")) : 1;
+  if (fused && D == 128 && N == (ra.Hq + 2 * ra.Hkv) * 128 && M > SKINNY_MAX_M &&
+      gemm_select(M, N, K) == 1 && gemm256d_ok(M, N, K) == 0 &&
+      launch_256d_impl(X, W, nullptr, nullptr, M, N, K, 3, 0, ra, s) == 0)
+    return;
+  launch_gemm_tn(X, W, qkv, nullptr, M, N, K, s);
+  launch_rope_kv(qkv, ra.pos, ra.slots, ra.cos_sin, ra.q_out, ra.k_cache, ra.v_cache, M, ra.Hq,
+                 ra.Hkv, D, ra.BS, s);
 }
 
 int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,

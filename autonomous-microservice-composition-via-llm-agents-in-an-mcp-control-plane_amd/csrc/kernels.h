@@ -16,6 +16,20 @@ void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const voi
                     void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
                     int BS, hipStream_t s);
 void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
+
+// QKV projection + RoPE + paged K/V write fused in the GEMM epilogue (K1+K4+K10)
+struct RopeArgs {
+  const int* pos;          // [T] positions
+  const int* slots;        // [T] KV-cache slots (-1: no write)
+  const float* cos_sin;    // [P, D/2, 2]
+  void* q_out;             // [T, Hq, D]
+  void* k_cache;           // [nb, Hkv, BS, D]
+  void* v_cache;
+  int Hq, Hkv, BS;
+};
+// fused when the AGPR GEMM serves the shape (D = 128), else GEMM into qkv + rope_kv
+void launch_qkv_rope(const void* X, const void* W, void* qkv, int M, int N, int K, int D,
+                     const RopeArgs& ra, hipStream_t s);
 void launch_copy_blocks(void* data, const int* src, const int* dst, int npairs, int layers2,
                         int nb, int block_elems, hipStream_t s);
 

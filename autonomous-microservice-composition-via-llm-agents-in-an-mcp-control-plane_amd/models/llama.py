@@ -203,9 +203,11 @@ class LlamaModel:
         rows = step.logit_rows
         for l in range(L):
             lw = self.w.layers[l]
-            qkv = ops.gemm(h, lw.wqkv)
             kc, vc = kv.layer(l)
-            ops.rope_kv(qkv, step.positions, step.slots, self.cos_sin, q, kc, vc, self.hq, self.hkv, D)
+            # q, K/V cache <- rope(h Wqkv^T): rotation + paged write fused in the
+            # GEMM epilogue on the AGPR path (ops.qkv_rope)
+            ops.qkv_rope(h, lw.wqkv, step.positions, step.slots, self.cos_sin, q, kc, vc,
+                         self.hq, self.hkv, D)
             if l + 1 == L:
                 # last layer: every token's K/V is in the cache now, but only the
                 # sampled rows' hidden states are read - the output projection

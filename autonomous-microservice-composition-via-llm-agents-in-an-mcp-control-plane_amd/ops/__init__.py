@@ -169,6 +169,20 @@ def gemm_silu(X, W, out=None):
     return r if out is None else out.copy_(r)
 
 
+def qkv_rope(h, wqkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, qkv=None):
+    """q_out, K/V cache <- rope(h wqkv^T).  On the GPU the rotation and the
+    paged K/V write run in the QKV GEMM's epilogue when the AGPR kernel serves
+    the shape (``qkv`` is then untouched scratch); otherwise GEMM + rope_kv."""
+    if h.is_cuda:
+        T = h.numel() // h.shape[-1]
+        qkv = h.new_empty(T, wqkv.shape[0]) if qkv is None else qkv
+        lib().qkv_rope(h, wqkv, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
+        return q_out
+    qkv = ref.gemm(h, wqkv)
+    ref.rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
+    return q_out
+
+
 def rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D):
     if qkv.is_cuda:
         lib().rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)

@@ -400,3 +400,33 @@ def test_gemm_splitk128(M, N, K):
     y = ops.gemm_silu(X, ref.interleave_gate_up(g, u).contiguous())
     e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
     assert rel_err(y, e) < 2e-2
+
+
+@pytest.mark.parametrize("M", [1500, 3000, 200])
+def test_qkv_rope_fused(M):
+    """QKV GEMM with RoPE + paged K/V write in its epilogue (AGPR path; M = 200
+    takes the GEMM + rope_kv fallback) against fp32 GEMM + reference rope_kv,
+    including rows without a cache slot (-1)."""
+    torch.manual_seed(9)
+    Hq, Hkv, D, H, BS = 32, 8, 128, 4096, 64
+    L = ops.lib()
+    X = torch.randn(M, H, device=DEV).bfloat16()
+    W = (torch.randn((Hq + 2 * Hkv) * D, H, device=DEV) / math.sqrt(H)).bfloat16()
+    nb = (M + BS - 1) // BS + 2
+    pos = torch.randint(0, 8000, (M,), device=DEV, dtype=torch.int32)
+    perm = torch.randperm(nb * BS, device=DEV)[:M].to(torch.int32)
+    slots = torch.where(torch.rand(M, device=DEV) < 0.1, torch.full_like(perm, -1), perm)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, DEV)
+    q = torch.zeros(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+    kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    ops.qkv_rope(X, W, pos, slots, cs, q, kc, vc, Hq, Hkv, D)
+    qkv = ref.gemm(X, W).cpu()
+    qr_c, kr_c, vr_c = torch.zeros_like(q.cpu()), torch.zeros_like(kc.cpu()), torch.zeros_like(vc.cpu())
+    ref.rope_kv(qkv, pos.cpu(), slots.cpu(), cs.cpu(), qr_c, kr_c, vr_c, Hq, Hkv, D)
+    assert rel_err(q.cpu(), qr_c) < 1e-2
+    assert rel_err(kc.cpu(), kr_c) < 1e-2 and rel_err(vc.cpu(), vr_c) < 1e-2
+    # untouched slots stay zero (rows with slot -1 wrote nothing)
+    used = torch.zeros(nb * BS, dtype=torch.bool)
+    used[slots.cpu()[slots.cpu() >= 0].long()] = True
+    assert kc.cpu().permute(0, 2, 1, 3).reshape(nb * BS, -1)[~used].abs().sum() == 0
