@@ -273,7 +273,12 @@ float* g_splitk_ws = nullptr;
 size_t g_splitk_ws_bytes = 0;
 }  // namespace
 
+int gemm256sk_prealloc();
+
 int gemm_splitk_init(size_t bytes) {
+  // the stream-K tail's slabs / counters too (gemm256sk.hip): both are
+  // allocated here, at library load, never inside a hipGraph capture
+  if (gemm256sk_prealloc() != 0) return 2;
   if (g_splitk_ws_bytes >= bytes) return 0;
   if (g_splitk_ws) (void)hipFree(g_splitk_ws);
   g_splitk_ws = nullptr;

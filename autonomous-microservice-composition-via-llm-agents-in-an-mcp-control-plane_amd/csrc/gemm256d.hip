@@ -104,7 +104,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nm = (M + BMT - 1) / BMT, nn = (N + BN - 1) / BN;
   int m0, n0;
-  tile_coords(xcd_remap(blockIdx.x, nm * nn), nm, nn, BMT, m0, n0);
+  // grid = the first gridDim.x tiles of the grouped order (all of them, or the
+  // full waves of a hybrid launch whose tail runs stream-K, gemm256sk.hip)
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), nm, nn, BMT, m0, n0);
 
   // ---- LDS-DMA: instruction q of an operand fills rows 8q..8q+7,
   //      lane-linearly (row 8q + lane/8, LDS chunk lane%8, swizzled source
@@ -444,12 +446,42 @@ int gemm256d_height(int M, int N, int K) {
 }
 
 // bm: tile height 256 or 192 (0: pick by gemm256d_height); ra: EPI 3 only
+int launch_gemm_tn_256sk_tail(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                              int K, int epi, int tile0, hipStream_t s);
+
+// hybrid data-parallel + stream-K tail: the full waves here, a tail wave at
+// most half full spread over every CU (MCP_GEMM_HYBRID=0 disables)
+static int hybrid_tile0(int M, int N, int bm, int epi) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("MCP_GEMM_HYBRID");
+    on = e ? atoi(e) : 1;
+  }
+  if (!on || bm != 256 || epi < 0 || epi > 2) return 0;
+  if (!g_cus) gemm256d_waves_bm(M, N, 128, 256);     // initialises g_cus
+  const int T = ((M + 255) / 256) * ((N + BN - 1) / BN);
+  const int full = (T / g_cus) * g_cus, tail = T - full;
+  return (full > 0 && tail > 0 && 2 * tail <= g_cus) ? full : 0;
+}
+
 static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R, int M, int N,
                             int K, int epi, int bm, const RopeArgs& ra, hipStream_t s) {
   if (const int rc = gemm256d_ok(M, N, K)) return rc;
   if (bm == 0) bm = gemm256d_height(M, N, K);
   const int nm = (M + bm - 1) / bm, nn = (N + BN - 1) / BN;
-  const dim3 grid(nm * nn);
+  const int tile0 = hybrid_tile0(M, N, bm, epi);
+  const dim3 grid(tile0 > 0 ? tile0 : nm * nn);
+  if (tile0 > 0) {
+    // full waves first (same stream: the tail starts when they are done)
+    int rc = 0;
+    switch (epi) {
+      case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N, K, ra); break;
+      case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, ra); break;
+      default: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N, K, ra); break;
+    }
+    rc = launch_gemm_tn_256sk_tail(X, W, Y, R, M, N, K, epi, tile0, s);
+    return rc;
+  }
   auto x = (const bf16*)X;
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;

@@ -100,13 +100,15 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256sk(const bf16* __restrict__
                                                         bf16* __restrict__ Y,
                                                         const bf16* __restrict__ R, int M, int N,
                                                         int K, f32x4* __restrict__ ws,
-                                                        int* __restrict__ cnt) {
+                                                        int* __restrict__ cnt, int tile0) {
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT_B];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const int T = nm * nn, U = K / (2 * BK);
+  // tiles [tile0, nm nn) in the data-parallel kernel's grouped order: the
+  // hybrid launch gives the full waves to gemm256d.hip and only the tail here
+  const int T = nm * nn - tile0, U = K / (2 * BK);
   const int G = gridDim.x;
   const int wg = xcd_remap(blockIdx.x, G);           // range neighbours share an XCD
   const long long I = (long long)T * U;
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256sk(const bf16* __restrict__
   while (it < it_end) {
     const int tile = it / U, u0 = it % U, u1 = min(U, u0 + (it_end - it));
     int m0, n0;
-    tile_coords(tile, nm, nn, m0, n0);
+    tile_coords(tile0 + tile, nm, nn, m0, n0);
     unsigned offA[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -368,9 +370,41 @@ int launch_gemm_tn_256sk(const void* X, const void* W, void* Y, const void* R, i
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
   switch (epi) {
-    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt); return 0;
-    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt); return 0;
-    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt); return 0;
+    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, 0); return 0;
+    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt, 0); return 0;
+    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, 0); return 0;
     default: return 5;
   }
 }
+
+// Hybrid tail: tiles [tile0, T) of the data-parallel order, stream-K over one
+// persistent wave (gemm256d.hip launches the full waves [0, tile0) first).
+// The tail wave of a data-parallel grid that is at most half full costs a
+// whole tile time; spread over every CU it costs tail / G of one plus the
+// slab hand-offs, while the full waves keep their L2 panel sharing.
+int launch_gemm_tn_256sk_tail(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                              int K, int epi, int tile0, hipStream_t s) {
+  if (gemm256d_ok(M, N, K) != 0) return 1;
+  const int T = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) - tile0, U = K / (2 * BK);
+  if (T <= 0 || tile0 < 0) return 2;
+  SkState* st = sk_state(T);
+  if (!st) return 3;
+  // at most MCP_GEMM_TAIL_SPLIT (4) workgroups per tail tile: the last arriver
+  // sums every slab of its tile, so wider splits lose to the fix-up
+  static const int smax = getenv("MCP_GEMM_TAIL_SPLIT") ? atoi(getenv("MCP_GEMM_TAIL_SPLIT")) : 4;
+  const dim3 grid((unsigned)std::min<long long>(std::min<long long>(st->G, (long long)T * smax),
+                                                (long long)T * U));
+  auto x = (const bf16*)X;
+  auto w = (const bf16*)W;
+  auto y = (bf16*)Y;
+  auto r = (const bf16*)R;
+  switch (epi) {
+    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, tile0); return 0;
+    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt, tile0); return 0;
+    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, tile0); return 0;
+    default: return 5;
+  }
+}
+
+// workspace / counters allocated before any graph capture (library load)
+int gemm256sk_prealloc() { return sk_state(4096) ? 0 : 1; }

@@ -430,3 +430,25 @@ def test_qkv_rope_fused(M):
     used = torch.zeros(nb * BS, dtype=torch.bool)
     used[slots.cpu()[slots.cpu() >= 0].long()] = True
     assert kc.cpu().permute(0, 2, 1, 3).reshape(nb * BS, -1)[~used].abs().sum() == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(4352, 4096, 4096), (3000, 28672, 4096), (2304, 6144, 4096)])
+def test_gemm_hybrid_streamk_tail(M, N, K):
+    """Hybrid launch (gemm256d.hip full waves + gemm256sk.hip stream-K tail when
+    the last wave of 256-row tiles is at most half full): plain, residual in
+    place and SwiGLU against fp32."""
+    torch.manual_seed(10)
+    L = ops.lib()
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    L.gemm_variant(X, W, Y, 49)                     # 256-row tiles: hybrid when the tail is short
+    assert rel_err(Y, ref.gemm(X, W)) < 1e-2
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    R2 = R.clone()
+    ops.gemm(X, W, R=R2, out=R2, algo=1)
+    assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+    g, u = W[: N // 2], W[N // 2:]
+    y = ops.gemm_silu(X, ref.interleave_gate_up(g, u).contiguous())
+    e = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+    assert rel_err(y, e) < 2e-2
