@@ -117,24 +117,31 @@ class LocalPlanner(Planner):
         return f"\nUser intent: “{intent}”\n\nJSON DAG:"
 
     # ------------------------------------------------------- batch (sync)
+    def submit_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> list:
+        """Queue a batch of intents on the engine without running it (the
+        caller drives ``engine.step()``; ``plan_many`` = this + run)."""
+        services = self.registry.list_services()
+        seqs = []
+        batch_enc = getattr(self.tok, "encode_batch", None)
+        sufs = batch_enc([self.suffix_text(it) for it in intents]) if batch_enc else None
+        for i, it in enumerate(intents):
+            if sufs is not None and (self.retriever is None or
+                                     len(services) <= self.retrieval_threshold):
+                dec, ptoks = self._decoder_and_prefix(it, services)
+                stoks = sufs[i]
+            else:
+                dec, ptoks, stoks = self.prepare(it, services)
+            seqs.append(self.engine.submit(dec, stoks, prefix_tokens=ptoks))
+        if fresh_prefix:
+            # batch-local prefix: this batch's requests hold their references,
+            # the next batch recomputes it
+            self.engine.drop_prefixes()
+        return seqs
+
     def plan_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> List[dict]:
         """Plan a batch of intents to completion on the calling thread."""
         with self._lock:
-            services = self.registry.list_services()
-            seqs = []
-            # one batched (multi-threaded) tokenizer call for the per-intent suffixes
-            batch_enc = getattr(self.tok, "encode_batch", None)
-            sufs = batch_enc([self.suffix_text(it) for it in intents]) if batch_enc else None
-            for i, it in enumerate(intents):
-                if sufs is not None and (self.retriever is None or
-                                         len(services) <= self.retrieval_threshold):
-                    dec, ptoks = self._decoder_and_prefix(it, services)
-                    stoks = sufs[i]
-                else:
-                    dec, ptoks, stoks = self.prepare(it, services)
-                seqs.append(self.engine.submit(dec, stoks, prefix_tokens=ptoks))
-            if fresh_prefix:
-                self.engine.drop_prefixes()   # batch-local prefix: recomputed next batch
+            seqs = self.submit_many(intents, fresh_prefix)
             self.engine.run()
         out = []
         for s in seqs:
