@@ -77,6 +77,8 @@ class LocalPlanner(Planner):
         else:                                     # a named architecture, random-init weights
             model = LlamaModel.random(settings.model, dev, seed=settings.seed)
         kw = {} if dev != "cpu" else {"num_blocks": 512}
+        if getattr(settings, "kv_blocks", 0):
+            kw["num_blocks"] = settings.kv_blocks
         eng = LLMEngine(model, max_batch=settings.max_batch, max_step_tokens=settings.max_step_tokens,
                         temperature=settings.temperature, seed=settings.seed, **kw)
         retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)

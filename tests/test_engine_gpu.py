@@ -48,3 +48,44 @@ def test_pipelined_and_cascade_paths_valid():
     # the cascade (LSE-merged) and plain attention paths; require broad agreement
     same = sum(x == y for x, y in zip(a, b))
     assert same >= len(a) * 0.8, same
+
+
+def test_api_local_planner_end_to_end():
+    """FastAPI app with the on-GPU planner (tiny Llama shapes, same kernels):
+    concurrent /plan requests through the async engine thread, /plan_and_execute
+    against mocked services, /healthz and /metrics."""
+    import asyncio
+    import json
+
+    import httpx
+    from fastapi.testclient import TestClient
+
+    from mcp_amd.api.server import create_app
+    from mcp_amd.config import Settings
+
+    reg = MemoryRegistry(synthetic_registry(6, seed=5))
+    names = [s.name for s in reg.list_services()]
+
+    def h(request):
+        return httpx.Response(200, json={"svc": request.url.host, "in": json.loads(request.content)})
+
+    st = Settings(planner_backend="local", model="tiny", max_batch=16, max_step_tokens=2048,
+                  kv_blocks=256, max_nodes=4, embed_dim=256)
+    app = create_app(st, registry=reg, transport=httpx.MockTransport(h))
+    with TestClient(app, raise_server_exceptions=False) as c:
+        assert c.get("/healthz").json()["ok"]
+
+        async def many():
+            transport = httpx.ASGITransport(app=app)
+            async with httpx.AsyncClient(transport=transport, base_url="http://t") as ac:
+                rs = await asyncio.gather(*[ac.post("/plan", json={"intent": synthetic_intent(i)})
+                                            for i in range(8)])
+            return rs
+
+        for r in asyncio.run(many()):
+            assert r.status_code == 200
+            validate_dag(r.json()["graph"], names)
+        r = c.post("/plan_and_execute", json={"intent": synthetic_intent(99)})
+        assert r.status_code == 200 and set(r.json()) == {"results", "errors"}
+        m = c.get("/metrics")
+        assert m.status_code == 200 and "mcp_" in m.text
