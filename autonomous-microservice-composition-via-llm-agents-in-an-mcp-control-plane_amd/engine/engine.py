@@ -123,6 +123,7 @@ class LLMEngine:
         self.running: List[Sequence] = []
         self.waiting: List[Sequence] = []
         self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
+        self._last_prefix = None                         # (token list object, entry)
         self.max_prefixes = 64
         self.steps = 0
         if self._graphs_wanted:
@@ -135,6 +136,12 @@ class LLMEngine:
     def get_prefix(self, tokens: Seq[int]) -> Optional[PrefixEntry]:
         """Shared prefix entry for ``tokens``; the first request creates a
         prefix job that computes the prefix KV once."""
+        # the planner hands every request of a batch the same cached token list:
+        # skip re-tupling / re-hashing ~700 tokens per request
+        last = self._last_prefix
+        if last is not None and last[0] is tokens and self.prefixes.get(last[1].tokens) is last[1]:
+            return last[1]
+        src = tokens
         tokens = tuple(tokens)
         if len(tokens) < BLOCK_SIZE:
             return None
@@ -153,6 +160,7 @@ class LLMEngine:
             job.prefix_entry = e
             self.alloc.incref(blocks)          # the job's own reference
             self.waiting.insert(0, job)
+        self._last_prefix = (src, e)
         return e
 
     def drop_prefixes(self):
@@ -160,6 +168,7 @@ class LLMEngine:
         for e in self.prefixes.values():
             self.alloc.free(e.blocks)
         self.prefixes.clear()
+        self._last_prefix = None
 
     def _materialize(self, seq: Sequence, copies: list):
         """Attach a request to its computed prefix: share the full blocks, copy
