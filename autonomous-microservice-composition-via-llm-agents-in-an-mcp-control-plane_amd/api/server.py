@@ -56,7 +56,8 @@ class ExecuteResponse(BaseModel):
 
 def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegistry] = None,
                planner: Optional[Planner] = None,
-               transport: Optional[httpx.AsyncBaseTransport] = None) -> FastAPI:
+               transport: Optional[httpx.AsyncBaseTransport] = None,
+               planner_transport: Optional[httpx.AsyncBaseTransport] = None) -> FastAPI:
     settings = settings or Settings.from_env()
     registry = registry if registry is not None else make_registry(settings.redis_url,
                                                                    settings.services_prefix)
@@ -73,6 +74,11 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
                                      seed=settings.seed)
             from ..planner.local import LocalPlanner
             return LocalPlanner.from_settings(settings, registry)
+        if settings.planner_backend == "openai":
+            from ..planner.remote import RemotePlanner
+            return RemotePlanner(registry, settings.openai_base_url, settings.openai_api_key,
+                                 settings.remote_model, settings.temperature,
+                                 transport=planner_transport)
         return StubPlanner(registry)
 
     @contextlib.asynccontextmanager

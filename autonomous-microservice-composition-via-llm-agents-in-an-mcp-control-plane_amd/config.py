@@ -32,7 +32,10 @@ class Settings:
     postgres_dsn: Optional[str] = None       # accepted for parity, unused
     services_prefix: str = SERVICES_PREFIX
     # planner
-    planner_backend: str = "stub"            # stub | local
+    planner_backend: str = "stub"            # stub | local | openai
+    openai_base_url: str = "https://api.openai.com/v1"   # openai backend (reference parity)
+    openai_api_key: Optional[str] = None     # OPENAI_API_KEY (control_plane.py:19)
+    remote_model: str = "gpt-4o-mini"        # control_plane.py:70
     model: str = "llama3-8b"                 # llama3-8b | llama3-70b | tiny
     tp: int = 1
     replicas: int = 1
@@ -58,6 +61,9 @@ class Settings:
             redis_url=_env("REDIS_URL", None),
             postgres_dsn=_env("POSTGRES_DSN", None),
             planner_backend=_env("MCP_PLANNER_BACKEND", "stub"),
+            openai_base_url=_env("OPENAI_BASE_URL", "https://api.openai.com/v1"),
+            openai_api_key=_env("OPENAI_API_KEY", None),
+            remote_model=_env("MCP_REMOTE_MODEL", "gpt-4o-mini"),
             model=_env("MCP_MODEL", "llama3-8b"),
             tp=_env("MCP_TP", 1, int),
             replicas=_env("MCP_REPLICAS", 1, int),

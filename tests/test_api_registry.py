@@ -115,3 +115,31 @@ def test_prompt_parts_share_prefix():
     full = build_prompt(svcs, "a")
     assert full == p1 + s1
     assert "\\n" not in full and "“a”" in full and full.endswith("JSON DAG:")
+
+
+def test_openai_compatible_remote_planner():
+    """MCP_PLANNER_BACKEND=openai: the reference's request shape (one system
+    message, temperature 0.2, model gpt-4o-mini, bearer key) against a mocked
+    /chat/completions; a non-object reply is the reference's HTTP 500."""
+    seen = []
+    replies = [json.dumps({"nodes": [{"name": "user-profile", "endpoint": "http://user-profile/api",
+                                      "inputs": {"user_id": "user_id"}}], "edges": []}),
+               "[1, 2]"]
+
+    def llm(request):
+        seen.append((str(request.url), request.headers.get("authorization"), json.loads(request.content)))
+        return httpx.Response(200, json={"choices": [{"message": {"content": replies[len(seen) - 1]}}]})
+
+    reg = MemoryRegistry(services3())
+    st = Settings(planner_backend="openai", openai_base_url="http://llm.test/v1", openai_api_key="k1")
+    app = create_app(st, registry=reg, transport=mock_transport(),
+                     planner_transport=httpx.MockTransport(llm))
+    with TestClient(app, raise_server_exceptions=False) as c:
+        r = c.post("/plan", json={"intent": "look up the user"})
+        assert r.status_code == 200 and r.json()["graph"]["nodes"][0]["name"] == "user-profile"
+        url, auth, body = seen[0]
+        assert url == "http://llm.test/v1/chat/completions" and auth == "Bearer k1"
+        assert body["model"] == "gpt-4o-mini" and body["temperature"] == 0.2
+        assert [m["role"] for m in body["messages"]] == ["system"]
+        assert "look up the user" in body["messages"][0]["content"]
+        assert c.post("/plan", json={"intent": "x"}).status_code == 500
