@@ -91,6 +91,9 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
                                      use_registry_fallback=settings.use_registry_fallback,
                                      telemetry_to_registry=settings.telemetry_to_registry)
         state["planner"] = _make_planner()
+        if settings.plan_cache > 0:
+            from ..planner.base import CachedPlanner
+            state["planner"] = CachedPlanner(state["planner"], registry, settings.plan_cache)
         try:
             yield
         finally:

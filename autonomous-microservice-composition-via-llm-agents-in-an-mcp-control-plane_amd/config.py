@@ -36,6 +36,7 @@ class Settings:
     openai_base_url: str = "https://api.openai.com/v1"   # openai backend (reference parity)
     openai_api_key: Optional[str] = None     # OPENAI_API_KEY (control_plane.py:19)
     remote_model: str = "gpt-4o-mini"        # control_plane.py:70
+    plan_cache: int = 0                      # >0: LRU plan cache entries (intent, registry version)
     model: str = "llama3-8b"                 # llama3-8b | llama3-70b | tiny
     tp: int = 1
     replicas: int = 1
@@ -64,6 +65,7 @@ class Settings:
             openai_base_url=_env("OPENAI_BASE_URL", "https://api.openai.com/v1"),
             openai_api_key=_env("OPENAI_API_KEY", None),
             remote_model=_env("MCP_REMOTE_MODEL", "gpt-4o-mini"),
+            plan_cache=_env("MCP_PLAN_CACHE", 0, int),
             model=_env("MCP_MODEL", "llama3-8b"),
             tp=_env("MCP_TP", 1, int),
             replicas=_env("MCP_REPLICAS", 1, int),

@@ -82,3 +82,40 @@ class StubPlanner(Planner):
                 edges.append(e)
             prev = s["name"]
         return {"nodes": nodes, "edges": edges}
+
+
+class CachedPlanner(Planner):
+    """LRU plan cache keyed by (intent, registry version) in front of any
+    planner (optional; ``MCP_PLAN_CACHE=<entries>``).  A registry
+    change bumps its version and so misses every old entry.  Plans are
+    returned as copies, so callers may mutate them."""
+
+    def __init__(self, inner: Planner, registry=None, size: int = 1024):
+        from collections import OrderedDict
+        self.inner = inner
+        self.registry = registry
+        self.size = max(1, size)
+        self._lru = OrderedDict()
+        self.hits = self.misses = 0
+
+    async def plan(self, intent: str) -> dict:
+        key = (intent, getattr(self.registry, "version", None))
+        dag = self._lru.get(key)
+        if dag is not None:
+            self._lru.move_to_end(key)
+            self.hits += 1
+            METRICS.inc("plan_cache_hits")
+            return json.loads(dag)
+        self.misses += 1
+        out = await self.inner.plan(intent)
+        self._lru[key] = json.dumps(out)
+        if len(self._lru) > self.size:
+            self._lru.popitem(last=False)
+        return out
+
+    async def aclose(self):
+        await self.inner.aclose()
+
+    def __getattr__(self, name):          # stalled / engine / ... of the wrapped planner
+        return getattr(self.inner, name)
+

@@ -143,3 +143,32 @@ def test_openai_compatible_remote_planner():
         assert [m["role"] for m in body["messages"]] == ["system"]
         assert "look up the user" in body["messages"][0]["content"]
         assert c.post("/plan", json={"intent": "x"}).status_code == 500
+
+
+def test_plan_cache_keyed_by_registry_version():
+    """MCP_PLAN_CACHE: repeated intents hit the LRU; a registry change misses."""
+    from mcp_amd.planner.base import CachedPlanner
+    reg = MemoryRegistry(services3())
+    inner = StubPlanner(reg)
+    calls = []
+    orig = inner.plan
+
+    async def counting(intent):
+        calls.append(intent)
+        return await orig(intent)
+    inner.plan = counting
+    cp = CachedPlanner(inner, reg, size=2)
+    a = asyncio.run(cp.plan("quote the order"))
+    b = asyncio.run(cp.plan("quote the order"))
+    assert a == b and len(calls) == 1 and cp.hits == 1
+    b["nodes"].clear()                                   # copies: the cache is not mutated
+    assert asyncio.run(cp.plan("quote the order")) == a
+    reg.register(make_service("new-svc", {"x": "string"}, {"y": "string"}))
+    asyncio.run(cp.plan("quote the order"))
+    assert len(calls) == 2                               # new registry version: miss
+    st = Settings(plan_cache=8)
+    app = create_app(st, registry=reg, planner=StubPlanner(reg), transport=mock_transport())
+    with TestClient(app) as c:
+        r1 = c.post("/plan", json={"intent": "email the user"}).json()
+        r2 = c.post("/plan", json={"intent": "email the user"}).json()
+        assert r1 == r2 and isinstance(app.state.components["planner"], CachedPlanner)
