@@ -21,7 +21,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -147,8 +149,13 @@ py::tuple pack_step(const py::list& seqs, int block_size, int group, const py::o
     maxb = std::max(maxb, tab.size());
   }
   // attention work lists (engine.batch.build_work)
-  const int t1 = 16 / group, t4 = 4 * (16 / group), cutoff = 2 * t1;
+  const int t1 = 16 / group, t4 = 4 * (16 / group);
+  static const char* cut_env = getenv("MCP_ATTN_NW1_CUTOFF");
+  static const char* xcd_env = getenv("MCP_ATTN_XCD_ORDER");
+  const int cutoff = cut_env ? atoi(cut_env) : 2 * t1;
+  const bool xcd_order = !xcd_env || atoi(xcd_env) == 1;
   std::vector<int32_t> w1s, w1q, w4s, w4q;
+  std::vector<int> depth1(S, 0);
   for (int s = 0; s < S; ++s) {
     const int ql = q_len[s];
     const bool small = ql <= cutoff;
@@ -156,7 +163,33 @@ py::tuple pack_step(const py::list& seqs, int block_size, int group, const py::o
     for (int q0 = 0; q0 < ql; q0 += qt) {
       (small ? w1s : w4s).push_back(s);
       (small ? w1q : w4q).push_back(q0);
+      if (small) ++depth1[s];
     }
+  }
+  if (xcd_order && !w1s.empty()) {
+    // 1-wave items of one sequence read the same K/V: sequences bucketed by
+    // item count (deepest first), blocks of 8, item d of the block's i-th
+    // sequence at 8 d + i - one XCD (block id % 8) and its L2 per sequence
+    int maxd = 0;
+    for (int s = 0; s < S; ++s) maxd = std::max(maxd, depth1[s]);
+    std::vector<int32_t> rs, rq;
+    rs.reserve(w1s.size());
+    rq.reserve(w1q.size());
+    for (int d = maxd; d >= 1; --d) {
+      std::vector<int> order;
+      for (int s = 0; s < S; ++s)
+        if (depth1[s] == d) order.push_back(s);
+      for (size_t b = 0; b < order.size(); b += 8) {
+        const size_t e = std::min(order.size(), b + 8);
+        for (int k = 0; k < d; ++k)
+          for (size_t i = b; i < e; ++i) {
+            rs.push_back(order[i]);
+            rq.push_back(k * t1);
+          }
+      }
+    }
+    w1s.swap(rs);
+    w1q.swap(rq);
   }
   std::vector<int32_t> csrc, cdst;
   if (!copies.is_none())

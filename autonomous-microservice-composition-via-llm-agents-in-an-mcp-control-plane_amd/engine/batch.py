@@ -12,6 +12,7 @@ the 4-wave variant (csrc/attention.hip).
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -41,13 +42,18 @@ class AttnMeta:
         return self.work
 
 
+_XCD_ORDER = os.environ.get("MCP_ATTN_XCD_ORDER", "1") == "1"
+
+
 def build_work(q_len: Sequence[int], group: int, small_cutoff: Optional[int] = None):
     """Split each sequence's query span into work items.
 
     Returns {nw: (seq_ids, q0s)} with nw in {1, 4}."""
     t1 = tokens_per_item(1, group)
     t4 = tokens_per_item(4, group)
-    cutoff = t1 * 2 if small_cutoff is None else small_cutoff
+    if small_cutoff is None:
+        small_cutoff = int(os.environ.get("MCP_ATTN_NW1_CUTOFF", str(t1 * 2)))
+    cutoff = small_cutoff
     out = {1: ([], []), 4: ([], [])}
     for s, ql in enumerate(q_len):
         if ql <= 0:
@@ -56,6 +62,25 @@ def build_work(q_len: Sequence[int], group: int, small_cutoff: Optional[int] = N
         for q0 in range(0, ql, qt):
             out[nw][0].append(s)
             out[nw][1].append(q0)
+    if _XCD_ORDER and out[1][0]:
+        # 1-wave items of one sequence read the same K/V: place them 8 work
+        # slots apart so they land on one XCD (block id % 8) and share its L2
+        # (sequences bucketed by item count, deepest first, so that a block of
+        # 8 sequences has equal depth and item d of sequence i sits at 8 d + i)
+        seqs, q0s = out[1]
+        groups = {}
+        for sq, q0 in zip(seqs, q0s):
+            groups.setdefault(sq, []).append(q0)
+        rs, rq = [], []
+        for depth in sorted({len(v) for v in groups.values()}, reverse=True):
+            order = [x for x in groups if len(groups[x]) == depth]
+            for b in range(0, len(order), 8):
+                blk = order[b:b + 8]
+                for d in range(depth):
+                    for x in blk:
+                        rs.append(x)
+                        rq.append(groups[x][d])
+        out[1] = (rs, rq)
     return out
 
 
