@@ -8,7 +8,12 @@ Same routes and request/response field names as the reference
 * ``POST /plan_and_execute`` {intent} -> {results, errors}  (payload ``{}``,
   control_plane.py:151)
 
-plus ``GET /metrics`` (Prometheus text, README.md:43-44) and ``GET /healthz``.
+plus ``GET /metrics`` (Prometheus text, README.md:43-44), ``GET /healthz`` and
+the audit surface the reference README claims (README.md:50): ``POST /plan``
+with ``"explain": true`` adds an ``explanation`` string next to ``graph`` (the
+response is unchanged otherwise), and ``POST /explain`` {graph} ->
+{explanation} (``planner/audit.py``).  ``MCP_ADAPTIVE=1`` hardens plans from
+recorded service telemetry (README.md:43-44,48).
 
 Differences by design: the app is built by a factory (no import-time DB
 connection), the HTTP client is lifespan-managed (D14) and the
@@ -24,7 +29,7 @@ from typing import Optional
 
 import httpx
 from fastapi import FastAPI, HTTPException
-from fastapi.responses import PlainTextResponse
+from fastapi.responses import JSONResponse, PlainTextResponse
 from pydantic import BaseModel
 
 from ..config import Settings
@@ -38,6 +43,15 @@ logging.basicConfig(level=logging.INFO)
 
 class PlanRequest(BaseModel):
     intent: str
+    explain: bool = False
+
+
+class ExplainRequest(BaseModel):
+    graph: dict
+
+
+class ExplainResponse(BaseModel):
+    explanation: str
 
 
 class PlanResponse(BaseModel):
@@ -94,6 +108,12 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
         if settings.plan_cache > 0:
             from ..planner.base import CachedPlanner
             state["planner"] = CachedPlanner(state["planner"], registry, settings.plan_cache)
+        if settings.adaptive:        # outside the cache: fresh telemetry applies to cached plans
+            from ..planner.audit import AdaptivePlanner
+            state["planner"] = AdaptivePlanner(state["planner"], registry,
+                                               settings.adaptive_error_rate,
+                                               settings.adaptive_min_calls,
+                                               settings.adaptive_retries)
         try:
             yield
         finally:
@@ -113,9 +133,27 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
                 raise HTTPException(status_code=503, detail=str(e))
             raise
 
+    def _explain(graph: dict) -> str:
+        from ..planner.audit import explain_plan
+        return explain_plan(graph, registry, settings.retries, settings.use_registry_fallback)
+
     @app.post("/plan", response_model=PlanResponse)
     async def plan_intent(req: PlanRequest):
-        return PlanResponse(graph=await _plan(req.intent))
+        resp = PlanResponse(graph=await _plan(req.intent))
+        if not req.explain:
+            return resp
+        try:
+            text = _explain(resp.graph)
+        except Exception as e:     # a plan the orchestrator would reject (T2 / cycle)
+            text = f"plan cannot be executed: {type(e).__name__}: {e}"
+        return JSONResponse({"graph": resp.graph, "explanation": text})
+
+    @app.post("/explain", response_model=ExplainResponse)
+    async def explain_graph(req: ExplainRequest):
+        try:
+            return ExplainResponse(explanation=_explain(req.graph))
+        except Exception as e:
+            raise HTTPException(status_code=422, detail=f"{type(e).__name__}: {e}")
 
     @app.post("/execute", response_model=ExecuteResponse)
     async def run_graph(req: ExecuteRequest):

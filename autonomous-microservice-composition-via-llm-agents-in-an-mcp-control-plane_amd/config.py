@@ -55,6 +55,11 @@ class Settings:
     concurrent_generations: bool = False     # parity default: strictly serial
     use_registry_fallback: bool = False      # parity default: edge fallback only
     telemetry_to_registry: bool = False
+    # adaptive planning from telemetry (README.md:43-44,48; planner/audit.py)
+    adaptive: bool = False
+    adaptive_error_rate: float = 0.2
+    adaptive_min_calls: int = 5
+    adaptive_retries: int = 1
 
     @classmethod
     def from_env(cls) -> "Settings":
@@ -83,4 +88,8 @@ class Settings:
             concurrent_generations=_env("MCP_CONCURRENT_GENERATIONS", False, bool),
             use_registry_fallback=_env("MCP_USE_REGISTRY_FALLBACK", False, bool),
             telemetry_to_registry=_env("MCP_TELEMETRY_TO_REGISTRY", False, bool),
+            adaptive=_env("MCP_ADAPTIVE", False, bool),
+            adaptive_error_rate=_env("MCP_ADAPTIVE_ERROR_RATE", 0.2, float),
+            adaptive_min_calls=_env("MCP_ADAPTIVE_MIN_CALLS", 5, int),
+            adaptive_retries=_env("MCP_ADAPTIVE_RETRIES", 1, int),
         )
