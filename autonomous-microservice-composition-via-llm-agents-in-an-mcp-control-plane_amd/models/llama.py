@@ -50,6 +50,9 @@ class LlamaConfig:
     rope_theta: float = 500000.0
     eps: float = 1e-5
     max_pos: int = 8192
+    # Llama-3.1 rope scaling: (factor, low_freq_factor, high_freq_factor,
+    # original_max_position_embeddings); None = plain RoPE (Llama-3)
+    rope_scaling: Optional[tuple] = None
 
     @property
     def group(self) -> int:
@@ -64,9 +67,16 @@ class LlamaConfig:
         return self.layers * 2 * (self.kv_heads // tp) * self.head_dim * 2
 
 
+_LLAMA31_ROPE = (8.0, 1.0, 4.0, 8192)
+
 CONFIGS = {
     "llama3-8b": LlamaConfig("llama3-8b"),
     "llama3-70b": LlamaConfig("llama3-70b", hidden=8192, layers=80, heads=64, kv_heads=8, ffn=28672),
+    # Llama-3.1: same shapes, 128k context through rope scaling (only the
+    # host-built cos/sin table changes; the kernels are shared)
+    "llama3.1-8b": LlamaConfig("llama3.1-8b", max_pos=131072, rope_scaling=_LLAMA31_ROPE),
+    "llama3.1-70b": LlamaConfig("llama3.1-70b", hidden=8192, layers=80, heads=64, kv_heads=8,
+                                ffn=28672, max_pos=131072, rope_scaling=_LLAMA31_ROPE),
     # reduced configs with the same kernels (tests / smoke): head_dim stays 128
     "llama3-1b-ish": LlamaConfig("llama3-1b-ish", hidden=2048, layers=16, heads=16, kv_heads=4, ffn=8192),
     "tiny": LlamaConfig("tiny", hidden=256, layers=2, heads=2, kv_heads=1, ffn=512),
@@ -167,8 +177,13 @@ class LlamaModel:
         self.tp_rank, self.tp, self.tp_group = tp_rank, tp, tp_group
         if cfg.heads % tp or cfg.kv_heads % tp or cfg.ffn % tp:
             raise ValueError(f"tp={tp} does not divide heads/kv_heads/ffn of {cfg.name}")
+        if cfg.head_dim != 128 or 16 % cfg.group:
+            # attention packs 16 MFMA rows as (16 / group) tokens x group heads of d=128
+            raise NotImplementedError(f"{cfg.name}: head_dim {cfg.head_dim} / GQA group {cfg.group} "
+                                      "not served by the gfx950 kernels (need d=128, group | 16)")
         self.hq, self.hkv = cfg.heads // tp, cfg.kv_heads // tp
-        self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device)
+        self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device,
+                                        cfg.rope_scaling)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self._allreduce = allreduce      # injectable (simulated ranks in tests)
         if tp > 1 and allreduce is None:

@@ -36,13 +36,22 @@ def config_from_hf(path) -> LlamaConfig:
     """``config.json`` of an HF Llama checkpoint -> LlamaConfig."""
     c = json.loads((Path(path) / "config.json").read_text())
     heads = c["num_attention_heads"]
+    rs = c.get("rope_scaling") or None
+    scaling = None
+    if rs is not None:
+        kind = rs.get("rope_type", rs.get("type"))
+        if kind != "llama3":
+            raise NotImplementedError(f"rope_scaling type {kind!r} (supported: llama3)")
+        scaling = (float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)),
+                   float(rs.get("high_freq_factor", 4.0)),
+                   int(rs.get("original_max_position_embeddings", 8192)))
     return LlamaConfig(
         name=c.get("_name_or_path") or Path(path).name,
         vocab_size=c["vocab_size"], hidden=c["hidden_size"], layers=c["num_hidden_layers"],
         heads=heads, kv_heads=c.get("num_key_value_heads", heads),
         head_dim=c.get("head_dim") or c["hidden_size"] // heads, ffn=c["intermediate_size"],
         rope_theta=float(c.get("rope_theta", 10000.0)), eps=float(c.get("rms_norm_eps", 1e-5)),
-        max_pos=int(c.get("max_position_embeddings", 8192)))
+        max_pos=int(c.get("max_position_embeddings", 8192)), rope_scaling=scaling)
 
 
 def _tensor_index(path: Path) -> Dict[str, Path]:
@@ -168,7 +177,12 @@ def save_llama_safetensors(cfg: LlamaConfig, w: LlamaWeights, path, shard_layers
         "vocab_size": cfg.vocab_size, "hidden_size": cfg.hidden, "num_hidden_layers": cfg.layers,
         "num_attention_heads": cfg.heads, "num_key_value_heads": cfg.kv_heads, "head_dim": D,
         "intermediate_size": cfg.ffn, "rope_theta": cfg.rope_theta, "rms_norm_eps": cfg.eps,
-        "max_position_embeddings": cfg.max_pos, "torch_dtype": "bfloat16"}, indent=1))
+        "max_position_embeddings": cfg.max_pos, "torch_dtype": "bfloat16",
+        **({"rope_scaling": {"rope_type": "llama3", "factor": cfg.rope_scaling[0],
+                             "low_freq_factor": cfg.rope_scaling[1],
+                             "high_freq_factor": cfg.rope_scaling[2],
+                             "original_max_position_embeddings": cfg.rope_scaling[3]}}
+           if cfg.rope_scaling else {})}, indent=1))
 
 
 def model_from_checkpoint(path, device, tp_rank: int = 0, tp: int = 1, tp_group=None):

@@ -61,8 +61,26 @@ def gemm(X, W, R: Optional[torch.Tensor] = None):
     return y.to(X.dtype)
 
 
-def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+def rope_inv_freq(head_dim: int, theta: float, scaling=None) -> torch.Tensor:
+    """Rotary inverse frequencies [D/2] (fp64).  ``scaling`` = (factor,
+    low_freq_factor, high_freq_factor, original_max_pos) applies Llama-3.1's
+    frequency-dependent rescaling: wavelengths longer than
+    original_max_pos / low_freq_factor are divided by ``factor``, shorter than
+    original_max_pos / high_freq_factor are kept, and the band in between is
+    interpolated linearly in 1/wavelength."""
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling is None:
+        return inv
+    factor, lo, hi, orig = scaling
+    wavelen = 2 * math.pi / inv
+    smooth = (orig / wavelen - lo) / (hi - lo)
+    mid = (1 - smooth) * inv / factor + smooth * inv
+    return torch.where(wavelen > orig / lo, inv / factor, torch.where(wavelen < orig / hi, inv, mid))
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None,
+                 scaling=None) -> torch.Tensor:
+    inv = rope_inv_freq(head_dim, theta, scaling)
     t = torch.arange(max_pos, dtype=torch.float64)
     f = torch.outer(t, inv)
     cs = torch.stack([f.cos(), f.sin()], dim=-1).float()      # [P, D/2, 2]

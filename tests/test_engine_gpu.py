@@ -89,3 +89,22 @@ def test_api_local_planner_end_to_end():
         assert r.status_code == 200 and set(r.json()) == {"results", "errors"}
         m = c.get("/metrics")
         assert m.status_code == 200 and "mcp_" in m.text
+
+
+def test_llama31_scaled_rope_engine_graph_matches_eager():
+    """Llama-3.1-style model (rope scaling, 128k max positions -> 2048-entry
+    block tables in the captured graphs) through the planner: hipGraph replay
+    and eager launches agree, and every plan validates."""
+    import dataclasses
+    from mcp_amd.models.llama import CONFIGS, random_weights
+    cfg = dataclasses.replace(CONFIGS["tiny"], name="tiny31", max_pos=131072,
+                              rope_scaling=CONFIGS["llama3.1-8b"].rope_scaling)
+    model = LlamaModel(cfg, random_weights(cfg, "cuda", seed=5), "cuda")
+    reg = MemoryRegistry(synthetic_registry(8, seed=2))
+    intents = [synthetic_intent(i) for i in range(6)]
+    eager, _ = _plans(model, reg, intents, graphs=False, cascade=False, pipeline=False)
+    graph, e2 = _plans(model, reg, intents, graphs=True, cascade=False, pipeline=False)
+    assert e2.stats["graph_steps"] > 0 and graph == eager
+    names = [s.name for s in reg.list_services()]
+    for d in graph:
+        validate_dag(d, names)

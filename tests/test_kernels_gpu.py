@@ -402,21 +402,24 @@ def test_gemm_splitk128(M, N, K):
     assert rel_err(y, e) < 2e-2
 
 
-@pytest.mark.parametrize("M", [1500, 3000, 200])
-def test_qkv_rope_fused(M):
+@pytest.mark.parametrize("M,long_ctx", [(1500, False), (3000, False), (200, False),
+                                         (1500, True), (200, True)])
+def test_qkv_rope_fused(M, long_ctx):
     """QKV GEMM with RoPE + paged K/V write in its epilogue (AGPR path; M = 200
     takes the GEMM + rope_kv fallback) against fp32 GEMM + reference rope_kv,
-    including rows without a cache slot (-1)."""
+    including rows without a cache slot (-1).  ``long_ctx``: Llama-3.1's
+    scaled 128k-position table with positions past 8k."""
     torch.manual_seed(9)
     Hq, Hkv, D, H, BS = 32, 8, 128, 4096, 64
     L = ops.lib()
     X = torch.randn(M, H, device=DEV).bfloat16()
     W = (torch.randn((Hq + 2 * Hkv) * D, H, device=DEV) / math.sqrt(H)).bfloat16()
     nb = (M + BS - 1) // BS + 2
-    pos = torch.randint(0, 8000, (M,), device=DEV, dtype=torch.int32)
+    P = 131072 if long_ctx else 8192
+    pos = torch.randint(0, P - 192, (M,), device=DEV, dtype=torch.int32)
     perm = torch.randperm(nb * BS, device=DEV)[:M].to(torch.int32)
     slots = torch.where(torch.rand(M, device=DEV) < 0.1, torch.full_like(perm, -1), perm)
-    cs = ref.rope_cos_sin(8192, D, 500000.0, DEV)
+    cs = ref.rope_cos_sin(P, D, 500000.0, DEV, (8.0, 1.0, 4.0, 8192) if long_ctx else None)
     q = torch.zeros(M, Hq, D, device=DEV, dtype=torch.bfloat16)
     kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
     vc = torch.zeros_like(kc)
