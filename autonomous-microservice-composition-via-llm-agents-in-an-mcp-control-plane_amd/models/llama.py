@@ -53,15 +53,74 @@ class LlamaConfig:
     # Llama-3.1 rope scaling: (factor, low_freq_factor, high_freq_factor,
     # original_max_position_embeddings); None = plain RoPE (Llama-3)
     rope_scaling: Optional[tuple] = None
+    # GQA padding: the checkpoint has q_heads_true query heads (group not a
+    # divisor of 16, e.g. Llama-3.2-3B's 24 q / 8 kv = 3); the engine runs
+    # ``heads`` = kv_heads x (group rounded up to a divisor of 16) with
+    # all-zero Wq rows / Wo columns in the pad heads, which is exact: a pad
+    # head's attention output only meets zero columns of Wo.  0 = no padding.
+    q_heads_true: int = 0
+    tie_embeddings: bool = False
 
     @property
     def group(self) -> int:
         return self.heads // self.kv_heads
 
+    @property
+    def group_true(self) -> int:
+        return (self.q_heads_true or self.heads) // self.kv_heads
+
     def params(self) -> int:
-        H, D = self.hidden, self.head_dim
-        per_layer = H * (self.heads + 2 * self.kv_heads) * D + self.heads * D * H + 3 * H * self.ffn + 2 * H
-        return self.layers * per_layer + 2 * self.vocab_size * H + H
+        H, D, hq = self.hidden, self.head_dim, self.q_heads_true or self.heads
+        per_layer = H * (hq + 2 * self.kv_heads) * D + hq * D * H + 3 * H * self.ffn + 2 * H
+        return self.layers * per_layer + (1 if self.tie_embeddings else 2) * self.vocab_size * H + H
+
+
+def padded_group(group: int) -> int:
+    """Smallest divisor of 16 (the MFMA row count attention packs heads into)
+    that is >= ``group``."""
+    for g in (1, 2, 4, 8, 16):
+        if g >= group:
+            return g
+    raise ValueError(f"GQA group {group} > 16")
+
+
+def pad_gqa(cfg: "LlamaConfig") -> "LlamaConfig":
+    """Config with query heads padded so the GQA group divides 16 (identity
+    when it already does)."""
+    g = cfg.heads // cfg.kv_heads
+    gp = padded_group(g)
+    if gp == g:
+        return cfg
+    return dataclasses.replace(cfg, heads=cfg.kv_heads * gp, q_heads_true=cfg.heads)
+
+
+def pad_q_rows(w: torch.Tensor, cfg: "LlamaConfig") -> torch.Tensor:
+    """[q_heads_true*D, H] -> [heads*D, H] with zero pad heads at the end of
+    each kv group (full, unsharded tensors)."""
+    if not cfg.q_heads_true:
+        return w
+    D, kv = cfg.head_dim, cfg.kv_heads
+    x = w.reshape(kv, cfg.group_true, D, -1)
+    out = x.new_zeros(kv, cfg.group, D, x.shape[-1])
+    out[:, :cfg.group_true] = x
+    return out.reshape(cfg.heads * D, -1)
+
+
+def pad_o_cols(w: torch.Tensor, cfg: "LlamaConfig") -> torch.Tensor:
+    """[H, q_heads_true*D] -> [H, heads*D] (zero columns for the pad heads)."""
+    return w if not cfg.q_heads_true else pad_q_rows(w.t().contiguous(), cfg).t().contiguous()
+
+
+def unpad_q_rows(w: torch.Tensor, cfg: "LlamaConfig") -> torch.Tensor:
+    if not cfg.q_heads_true:
+        return w
+    D = cfg.head_dim
+    return w.reshape(cfg.kv_heads, cfg.group, D, -1)[:, :cfg.group_true].reshape(
+        cfg.q_heads_true * D, -1).contiguous()
+
+
+def unpad_o_cols(w: torch.Tensor, cfg: "LlamaConfig") -> torch.Tensor:
+    return w if not cfg.q_heads_true else unpad_q_rows(w.t().contiguous(), cfg).t().contiguous()
 
     def kv_bytes_per_token(self, tp: int = 1) -> int:
         return self.layers * 2 * (self.kv_heads // tp) * self.head_dim * 2
@@ -77,6 +136,11 @@ CONFIGS = {
     "llama3.1-8b": LlamaConfig("llama3.1-8b", max_pos=131072, rope_scaling=_LLAMA31_ROPE),
     "llama3.1-70b": LlamaConfig("llama3.1-70b", hidden=8192, layers=80, heads=64, kv_heads=8,
                                 ffn=28672, max_pos=131072, rope_scaling=_LLAMA31_ROPE),
+    # Llama-3.2-3B: 24 q / 8 kv heads (group 3) padded to 32 q heads, tied
+    # embeddings, rope scaling factor 32
+    "llama3.2-3b": LlamaConfig("llama3.2-3b", hidden=3072, layers=28, heads=32, kv_heads=8,
+                               ffn=8192, max_pos=131072, rope_scaling=(32.0, 1.0, 4.0, 8192),
+                               q_heads_true=24, tie_embeddings=True),
     # reduced configs with the same kernels (tests / smoke): head_dim stays 128
     "llama3-1b-ish": LlamaConfig("llama3-1b-ish", hidden=2048, layers=16, heads=16, kv_heads=4, ffn=8192),
     "tiny": LlamaConfig("tiny", hidden=256, layers=2, heads=2, kv_heads=1, ffn=512),
@@ -154,16 +218,21 @@ def random_weights(cfg: LlamaConfig, device, dtype=torch.bfloat16, seed: int = 0
     out_std = std / math.sqrt(2 * cfg.layers)
     for l in range(cfg.layers):
         s = base + 1000 * (l + 1) + 97 * tp_rank
+        wqkv = rnd(((hq + 2 * hk) * D, H), s + 1)
+        wo = rnd((H, hq * D), s + 2, out_std)
+        if cfg.q_heads_true:       # pad heads: zero Wq rows and Wo columns (exact)
+            wqkv[:hq * D].view(hk, cfg.group, D, H)[:, cfg.group_true:] = 0
+            wo.view(H, hk, cfg.group, D)[:, :, cfg.group_true:] = 0
         layers.append(LayerWeights(
             attn_norm=norm_w(),
-            wqkv=rnd(((hq + 2 * hk) * D, H), s + 1),
-            wo=rnd((H, hq * D), s + 2, out_std),
+            wqkv=wqkv,
+            wo=wo,
             mlp_norm=norm_w(),
             w_gate_up=rnd((2 * f, H), s + 3),
             w_down=rnd((H, f), s + 4, out_std)))
-    return LlamaWeights(embed=rnd((cfg.vocab_size, H), base + 11, 1.0),
-                        layers=layers, final_norm=norm_w(),
-                        lm_head=rnd((cfg.vocab_size, H), base + 13))
+    embed = rnd((cfg.vocab_size, H), base + 11, 1.0)
+    return LlamaWeights(embed=embed, layers=layers, final_norm=norm_w(),
+                        lm_head=embed if cfg.tie_embeddings else rnd((cfg.vocab_size, H), base + 13))
 
 
 class LlamaModel:
@@ -180,7 +249,8 @@ class LlamaModel:
         if cfg.head_dim != 128 or 16 % cfg.group:
             # attention packs 16 MFMA rows as (16 / group) tokens x group heads of d=128
             raise NotImplementedError(f"{cfg.name}: head_dim {cfg.head_dim} / GQA group {cfg.group} "
-                                      "not served by the gfx950 kernels (need d=128, group | 16)")
+                                      "not served by the gfx950 kernels (need d=128, group | 16; "
+                                      "models.llama.pad_gqa pads the query heads)")
         self.hq, self.hkv = cfg.heads // tp, cfg.kv_heads // tp
         self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device,
                                         cfg.rope_scaling)

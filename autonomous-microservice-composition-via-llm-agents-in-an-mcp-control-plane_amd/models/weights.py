@@ -29,7 +29,8 @@ from typing import Dict, List, Optional
 import torch
 
 from ..ops import reference as ref
-from .llama import LayerWeights, LlamaConfig, LlamaWeights
+from .llama import (LayerWeights, LlamaConfig, LlamaWeights, pad_gqa, pad_o_cols, pad_q_rows,
+                    shard_cols, shard_rows, unpad_o_cols, unpad_q_rows)
 
 
 def config_from_hf(path) -> LlamaConfig:
@@ -45,13 +46,14 @@ def config_from_hf(path) -> LlamaConfig:
         scaling = (float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)),
                    float(rs.get("high_freq_factor", 4.0)),
                    int(rs.get("original_max_position_embeddings", 8192)))
-    return LlamaConfig(
+    return pad_gqa(LlamaConfig(
         name=c.get("_name_or_path") or Path(path).name,
         vocab_size=c["vocab_size"], hidden=c["hidden_size"], layers=c["num_hidden_layers"],
         heads=heads, kv_heads=c.get("num_key_value_heads", heads),
         head_dim=c.get("head_dim") or c["hidden_size"] // heads, ffn=c["intermediate_size"],
         rope_theta=float(c.get("rope_theta", 10000.0)), eps=float(c.get("rms_norm_eps", 1e-5)),
-        max_pos=int(c.get("max_position_embeddings", 8192)), rope_scaling=scaling)
+        max_pos=int(c.get("max_position_embeddings", 8192)), rope_scaling=scaling,
+        tie_embeddings=bool(c.get("tie_word_embeddings", False))))
 
 
 def _tensor_index(path: Path) -> Dict[str, Path]:
@@ -118,7 +120,12 @@ def load_llama_safetensors(path, device, cfg: Optional[LlamaConfig] = None, tp_r
     layers: List[LayerWeights] = []
     for i in range(cfg.layers):
         p = f"model.layers.{i}."
-        q = r.rows(p + "self_attn.q_proj.weight", tp_rank, tp)
+        if cfg.q_heads_true:       # GQA padding happens on the full tensor, then the TP split
+            q = shard_rows(pad_q_rows(r.full(p + "self_attn.q_proj.weight"), cfg), tp_rank, tp)
+            o = shard_cols(pad_o_cols(r.full(p + "self_attn.o_proj.weight"), cfg), tp_rank, tp)
+        else:
+            q = r.rows(p + "self_attn.q_proj.weight", tp_rank, tp)
+            o = r.cols(p + "self_attn.o_proj.weight", tp_rank, tp)
         k = r.rows(p + "self_attn.k_proj.weight", tp_rank, tp)
         v = r.rows(p + "self_attn.v_proj.weight", tp_rank, tp)
         g = r.rows(p + "mlp.gate_proj.weight", tp_rank, tp)
@@ -126,7 +133,7 @@ def load_llama_safetensors(path, device, cfg: Optional[LlamaConfig] = None, tp_r
         layers.append(LayerWeights(
             attn_norm=put(r.full(p + "input_layernorm.weight")),
             wqkv=put(torch.cat([q, k, v])),
-            wo=put(r.cols(p + "self_attn.o_proj.weight", tp_rank, tp)),
+            wo=put(o),
             mlp_norm=put(r.full(p + "post_attention_layernorm.weight")),
             w_gate_up=put(ref.interleave_gate_up(g, u)),
             w_down=put(r.cols(p + "mlp.down_proj.weight", tp_rank, tp))))
@@ -147,16 +154,18 @@ def save_llama_safetensors(cfg: LlamaConfig, w: LlamaWeights, path, shard_layers
     for i, lw in enumerate(w.layers):
         p = f"model.layers.{i}."
         q, k, v = torch.split(lw.wqkv, [cfg.heads * D, cfg.kv_heads * D, cfg.kv_heads * D])
+        q = unpad_q_rows(q, cfg)
         g, u = ref.deinterleave_gate_up(lw.w_gate_up)
         tensors.update({
             p + "input_layernorm.weight": lw.attn_norm, p + "self_attn.q_proj.weight": q,
             p + "self_attn.k_proj.weight": k, p + "self_attn.v_proj.weight": v,
-            p + "self_attn.o_proj.weight": lw.wo, p + "post_attention_layernorm.weight": lw.mlp_norm,
+            p + "self_attn.o_proj.weight": unpad_o_cols(lw.wo, cfg), p + "post_attention_layernorm.weight": lw.mlp_norm,
             p + "mlp.gate_proj.weight": g, p + "mlp.up_proj.weight": u,
             p + "mlp.down_proj.weight": lw.w_down})
     tensors["model.embed_tokens.weight"] = w.embed
     tensors["model.norm.weight"] = w.final_norm
-    tensors["lm_head.weight"] = w.lm_head
+    if not cfg.tie_embeddings:
+        tensors["lm_head.weight"] = w.lm_head
     tensors = {k: t.detach().cpu().contiguous() for k, t in tensors.items()}
     if shard_layers <= 0:
         save_file(tensors, str(path / "model.safetensors"))
@@ -175,7 +184,8 @@ def save_llama_safetensors(cfg: LlamaConfig, w: LlamaWeights, path, shard_layers
     (path / "config.json").write_text(json.dumps({
         "architectures": ["LlamaForCausalLM"], "model_type": "llama", "_name_or_path": cfg.name,
         "vocab_size": cfg.vocab_size, "hidden_size": cfg.hidden, "num_hidden_layers": cfg.layers,
-        "num_attention_heads": cfg.heads, "num_key_value_heads": cfg.kv_heads, "head_dim": D,
+        "num_attention_heads": cfg.q_heads_true or cfg.heads, "num_key_value_heads": cfg.kv_heads,
+        "head_dim": D, "tie_word_embeddings": cfg.tie_embeddings,
         "intermediate_size": cfg.ffn, "rope_theta": cfg.rope_theta, "rms_norm_eps": cfg.eps,
         "max_position_embeddings": cfg.max_pos, "torch_dtype": "bfloat16",
         **({"rope_scaling": {"rope_type": "llama3", "factor": cfg.rope_scaling[0],

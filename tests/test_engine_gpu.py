@@ -108,3 +108,44 @@ def test_llama31_scaled_rope_engine_graph_matches_eager():
     names = [s.name for s in reg.list_services()]
     for d in graph:
         validate_dag(d, names)
+
+
+def test_gqa_padded_group3_model_on_gpu_matches_cpu_and_plans():
+    """Llama-3.2-style GQA group 3 padded to 4 (zero pad heads): the GPU
+    forward matches the fp32 CPU forward of the same weights, and the planner
+    produces valid plans with graph replay == eager."""
+    import numpy as np
+    from mcp_amd.engine.batch import StepInputs, pack
+    from mcp_amd.engine.kv_cache import KVCache
+    from mcp_amd.models.llama import LlamaConfig, pad_gqa, random_weights
+    pc = pad_gqa(LlamaConfig("g3", hidden=768, layers=2, heads=6, kv_heads=2, ffn=1024,
+                             tie_embeddings=True))
+    assert pc.group == 4 and pc.group_true == 3
+    w = random_weights(pc, "cuda", seed=6, std=0.05)
+    model = LlamaModel(pc, w, "cuda")
+    T = 100
+    ids = torch.randint(0, pc.vocab_size, (T,), generator=torch.Generator().manual_seed(1))
+    step = StepInputs(token_ids=ids.int().numpy(), positions=np.arange(T, dtype=np.int32),
+                      slots=np.arange(T, dtype=np.int32), q_start=np.asarray([0], np.int32),
+                      q_len=np.asarray([T], np.int32), ctx_len=np.asarray([T], np.int32),
+                      block_table=np.asarray([[0, 1]], np.int32),
+                      logit_rows=np.asarray([T - 1], np.int32))
+    kv = KVCache(pc.layers, pc.kv_heads, pc.head_dim, 4, "cuda")
+    got = model.forward(pack(step, pc.group, "cuda"), kv).float().cpu()
+    import dataclasses
+    from mcp_amd.models.llama import LayerWeights, LlamaWeights
+    f32 = lambda t: t.float().cpu()
+    emb = f32(w.embed)
+    wc = LlamaWeights(emb, [LayerWeights(*[f32(getattr(l, fl.name)) for fl in dataclasses.fields(l)])
+                            for l in w.layers], f32(w.final_norm), emb)
+    kvc = KVCache(pc.layers, pc.kv_heads, pc.head_dim, 4, "cpu", dtype=torch.float32)
+    want = LlamaModel(pc, wc, "cpu").forward(pack(step, pc.group, "cpu"), kvc).float()
+    assert ((got - want).norm() / want.norm()).item() < 3e-2
+    reg = MemoryRegistry(synthetic_registry(8, seed=2))
+    intents = [synthetic_intent(i) for i in range(6)]
+    eager, _ = _plans(model, reg, intents, graphs=False, cascade=False, pipeline=False)
+    graph, e2 = _plans(model, reg, intents, graphs=True, cascade=True, pipeline=False)
+    names = [s.name for s in reg.list_services()]
+    for d in eager + graph:
+        validate_dag(d, names)
+    assert e2.stats["graph_steps"] > 0

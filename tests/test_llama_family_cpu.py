@@ -59,3 +59,63 @@ def test_unsupported_head_shapes_fail_loudly():
                 LlamaConfig("d64", hidden=256, layers=1, heads=4, kv_heads=1, head_dim=64, ffn=512)):
         with pytest.raises(NotImplementedError):
             LlamaModel(cfg, None, "cpu")
+
+
+# ---- GQA padding (Llama-3.2-3B: 24 q / 8 kv heads) --------------------------
+def _one_sequence_forward(model, cfg, ids):
+    import numpy as np
+    from mcp_amd.engine.batch import StepInputs, pack
+    from mcp_amd.engine.kv_cache import KVCache
+    kv = KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, 4, "cpu", dtype=torch.float32)
+    T = len(ids)
+    step = StepInputs(token_ids=np.asarray(ids, np.int32), positions=np.arange(T, dtype=np.int32),
+                      slots=np.arange(T, dtype=np.int32), q_start=np.asarray([0], np.int32),
+                      q_len=np.asarray([T], np.int32), ctx_len=np.asarray([T], np.int32),
+                      block_table=np.asarray([[0, 1]], np.int32),
+                      logit_rows=np.asarray([T - 1], np.int32))
+    return model.forward(pack(step, cfg.group, "cpu"), kv).float()[0]
+
+
+def _unpadded(pc, w):
+    from mcp_amd.models.llama import LayerWeights, LlamaWeights, unpad_o_cols, unpad_q_rows
+    D = pc.head_dim
+    layers = []
+    for lw in w.layers:
+        q, k, v = torch.split(lw.wqkv, [pc.heads * D, pc.kv_heads * D, pc.kv_heads * D])
+        layers.append(LayerWeights(lw.attn_norm, torch.cat([unpad_q_rows(q, pc), k, v]),
+                                   unpad_o_cols(lw.wo, pc), lw.mlp_norm, lw.w_gate_up, lw.w_down))
+    return LlamaWeights(w.embed, layers, w.final_norm, w.lm_head)
+
+
+def test_gqa_padding_is_exact_against_dense_unpadded_forward():
+    import dataclasses
+    from test_model_cpu import _dense_forward
+    from mcp_amd.models.llama import pad_gqa
+    cfg = LlamaConfig("g3", hidden=384, layers=2, heads=3, kv_heads=1, ffn=512, tie_embeddings=True)
+    pc = pad_gqa(cfg)
+    assert (pc.heads, pc.q_heads_true, pc.group, pc.group_true) == (4, 3, 4, 3)
+    w = random_weights(pc, "cpu", dtype=torch.float32, seed=7, std=0.05)
+    assert w.lm_head is w.embed
+    ids = torch.randint(0, cfg.vocab_size, (90,), generator=torch.Generator().manual_seed(2)).tolist()
+    got = _one_sequence_forward(LlamaModel(pc, w, "cpu"), pc, ids)
+    want = _dense_forward(dataclasses.replace(cfg), _unpadded(pc, w), ids)[-1]
+    assert ((got - want).norm() / want.norm()).item() < 1e-4
+
+
+def test_gqa_padding_checkpoint_roundtrip(tmp_path):
+    from mcp_amd.models.llama import pad_gqa
+    from mcp_amd.models.weights import load_llama_safetensors
+    pc = pad_gqa(LlamaConfig("g3", hidden=384, layers=2, heads=3, kv_heads=1, ffn=512,
+                             tie_embeddings=True))
+    w = random_weights(pc, "cpu", dtype=torch.float32, seed=3)
+    save_llama_safetensors(pc, w, tmp_path)
+    c = json.loads((tmp_path / "config.json").read_text())
+    assert c["num_attention_heads"] == 3 and c["tie_word_embeddings"] is True
+    cfg2, w2 = load_llama_safetensors(tmp_path, "cpu", dtype=torch.float32)
+    assert (cfg2.heads, cfg2.q_heads_true, cfg2.tie_embeddings) == (4, 3, True)
+    for a, b in zip(w.layers, w2.layers):
+        assert torch.equal(a.wqkv, b.wqkv) and torch.equal(a.wo, b.wo)
+    assert w2.lm_head is w2.embed
+    # TP=2 is not possible with one kv head; shapes of the 3B config per rank at TP=8
+    big = CONFIGS["llama3.2-3b"]
+    assert big.group == 4 and big.group_true == 3 and abs(big.params() / 1e9 - 3.21) < 0.01
