@@ -24,11 +24,21 @@ heads / FFN slices per rank), Wo / Wdown row-parallel followed by an
 all-reduce; embeddings and the LM head are replicated (the constrained sampler
 only touches a few LM-head rows, so every rank samples identically and no
 logit collective is needed).
+
+Sequence parallelism (Megatron SP; ``seq_parallel=True`` or
+``MCP_SEQ_PARALLEL=1``, TP > 1 only): the residual stream is split by rows
+across the TP ranks.  Each all-reduce after Wo / Wdown becomes a
+reduce-scatter, and the residual add + RMSNorm run fused (``add_rmsnorm``, K3)
+on this rank's T/tp rows.  Then an all-gather rebuilds the normed [T, H]
+input of the next column-parallel GEMM.  The bytes moved are those of the
+all-reduce.  The per-rank residual and norm traffic drops by tp.  The last
+layer gathers the residual once and takes the row-selected path above.
 """
 from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -239,7 +249,8 @@ class LlamaModel:
     """Stateless forward over weights + an external paged KV cache."""
 
     def __init__(self, cfg: LlamaConfig, weights: LlamaWeights, device, tp_rank: int = 0,
-                 tp: int = 1, tp_group=None, allreduce=None):
+                 tp: int = 1, tp_group=None, allreduce=None, seq_parallel: Optional[bool] = None,
+                 sp_collectives=None):
         self.cfg = cfg
         self.w = weights
         self.device = torch.device(device)
@@ -259,6 +270,13 @@ class LlamaModel:
         if tp > 1 and allreduce is None:
             from ..parallel.comm import make_allreduce
             self._allreduce = make_allreduce(tp_group, self.device)
+        if seq_parallel is None:
+            seq_parallel = os.environ.get("MCP_SEQ_PARALLEL", "0") == "1"
+        self.seq_parallel = bool(seq_parallel) and tp > 1
+        self._sp = sp_collectives          # (reduce_scatter, all_gather), injectable
+        if self.seq_parallel and sp_collectives is None:
+            from ..parallel.comm import make_sp_collectives
+            self._sp = make_sp_collectives(tp_group, self.device)
 
     @classmethod
     def random(cls, name: str, device, seed: int = 0, tp_rank: int = 0, tp: int = 1, tp_group=None):
@@ -276,6 +294,26 @@ class LlamaModel:
         self._allreduce(y)
         return y
 
+    @staticmethod
+    def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
+        if t.shape[0] == rows:
+            return t
+        out = t.new_zeros(rows, *t.shape[1:])
+        out[:t.shape[0]] = t
+        return out
+
+    def _sp_reduce_norm(self, a: torch.Tensor, w: torch.Tensor, x_sh: torch.Tensor,
+                        norm_w: torch.Tensor, Tp: int) -> torch.Tensor:
+        """Sequence-parallel row-parallel GEMM: partial ``a w^T`` over padded
+        rows, reduce-scatter to this rank's rows, then ``x_sh +=`` and RMSNorm
+        fused in one kernel.  Returns the normed rows."""
+        T = a.shape[0]
+        y = torch.empty(Tp * self.tp, w.shape[0], device=a.device, dtype=a.dtype)
+        if Tp * self.tp > T:
+            y[T:].zero_()
+        ops.gemm(a, w, out=y[:T])
+        return ops.add_rmsnorm(self._sp[0](y), x_sh, norm_w, self.cfg.eps)
+
     def forward(self, step, kv) -> torch.Tensor:
         """Runs one ragged step; returns final-normed hidden states of
         ``step.logit_rows`` ([R, H], bf16)."""
@@ -283,12 +321,32 @@ class LlamaModel:
         T = step.token_ids.numel()
         x = ops.embedding(step.token_ids, self.w.embed)
         L = cfg.layers
-        h = ops.rmsnorm(x, self.w.layers[0].attn_norm, cfg.eps)
-        q = torch.empty(T, self.hq, D, device=x.device, dtype=x.dtype)
+        sp = self.seq_parallel
+        if sp:
+            # x: this rank's Tp rows of the residual stream (T padded to tp*Tp)
+            Tp = -(-T // self.tp)
+            x = self._pad_rows(x, Tp * self.tp)[self.tp_rank * Tp:(self.tp_rank + 1) * Tp].clone()
+            h = self._sp[1](ops.rmsnorm(x, self.w.layers[0].attn_norm, cfg.eps))[:T]
+        else:
+            h = ops.rmsnorm(x, self.w.layers[0].attn_norm, cfg.eps)
+        q = torch.empty(T, self.hq, D, device=h.device, dtype=h.dtype)
         rows = step.logit_rows
         for l in range(L):
             lw = self.w.layers[l]
             kc, vc = kv.layer(l)
+            if sp and l + 1 < L:
+                ops.qkv_rope(h, lw.wqkv, step.positions, step.slots, self.cos_sin, q, kc, vc,
+                             self.hq, self.hkv, D)
+                a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
+                h = self._sp[1](self._sp_reduce_norm(a.view(T, self.hq * D), lw.wo, x,
+                                                     lw.mlp_norm, Tp))[:T]
+                act = ops.gemm_silu(h, lw.w_gate_up)
+                h = self._sp[1](self._sp_reduce_norm(act, lw.w_down, x,
+                                                     self.w.layers[l + 1].attn_norm, Tp))[:T]
+                continue
+            if sp:
+                # last layer: gather the residual once, then the row-selected path
+                x = self._sp[1](x)[:T].contiguous()
             # q, K/V cache <- rope(h Wqkv^T): rotation + paged write fused in the
             # GEMM epilogue on the AGPR path (ops.qkv_rope)
             ops.qkv_rope(h, lw.wqkv, step.positions, step.slots, self.cos_sin, q, kc, vc,

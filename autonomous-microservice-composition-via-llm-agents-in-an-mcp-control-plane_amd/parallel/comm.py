@@ -110,6 +110,51 @@ def make_allreduce(group, device) -> Callable[[torch.Tensor], None]:
     return gpu_allreduce
 
 
+def make_sp_collectives(group, device):
+    """Sequence-parallel pair (SURVEY §2.3 "Megatron SP"): ``reduce_scatter(y)``
+    sums the row-parallel partials ``y [tp*Tp, H]`` over the group and returns
+    this rank's ``[Tp, H]`` row block; ``all_gather(x)`` concatenates every
+    rank's ``[Tp, H]`` block into ``[tp*Tp, H]`` (rank order).  Together they
+    move the same bytes as the all-reduce they replace (C1/C2), but the
+    residual stream and the RMSNorms in between touch only ``Tp`` rows per rank.
+    GPU: the direct RCCL communicator; CPU: gloo in fp32 (gloo has no
+    reduce-scatter, so it is all-reduce + slice there)."""
+    device = torch.device(device)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if device.type != "cuda":
+        def cpu_rs(y: torch.Tensor) -> torch.Tensor:
+            yf = y.float()
+            dist.all_reduce(yf, group=group)
+            tp_rows = y.shape[0] // world
+            return yf[rank * tp_rows:(rank + 1) * tp_rows].to(y.dtype).contiguous()
+
+        def cpu_ag(x: torch.Tensor) -> torch.Tensor:
+            parts = [torch.empty_like(x, dtype=torch.float32) for _ in range(world)]
+            dist.all_gather(parts, x.float().contiguous(), group=group)
+            return torch.cat(parts).to(x.dtype)
+        return cpu_rs, cpu_ag
+    if os.environ.get("MCP_COMM", "native") == "native":
+        comm = NativeComm(group, device)
+
+        def gpu_rs(y: torch.Tensor) -> torch.Tensor:
+            return comm.reduce_scatter(y).view(y.shape[0] // world, *y.shape[1:])
+
+        def gpu_ag(x: torch.Tensor) -> torch.Tensor:
+            return comm.all_gather(x).view(world * x.shape[0], *x.shape[1:])
+        return gpu_rs, gpu_ag
+
+    def torch_rs(y: torch.Tensor) -> torch.Tensor:
+        out = y.new_empty(y.shape[0] // world, *y.shape[1:])
+        dist.reduce_scatter_tensor(out, y.contiguous(), group=group)
+        return out
+
+    def torch_ag(x: torch.Tensor) -> torch.Tensor:
+        out = x.new_empty(world * x.shape[0], *x.shape[1:])
+        dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+        return out
+    return torch_rs, torch_ag
+
+
 class StepBroadcaster:
     """Driver -> worker step descriptors for tensor-parallel engines."""
 

@@ -36,5 +36,12 @@ def test_native_rccl_single_rank():
         c.broadcast(m, 0)
         torch.cuda.synchronize()
         c.close()
+        # sequence-parallel pair over the same communicator type: row views
+        from mcp_amd.parallel.comm import make_sp_collectives
+        rs, ag = make_sp_collectives(dist.group.WORLD, "cuda:0")
+        y = torch.randn(6, 64, device="cuda").bfloat16()
+        assert rs(y).shape == (6, 64) and torch.equal(rs(y), y)
+        assert ag(y[:3]).shape == (3, 64) and torch.equal(ag(y[:3]), y[:3])
+        torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()

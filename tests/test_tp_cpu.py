@@ -2,6 +2,9 @@
 
 * the Megatron-sharded forward (column-parallel Wqkv / Wgate|up, row-parallel
   Wo / Wdown + all-reduce) equals the unsharded forward;
+* the sequence-parallel forward (reduce-scatter -> fused add+RMSNorm on T/tp
+  rows -> all-gather, ``MCP_SEQ_PARALLEL``) equals it too, also for a token
+  count that tp does not divide (padded rows);
 * the driver/worker engine (rank 0 schedules, samples and broadcasts step
   descriptors, rank 1 mirrors the forward) plans valid DAGs and shuts down.
 """
@@ -23,9 +26,9 @@ def _free_port():
     return p
 
 
-def _step_inputs():
+def _step_inputs(q_lens=(70, 5, 1)):
     from mcp_amd.engine.batch import StepInputs
-    q_lens, ctx = [70, 5, 1], [70, 5, 1]
+    q_lens, ctx = list(q_lens), list(q_lens)
     T = sum(q_lens)
     rng = np.random.RandomState(0)
     ids = rng.randint(0, 2000, T).astype(np.int32)
@@ -37,12 +40,13 @@ def _step_inputs():
     slots = np.concatenate([np.asarray(blocks[i])[p // 64] * 64 + p % 64
                             for i, p in enumerate(np.split(pos, np.cumsum(q_lens)[:-1]))]).astype(np.int32)
     return StepInputs(token_ids=ids, positions=pos, slots=slots,
-                      q_start=np.array([0, 70, 75], np.int32), q_len=np.array(q_lens, np.int32),
+                      q_start=np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32),
+                      q_len=np.array(q_lens, np.int32),
                       ctx_len=np.array(ctx, np.int32), block_table=bt,
-                      logit_rows=np.array([69, 74, 75], np.int32))
+                      logit_rows=(np.cumsum(q_lens) - 1).astype(np.int32))
 
 
-def _forward_worker(rank, world, port, out_dir):
+def _forward_worker(rank, world, port, out_dir, sp=False, q_lens=(70, 5, 1)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(2)
@@ -51,13 +55,15 @@ def _forward_worker(rank, world, port, out_dir):
     from mcp_amd.models.llama import LlamaModel, LlamaWeights, get_config, random_weights, shard_layer
     cfg = get_config("tiny-tp")
     full = random_weights(cfg, "cpu", seed=3)
-    step = pack(_step_inputs(), cfg.group, "cpu")
+    step = pack(_step_inputs(q_lens), cfg.group, "cpu")
     ref_model = LlamaModel(cfg, full, "cpu")
     kv1 = KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, 8, "cpu")
     h_ref = ref_model.forward(step, kv1).float()
     sh = LlamaWeights(embed=full.embed, final_norm=full.final_norm, lm_head=full.lm_head,
                       layers=[shard_layer(l, cfg, rank, world) for l in full.layers])
-    model = LlamaModel(cfg, sh, "cpu", tp_rank=rank, tp=world, tp_group=dist.group.WORLD)
+    model = LlamaModel(cfg, sh, "cpu", tp_rank=rank, tp=world, tp_group=dist.group.WORLD,
+                       seq_parallel=sp)
+    assert model.seq_parallel == sp
     kv = KVCache(cfg.layers, cfg.kv_heads // world, cfg.head_dim, 8, "cpu")
     h = model.forward(step, kv).float()
     err = ((h - h_ref).norm() / h_ref.norm()).item()
@@ -66,8 +72,8 @@ def _forward_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def _engine_worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _engine_worker(rank, world, port, out_dir, sp=False):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MCP_SEQ_PARALLEL=str(int(sp)))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(2)
     import json
@@ -106,10 +112,20 @@ def test_tp2_forward_matches_tp1(tmp_path):
         assert err < 2e-2, err
 
 
-def test_tp2_driver_worker_engine(tmp_path):
+@pytest.mark.parametrize("q_lens", [(70, 5, 1), (70, 4, 1)])
+def test_tp2_sequence_parallel_forward_matches_tp1(tmp_path, q_lens):
+    mp.spawn(_forward_worker, args=(2, _free_port(), str(tmp_path), True, q_lens), nprocs=2,
+             join=True)
+    for r in range(2):
+        err = float(open(tmp_path / f"r{r}.txt").read())
+        assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("sp", [False, True])
+def test_tp2_driver_worker_engine(tmp_path, sp):
     import json
     from mcp_amd.orchestrator import validate_dag
-    mp.spawn(_engine_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_engine_worker, args=(2, _free_port(), str(tmp_path), sp), nprocs=2, join=True)
     out = json.load(open(tmp_path / "dags.json"))
     for d in out["dags"]:
         validate_dag(d, out["names"])

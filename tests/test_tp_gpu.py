@@ -83,3 +83,70 @@ def test_tp8_simulated_ranks_match_tp1():
     for r in range(TP):
         err = (outs[r] - ref).norm() / ref.norm()
         assert err < 2e-2, (r, err.item())
+
+
+class ThreadSeqParallel:
+    """In-process reduce-scatter / all-gather across simulated ranks."""
+
+    def __init__(self, n):
+        self.n = n
+        self.slots = [None] * n
+        self.bar = threading.Barrier(n)
+
+    def for_rank(self, r):
+        def rs(y):
+            torch.cuda.synchronize()
+            self.slots[r] = y
+            self.bar.wait()
+            rows = y.shape[0] // self.n
+            s = sum(x[r * rows:(r + 1) * rows].float() for x in self.slots).to(y.dtype)
+            torch.cuda.synchronize()
+            self.bar.wait()
+            return s
+
+        def ag(x):
+            torch.cuda.synchronize()
+            self.slots[r] = x
+            self.bar.wait()
+            out = torch.cat(self.slots)
+            torch.cuda.synchronize()
+            self.bar.wait()
+            return out
+        return rs, ag
+
+
+def test_tp8_sequence_parallel_matches_tp1():
+    """SP with the HIP kernels: 18 tokens over 8 ranks (3 rows each, 6 padded),
+    fused add+RMSNorm on each rank's rows, row-selected last layer."""
+    cfg = LlamaConfig("tp8-sp-test", vocab_size=2048, hidden=1024, layers=3, heads=8, kv_heads=8,
+                      ffn=2048)
+    full = random_weights(cfg, "cuda", seed=11)
+    step = pack(_step(), cfg.group, "cuda")
+    ref = LlamaModel(cfg, full, "cuda").forward(
+        step, KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, 8, "cuda")).float()
+    ar, sp = ThreadAllReduce(TP), ThreadSeqParallel(TP)
+    outs = [None] * TP
+    errs = []
+
+    def rank(r):
+        try:
+            w = LlamaWeights(embed=full.embed, final_norm=full.final_norm, lm_head=full.lm_head,
+                             layers=[shard_layer(l, cfg, r, TP) for l in full.layers])
+            m = LlamaModel(cfg, w, "cuda", tp_rank=r, tp=TP, allreduce=ar.for_rank(r),
+                           seq_parallel=True, sp_collectives=sp.for_rank(r))
+            kvr = KVCache(cfg.layers, cfg.kv_heads // TP, cfg.head_dim, 8, "cuda")
+            outs[r] = m.forward(step, kvr).float()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+            ar.bar.abort()
+            sp.bar.abort()
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(TP)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    for r in range(TP):
+        err = (outs[r] - ref).norm() / ref.norm()
+        assert err < 2e-2, (r, err.item())
