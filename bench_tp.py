@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--max-nodes", type=int, default=6)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--seq-parallel", action="store_true",
+                    help="Megatron sequence parallelism (reduce-scatter / all-gather) for TP > 1")
     args = ap.parse_args()
 
     from mcp_amd.engine.engine import LLMEngine
@@ -57,6 +59,8 @@ def main():
     tp = world
     group = dist.group.WORLD if world > 1 else None
     t0 = time.time()
+    if args.seq_parallel:
+        os.environ["MCP_SEQ_PARALLEL"] = "1"
     model = LlamaModel.random(args.model, dev, seed=args.seed, tp_rank=rank, tp=tp, tp_group=group)
     torch.cuda.synchronize()
     log(f"[rank {rank}] {args.model} TP={tp} shard ready in {time.time() - t0:.1f}s")
@@ -132,7 +136,7 @@ def main():
     exec_stats = asyncio.run(run_all())
     print(json.dumps({
         "config": "llama3-70b TP planner, 50-service registry, retries + ordered fallbacks",
-        "model": args.model, "tp": tp, "services": args.services, "batch": args.batch,
+        "model": args.model, "tp": tp, "seq_parallel": model.seq_parallel, "services": args.services, "batch": args.batch,
         "plans_per_s": round(len(dags) / elapsed, 3),
         "p50_latency_ms": round(statistics.median(lats) * 1e3, 1) if lats else None,
         "tokens": eng.stats["tokens"], "execution": exec_stats,
