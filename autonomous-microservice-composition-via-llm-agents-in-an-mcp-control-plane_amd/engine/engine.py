@@ -225,16 +225,20 @@ class LLMEngine:
         if seq.is_prefix_job:
             seq.prefix_entry.computed = True
         else:
+            t_parse = time.perf_counter()
             try:
                 seq.result = seq.decoder.result()
             except Exception as e:  # pragma: no cover - grammar guarantees JSON
                 seq.error = repr(e)
+            METRICS.observe("parse_s", time.perf_counter() - t_parse)
             METRICS.plan_done(seq.t_done - seq.t_submit)
-            # per-request phases: queue (submit -> admitted), first sampled token, total
+            # per-request phases: queue (submit -> admitted), first sampled
+            # token (prefill), first token -> done (decode + jump-forward), total
             if seq.t_admit is not None:
                 METRICS.observe("queue_s", seq.t_admit - seq.t_submit)
             if seq.t_first is not None:
                 METRICS.observe("ttft_s", seq.t_first - seq.t_submit)
+                METRICS.observe("decode_s", seq.t_done - seq.t_first)
             METRICS.inc("sampled_tokens", seq.n_samples)
         if seq.on_done is not None:
             seq.on_done(seq)

@@ -92,12 +92,20 @@ class LocalPlanner(Planner):
         return self.retriever.search(intent, self.topk, services)
 
     def prepare(self, intent: str, services: Optional[Sequence[dict]] = None):
+        """Per-request host phases: registry read + top-k
+        retrieval (``retrieval_s``), grammar / prompt build + tokenisation
+        (``prompt_s``); the engine adds queue / TTFT / decode / parse."""
+        t0 = time.perf_counter()
         services = self.registry.list_services() if services is None else services
-        dec, ptoks = self._decoder_and_prefix(intent, services)
-        return dec, ptoks, self.tok.encode(self.suffix_text(intent))
+        dec, ptoks, t1 = self._decoder_and_prefix(intent, services, timed=True)
+        stoks = self.tok.encode(self.suffix_text(intent))
+        METRICS.observe("retrieval_s", t1 - t0)
+        METRICS.observe("prompt_s", time.perf_counter() - t1)
+        return dec, ptoks, stoks
 
-    def _decoder_and_prefix(self, intent: str, services: Sequence[dict]):
+    def _decoder_and_prefix(self, intent: str, services: Sequence[dict], timed: bool = False):
         cands = self.candidates(intent, services)
+        t1 = time.perf_counter() if timed else None
         key = tuple(s["name"] for s in cands) + (getattr(self.registry, "version", 0),)
         spec = self._spec_cache.get(key)
         if spec is None:
@@ -112,7 +120,7 @@ class LocalPlanner(Planner):
             if len(self._prefix_cache) > 256:
                 self._prefix_cache.clear()
             self._prefix_cache[key] = ptoks
-        return DagDecoder(spec), ptoks
+        return (DagDecoder(spec), ptoks, t1) if timed else (DagDecoder(spec), ptoks)
 
     @staticmethod
     def suffix_text(intent: str) -> str:

@@ -135,6 +135,11 @@ def test_local_planner_behind_api(tiny_engine):
         validate_dag(r.json()["graph"], [s.name for s in reg.list_services()])
         r2 = c.post("/plan_and_execute", json={"intent": "score the order"})
         assert r2.status_code == 200 and set(r2.json()) == {"results", "errors"}
+        # per-request phases reach /metrics
+        text = c.get("/metrics").text
+        for phase in ("retrieval_s", "prompt_s", "queue_s", "ttft_s", "decode_s", "parse_s",
+                      "execute_latency_s"):
+            assert f"mcp_{phase}" in text, phase
 
 
 def test_retrieval_cpu_prunes_prompt():
