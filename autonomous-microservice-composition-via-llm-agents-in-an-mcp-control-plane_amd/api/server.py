@@ -177,6 +177,22 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
     return app
 
 
+_APP = None
+
+
+def __getattr__(name):
+    """``uvicorn mcp_amd.api.server:app`` (the reference's
+    ``uvicorn control_plane:app``): the app is built from the environment on
+    first access, not at import, so importing the module opens no connection
+    and loads no model (the reference built its singletons at import, :135-138)."""
+    global _APP
+    if name == "app":
+        if _APP is None:
+            _APP = create_app()
+        return _APP
+    raise AttributeError(name)
+
+
 def main():  # pragma: no cover - CLI entry (reference :155-157)
     import argparse
 

@@ -172,3 +172,21 @@ def test_plan_cache_keyed_by_registry_version():
         r1 = c.post("/plan", json={"intent": "email the user"}).json()
         r2 = c.post("/plan", json={"intent": "email the user"}).json()
         assert r1 == r2 and isinstance(app.state.components["planner"], CachedPlanner)
+
+
+def test_module_level_app_for_uvicorn(monkeypatch):
+    """``uvicorn mcp_amd.api.server:app`` works like the reference's
+    ``uvicorn control_plane:app``: a lazily built app from the environment."""
+    import importlib
+
+    from fastapi import FastAPI
+    monkeypatch.setenv("MCP_PLANNER_BACKEND", "stub")
+    monkeypatch.delenv("REDIS_URL", raising=False)
+    mod = importlib.import_module("mcp_amd.api.server")
+    monkeypatch.setattr(mod, "_APP", None)
+    from uvicorn.importer import import_from_string
+    app = import_from_string("mcp_amd.api.server:app")
+    assert isinstance(app, FastAPI) and app is mod.app
+    with TestClient(app) as c:
+        assert c.get("/healthz").status_code == 200
+        assert c.post("/plan", json={}).status_code == 422
