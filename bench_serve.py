@@ -132,6 +132,8 @@ def main():
     else:
         if world > 1:
             dist.barrier()
+        from mcp_amd.utils.metrics import METRICS
+        METRICS.reset()
         lat, dags, elapsed, n, bs = run_qps(planner, engine, args.qps, args.duration, args.seed, rank)
         for d in dags:
             validate_dag(d, names)
@@ -149,7 +151,11 @@ def main():
                    value=round(plans_s, 2), unit="plans/s", p50_latency_ms=round(p50 * 1e3, 1),
                    p99_latency_ms=round(p99 * 1e3, 1), mean_running_batch=round(mean_b, 1),
                    graph_steps=engine.stats["graph_steps"], steps=engine.stats["steps"],
-                   duration_s=args.duration)
+                   duration_s=args.duration,
+                   # per-request phases on this rank, p50 in ms
+                   phases_p50_ms={k: round(METRICS.windows[k].quantile(0.5) * 1e3, 3)
+                                  for k in ("retrieval_s", "prompt_s", "queue_s", "ttft_s",
+                                            "decode_s", "parse_s") if k in METRICS.windows})
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
