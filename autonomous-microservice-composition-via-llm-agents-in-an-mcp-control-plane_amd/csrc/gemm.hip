@@ -309,6 +309,16 @@ int gemm128_splits(int M, int N, int K) {
   }
   if (tiles > G) return 1;
   const int nkt = K / BK;
+  // fewest splits that give every CU a workgroup while each keeps <= 32
+  // k-tiles: fewer fp32 partials to write and reduce.  Measured at M = 64-256
+  // on the 8B shapes (profiles/gemm_small_m_splitk_sweep.jsonl): gate|up 2 vs
+  // 4 splits -18..-20 %, qkv / o at M = 192-256 4 vs 8 -5..-16 %, down
+  // (K = 14336) keeps 8
+  for (int S = 2; S <= 16; S *= 2) {
+    if (nkt % S || nkt / S < 8 || nkt / S > 32) continue;
+    if ((size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) break;
+    if (tiles * S >= G) return S;
+  }
   for (int S = 2; S <= 16; ++S) {
     if (nkt % S || nkt / S < 8) continue;
     if ((size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) break;
