@@ -313,8 +313,8 @@ int gemm128_splits(int M, int N, int K) {
   // k-tiles: fewer fp32 partials to write and reduce.  Measured at M = 64-256
   // on the 8B shapes (profiles/gemm_small_m_splitk_sweep.jsonl): gate|up 2 vs
   // 4 splits -18..-20 %, qkv / o at M = 192-256 4 vs 8 -5..-16 %, down
-  // (K = 14336) keeps 8
-  for (int S = 2; S <= 16; S *= 2) {
+  // (K = 14336) keeps 8.  Applied in the measured range M <= 256 only.
+  for (int S = 2; S <= 16 && M <= 256; S *= 2) {
     if (nkt % S || nkt / S < 8 || nkt / S > 32) continue;
     if ((size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) break;
     if (tiles * S >= G) return S;
