@@ -12,6 +12,29 @@ namespace {
 
 inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// Launch-error check after every kernel launch: hipGetLastError is a host-side
+// query (no sync), so it is always on.  MCP_CHECK_LAUNCH=1 (the GPU tests set
+// it) additionally synchronises the stream outside graph capture, so an
+// asynchronous fault is reported by the op that caused it.
+bool sync_check() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("MCP_CHECK_LAUNCH");
+    on = e && e[0] == '1';
+  }
+  return on == 1;
+}
+
+void check_launch(const char* op) {
+  hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, op, ": kernel launch failed: ", hipGetErrorString(e));
+  if (!sync_check()) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  e = hipStreamSynchronize(stream());
+  TORCH_CHECK(e == hipSuccess, op, ": kernel failed: ", hipGetErrorString(e));
+}
+
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
@@ -24,6 +47,7 @@ void rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, double e
   const int H = x.size(-1);
   TORCH_CHECK(H % 8 == 0 && w.numel() == H && out.sizes() == x.sizes(), "rmsnorm shapes");
   launch_rmsnorm(x.data_ptr(), w.data_ptr(), out.data_ptr(), x.numel() / H, H, (float)eps, stream());
+  check_launch("rmsnorm");
 }
 
 void add_rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w, at::Tensor& out,
@@ -34,6 +58,7 @@ void add_rmsnorm(const at::Tensor& x, at::Tensor& residual, const at::Tensor& w,
               out.sizes() == x.sizes(), "add_rmsnorm shapes");
   launch_add_rmsnorm(x.data_ptr(), residual.data_ptr(), w.data_ptr(), out.data_ptr(),
                      x.numel() / H, H, (float)eps, stream());
+  check_launch("add_rmsnorm");
 }
 
 void silu_mul(const at::Tensor& x, at::Tensor& y) {
@@ -41,6 +66,7 @@ void silu_mul(const at::Tensor& x, at::Tensor& y) {
   const int F = y.size(-1);
   TORCH_CHECK(F % 8 == 0 && x.size(-1) == 2 * F && x.numel() == 2 * y.numel(), "silu_mul shapes");
   launch_silu_mul(x.data_ptr(), y.data_ptr(), y.numel() / F, F, stream());
+  check_launch("silu_mul");
 }
 
 void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) {
@@ -48,6 +74,7 @@ void embedding(const at::Tensor& ids, const at::Tensor& table, at::Tensor& out) 
   const int H = table.size(1);
   TORCH_CHECK(H % 8 == 0 && out.size(-1) == H && out.numel() == ids.numel() * H, "embedding shapes");
   launch_embedding(ids.data_ptr<int>(), table.data_ptr(), out.data_ptr(), ids.numel(), H, stream());
+  check_launch("embedding");
 }
 
 void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slots,
@@ -67,6 +94,7 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slo
   launch_rope_kv(qkv.data_ptr(), pos.data_ptr<int>(), slots.data_ptr<int>(), cos_sin.data_ptr(),
                  q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D,
                  k_cache.size(2), stream());
+  check_launch("rope_kv");
 }
 
 // QKV projection + RoPE + paged K/V write: fused in the GEMM epilogue when the
@@ -94,6 +122,7 @@ void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const a
               q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv,
               (int)k_cache.size(2)};
   launch_qkv_rope(X.data_ptr(), W.data_ptr(), qkv.data_ptr(), M, N, K, (int)D, ra, stream());
+  check_launch("qkv_rope");
 }
 
 void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::optional<at::Tensor>& R,
@@ -113,6 +142,7 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
     rp = R->data_ptr();
   }
   launch_gemm_tn_algo(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, (int)algo, stream());
+  check_launch("gemm");
 }
 
 void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
@@ -123,6 +153,7 @@ void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_silu: unsupported shape");
   TORCH_CHECK(launch_gemm_silu(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, stream()) == 0,
               "gemm_silu failed");
+  check_launch("gemm_silu");
 }
 
 void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64_t v) {
@@ -131,6 +162,7 @@ void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64
   TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_variant: unsupported shape");
   TORCH_CHECK(launch_gemm_tn_256_variant(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, v,
                                          stream()) == 0, "bad variant");
+  check_launch("gemm_variant");
 }
 
 void gemm_plan_set_py(int64_t N, int64_t K, const std::vector<int64_t>& codes) {
@@ -146,12 +178,14 @@ void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   TORCH_CHECK(W.size(1) == K && Y.numel() == (int64_t)M * N, "gemm_f32out shapes");
   TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_f32out: unsupported shape");
   launch_gemm_tn_f32out(X.data_ptr(), W.data_ptr(), Y.data_ptr<float>(), M, N, K, stream());
+  check_launch("gemm_f32out");
 }
 
 void l2norm_rows(at::Tensor& x) {
   CHECK_BF16_TENSOR(x);
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0, "l2norm_rows: [N, D], D % 8 == 0");
   launch_l2norm_rows(x.data_ptr(), x.size(0), x.size(1), stream());
+  check_launch("l2norm_rows");
 }
 
 void segment_topk(const at::Tensor& vals, const c10::optional<at::Tensor>& idx, int64_t seg_len,
@@ -166,6 +200,7 @@ void segment_topk(const at::Tensor& vals, const c10::optional<at::Tensor>& idx, 
   const int rc = launch_segment_topk(vals.data_ptr<float>(), ip, B, L, seg_len, k,
                                      out_v.data_ptr<float>(), out_i.data_ptr<int>(), stream());
   TORCH_CHECK(rc == 0, "segment_topk: seg_len <= 4096 and 0 < k <= seg_len");
+  check_launch("segment_topk");
 }
 
 void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -205,6 +240,7 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
       block_table.size(1), work_seq.data_ptr<int>(), work_q0.data_ptr<int>(), work_seq.numel(), nw,
       Hq, Hkv, D, (float)scale, kb, po, pl, stream());
   TORCH_CHECK(rc == 0, "paged_attention: unsupported config (code ", rc, ")");
+  check_launch("paged_attention");
 }
 
 void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -221,6 +257,7 @@ void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
                                          pre_bt.data_ptr<int>(), pre_keys, pre_tokens, Hq, Hkv, D,
                                          (float)scale, stream());
   TORCH_CHECK(rc == 0, "prefix_attention: unsupported config (code ", rc, ")");
+  check_launch("prefix_attention");
 }
 
 void sample_allowed(const at::Tensor& hidden, const at::Tensor& W, const at::Tensor& allow_ptr,
@@ -238,6 +275,7 @@ void sample_allowed(const at::Tensor& hidden, const at::Tensor& W, const at::Ten
                         allow_ids.data_ptr<int>(), ctr.data_ptr<int>(),
                         (float)temperature, (unsigned long long)seed, S, H,
                         out_tok.data_ptr<int>(), lp, stream());
+  check_launch("sample_allowed");
 }
 
 void sample_dense(const at::Tensor& logits, const at::Tensor& ctr, double temperature,
@@ -247,6 +285,7 @@ void sample_dense(const at::Tensor& logits, const at::Tensor& ctr, double temper
   launch_sample_dense(logits.data_ptr(), logits.size(0), logits.size(1),
                       ctr.data_ptr<int>(), (float)temperature,
                       (unsigned long long)seed, out_tok.data_ptr<int>(), stream());
+  check_launch("sample_dense");
 }
 
 void copy_blocks(at::Tensor& data, const at::Tensor& src, const at::Tensor& dst) {
@@ -256,12 +295,14 @@ void copy_blocks(at::Tensor& data, const at::Tensor& src, const at::Tensor& dst)
   const int64_t block_elems = data.size(3) * data.size(4) * data.size(5);
   launch_copy_blocks(data.data_ptr(), src.data_ptr<int>(), dst.data_ptr<int>(), src.numel(),
                      data.size(0) * 2, data.size(2), block_elems, stream());
+  check_launch("copy_blocks");
 }
 
 void add_inplace(at::Tensor& y, const at::Tensor& x) {
   CHECK_BF16_TENSOR(y); CHECK_BF16_TENSOR(x);
   TORCH_CHECK(y.numel() == x.numel() && y.numel() % 8 == 0, "add_inplace shapes");
   launch_add_inplace(y.data_ptr(), x.data_ptr(), y.numel(), stream());
+  check_launch("add_inplace");
 }
 
 // ---- K12 custom all-reduce: the state is an opaque int64 handle on the Python side
@@ -286,6 +327,7 @@ void car_run(int64_t h, const at::Tensor& inp, at::Tensor& out, int64_t mode, in
   const int rc = car_allreduce((void*)(intptr_t)h, inp.data_ptr(), out.data_ptr(), inp.numel(),
                                (int)mode, (int)blocks, stream());
   TORCH_CHECK(rc == 0, "custom all-reduce launch failed (", rc, ")");
+  check_launch("car_run");
 }
 
 // ---- K13 direct RCCL communicator: opaque int64 handle on the Python side
@@ -318,6 +360,7 @@ void nccl_all_reduce(int64_t comm, at::Tensor& t, int64_t op) {
   TORCH_CHECK(rccl_all_reduce((void*)(intptr_t)comm, t.data_ptr(), t.data_ptr(), t.numel(),
                               rccl_dtype(t), op, stream()) == 0,
               "ncclAllReduce: ", rccl_last_error((void*)(intptr_t)comm));
+  check_launch("nccl_all_reduce");
 }
 
 void nccl_all_gather(int64_t comm, const at::Tensor& in, at::Tensor& out) {
@@ -326,6 +369,7 @@ void nccl_all_gather(int64_t comm, const at::Tensor& in, at::Tensor& out) {
   TORCH_CHECK(rccl_all_gather((void*)(intptr_t)comm, in.data_ptr(), out.data_ptr(), in.numel(),
                               rccl_dtype(in), stream()) == 0,
               "ncclAllGather: ", rccl_last_error((void*)(intptr_t)comm));
+  check_launch("nccl_all_gather");
 }
 
 void nccl_reduce_scatter(int64_t comm, const at::Tensor& in, at::Tensor& out, int64_t op) {
@@ -334,6 +378,7 @@ void nccl_reduce_scatter(int64_t comm, const at::Tensor& in, at::Tensor& out, in
   TORCH_CHECK(rccl_reduce_scatter((void*)(intptr_t)comm, in.data_ptr(), out.data_ptr(),
                                   out.numel(), rccl_dtype(in), op, stream()) == 0,
               "ncclReduceScatter: ", rccl_last_error((void*)(intptr_t)comm));
+  check_launch("nccl_reduce_scatter");
 }
 
 void nccl_broadcast(int64_t comm, at::Tensor& t, int64_t root) {
@@ -341,6 +386,7 @@ void nccl_broadcast(int64_t comm, at::Tensor& t, int64_t root) {
   TORCH_CHECK(rccl_broadcast((void*)(intptr_t)comm, t.data_ptr(), t.numel(), rccl_dtype(t), root,
                              stream()) == 0,
               "ncclBroadcast: ", rccl_last_error((void*)(intptr_t)comm));
+  check_launch("nccl_broadcast");
 }
 
 }  // namespace

@@ -56,7 +56,6 @@ template <bool BAR4, bool PREA, bool PRIO, bool GFIRST, bool PP = false>
 struct V256 {
   static constexpr bool bar4 = BAR4, prea = PREA, prio = PRIO, gfirst = GFIRST, pp = PP;
 };
-using V256PingPong = V256<false, false, true, true, true>;
 
 DEV void sched_barrier_full() {
   __builtin_amdgcn_sched_barrier(0);
@@ -353,22 +352,8 @@ void launch_var(const void* X, const void* W, void* Y, int M, int N, int K, hipS
 
 }  // namespace
 
-int launch_gemm_tn_256_ring(const void* X, const void* W, void* Y, const void* R, int M, int N,
-                            int K, int stages, hipStream_t s);
-
-int launch_gemm_tn_256w4(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                         int stages, hipStream_t s);
-
-int launch_gemm_tn_256w4m16(const void* X, const void* W, void* Y, const void* R, int M, int N,
-                            int K, int stages, hipStream_t s);
-
 int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N, int K, int mode,
                             int pingpong, hipStream_t s);
-
-int launch_gemm_tn_256i(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                        int epi, hipStream_t s);
-int launch_gemm_tn_256a(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                        int epi, hipStream_t s);
 int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         int epi, hipStream_t s);
 int gemm256d_ok(int M, int N, int K);
@@ -380,35 +365,24 @@ int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R,
 int gemm256d_height(int M, int N, int K);
 double gemm256d_waves_bm(int M, int N, int K, int bm);
 
-// tuning entry: variant bits = BAR4 | PREA<<1 | PRIO<<2 | GFIRST<<3
+// tuning / test entry for the kernels the production selector can reach
+// (profiles/gemm_tuning.md keeps the measurements of the retired variants):
+//   8  ping-pong-free base body        25 ping-pong (production fallback body)
+//   30 data-parallel  31 forced 3-way split-K (base body)  32 auto  33 split-K + ping-pong
+//   49 AGPR 256-row tiles  50 AGPR stream-K  51 AGPR 192-row tiles  52 AGPR, height by model
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
                                hipStream_t s) {
   switch (v) {
-#define VCASE(i) case i: launch_var<V256<(i & 1) != 0, (i & 2) != 0, (i & 4) != 0, (i & 8) != 0>>(X, W, Y, M, N, K, s); return 0;
-    VCASE(0) VCASE(1) VCASE(2) VCASE(3) VCASE(4) VCASE(5) VCASE(6) VCASE(7)
-    VCASE(8) VCASE(9) VCASE(10) VCASE(11) VCASE(12) VCASE(13) VCASE(14) VCASE(15)
-#undef VCASE
-    case 16: case 17: case 18:
-      return launch_gemm_tn_256_ring(X, W, Y, nullptr, M, N, K, v - 13, s);
-    case 20: case 21:
-      return launch_gemm_tn_256w4(X, W, Y, nullptr, M, N, K, v - 16, s);
-    case 22: case 23:
-      return launch_gemm_tn_256w4m16(X, W, Y, nullptr, M, N, K, v - 18, s);
-    case 24: launch_var<V256PingPong>(X, W, Y, M, N, K, s); return 0;
-    case 25: launch_var<V256<false, false, false, true, true>>(X, W, Y, M, N, K, s); return 0;
-    case 26: launch_var<V256<false, true, true, true, true>>(X, W, Y, M, N, K, s); return 0;
-    case 30: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 1, 1, s);   // data-parallel
-    case 31: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 0, s);   // stream-K, variant 8 body
-    case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 1, s);   // auto (production)
-    case 33: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 1, s);   // stream-K + ping-pong
-    case 40: return launch_gemm_tn_256i(X, W, Y, nullptr, M, N, K, 0, s);  // one barrier per K-tile
-    case 41: case 42: case 43: case 44: case 45: case 46: case 47: case 48:   // 4 waves, AGPR acc, structure v - 41
-      return launch_gemm_tn_256a(X, W, Y, nullptr, M, N, K, 10 + v - 41, s);
-    case 49: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 256, s);   // 1 wave/SIMD, 128-B DMA rows
-    case 50: return launch_gemm_tn_256sk(X, W, Y, nullptr, M, N, K, 0, 1, s);   // its stream-K form
-    case 51: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 192, s);   // 192-row tiles
-    case 52: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);          // height by cost model
-    case 61: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 9, 256, s);   // direct (unstaged) epilogue
+    case 8: launch_var<V256<false, false, false, true>>(X, W, Y, M, N, K, s); return 0;
+    case 25: launch_var<V256Default>(X, W, Y, M, N, K, s); return 0;
+    case 30: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 1, 1, s);
+    case 31: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 0, s);
+    case 32: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 0, 1, s);
+    case 33: return launch_gemm_tn_256_mode(X, W, Y, M, N, K, 2, 1, s);
+    case 49: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 256, s);
+    case 50: return launch_gemm_tn_256sk(X, W, Y, nullptr, M, N, K, 0, 1, s);
+    case 51: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 192, s);
+    case 52: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);
     default: return 1;
   }
 }
@@ -569,166 +543,7 @@ int launch_gemm_tn_256_mode(const void* X, const void* W, void* Y, int M, int N,
                             int pingpong, hipStream_t s) {
   // mode: 0 auto split, 1 data-parallel, 2 forced 3-way split
   const int splits = mode == 0 ? 0 : mode == 1 ? 1 : 3;
-  if (pingpong) launch_256<0, V256PingPong>(X, W, Y, nullptr, M, N, K, splits, s);
+  if (pingpong) launch_256<0, V256Default>(X, W, Y, nullptr, M, N, K, splits, s);
   else launch_256<0, V256<false, false, false, true>>(X, W, Y, nullptr, M, N, K, splits, s);
   return 0;
-}
-
-// ============================================================================
-// Ring-pipelined 256x256 variant: 32-deep k-steps, an S-slot LDS ring (one
-// slot = A 256x32 + B 256x32 = 32 KiB), prefetch distance S-1 k-steps, ONE
-// barrier per k-step.  At k-step j the loads of k-step j+S-1 go into the slot
-// read at step j-1 (WAR-safe behind that step's barrier); before the barrier
-// ending step j every thread waits until step j+1's pieces landed: it may
-// leave 4 x (#later k-steps issued) LDS-DMA ops in flight (counted vmcnt).
-// Per k-step and wave: 12 ds_read_b128 (4 B + 8 A) and 32 MFMAs.
-namespace {
-
-template <int S, bool RESID>
-__global__ __launch_bounds__(512, 1) void gemm_tn_256_ring(const bf16* __restrict__ X,
-                                                           const bf16* __restrict__ W,
-                                                           bf16* __restrict__ Y,
-                                                           const bf16* __restrict__ R, int M,
-                                                           int N, int K) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[S * 2 * PIECE];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const int nwg = nm * nn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  constexpr int GROUP = 4;
-  const int per_group = GROUP * nn;
-  const int g = wg / per_group;
-  const int first_m = g * GROUP;
-  const int gsz = min(nm - first_m, GROUP);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const bf16* srcA[2];
-  const bf16* srcB[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (2 * wave + j) * 16 + (lane >> 2);
-    const int ch = swz(row, lane & 3);
-    srcA[j] = X + (size_t)min(m0 + row, M - 1) * K + ch * 8;
-    srcB[j] = W + (size_t)min(n0 + row, N - 1) * K + ch * 8;
-  }
-  auto stage = [&](int step) {               // both pieces of k-step `step`
-    const int koff = step * KH;
-    bf16* slot = smem + (step % S) * 2 * PIECE;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(srcA[j] + koff, slot + (2 * wave + j) * 512);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(srcB[j] + koff, slot + PIECE + (2 * wave + j) * 512);
-  };
-
-  const int wm = wave >> 2, wn = wave & 3;
-  const int fr = lane & 15, fq = lane >> 4;
-  f32x4 acc[2][4][4];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[a][b][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int offA[2][4], offB[4];
-#pragma unroll
-  for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int row = wm * 128 + mh * 64 + mt * 16 + fr;
-      offA[mh][mt] = row * KH + swz(row, fq) * 8;
-    }
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int row = wn * 64 + nt * 16 + fr;
-    offB[nt] = row * KH + swz(row, fq) * 8;
-  }
-
-  const int ns = K / KH;
-  // prologue: k-steps 0 .. S-2 in flight, wait for step 0
-#pragma unroll
-  for (int j = 0; j < S - 1; ++j)
-    if (j < ns) stage(j);
-  {
-    const int later = min(S - 1, ns) - 1;      // steps issued after step 0
-    if (later >= S - 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (S - 2)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  barrier();
-
-  for (int j = 0; j < ns; ++j) {
-    if (j + S - 1 < ns) stage(j + S - 1);
-    const bf16* sA = smem + (j % S) * 2 * PIECE;
-    const bf16* sB = sA + PIECE;
-    bf16x8 bfr[4], afr[2][4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bfr[nt] = *reinterpret_cast<const bf16x8*>(sB + offB[nt]);
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        afr[mh][mt] = *reinterpret_cast<const bf16x8*>(sA + offA[mh][mt]);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mh][mt][nt] = mfma16x16x32(bfr[nt], afr[mh][mt], acc[mh][mt][nt]);
-    __builtin_amdgcn_s_setprio(0);
-    // step j+1 must have landed; loads of steps j+2 .. min(j+S-1, ns-1) may stay in flight
-    const int later = min(j + S - 1, ns - 1) - (j + 1);
-    if (later >= S - 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (S - 2)) : "memory");
-    else if (later == 2 && S - 2 > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (later == 1 && S - 2 > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier();
-  }
-
-#pragma unroll
-  for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int m = m0 + wm * 128 + mh * 64 + mt * 16 + fr;
-      if (m >= M) continue;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n = n0 + wn * 64 + nt * 16 + fq * 4;
-        if (n >= N) continue;
-        f32x4 v = acc[mh][mt][nt];
-        if (RESID) {
-          const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += (float)r[q];
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = (bf16)v[q];
-        *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
-      }
-    }
-}
-
-}  // namespace
-
-int launch_gemm_tn_256_ring(const void* X, const void* W, void* Y, const void* R, int M, int N,
-                            int K, int stages, hipStream_t s) {
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const dim3 grid(nm * nn);
-  auto x = (const bf16*)X;
-  auto w = (const bf16*)W;
-  auto y = (bf16*)Y;
-  auto r = (const bf16*)R;
-  switch (stages) {
-    case 3: if (R) gemm_tn_256_ring<3, true><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K);
-            else gemm_tn_256_ring<3, false><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K); return 0;
-    case 4: if (R) gemm_tn_256_ring<4, true><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K);
-            else gemm_tn_256_ring<4, false><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K); return 0;
-    case 5: if (R) gemm_tn_256_ring<5, true><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K);
-            else gemm_tn_256_ring<5, false><<<grid, 512, 0, s>>>(x, w, y, r, M, N, K); return 0;
-    default: return 1;
-  }
 }

@@ -79,16 +79,15 @@ DEV void tile_coords(int t, int nm, int nn, int bm, int& m0, int& n0) {
 constexpr int ops_at(int j, int n, int P) { return ((j + 1) * n) / P - (j * n) / P; }
 constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 
-// EPS = 1: the epilogue goes through LDS (row-contiguous 16-B stores); EPS = 0:
-// every lane stores its 4-column pieces straight from the MFMA layout.
-template <int EPI, int BMT, int EPS = 1>
+// The epilogue goes through LDS (row-contiguous 16-B stores); the direct
+// MFMA-layout store measured 10-15 % slower (profiles/gemm_tuning.md).
+template <int EPI, int BMT>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
                                                        int K, const RopeArgs ra) {
   static_assert(BMT == 256 || BMT == 192, "tile height");
-  static_assert(EPI != 3 || EPS, "the RoPE epilogue is staged");
   constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (8 or 6)
   constexpr int WROWS = BMT / 2;                    // rows per wave (128 or 96)
   constexpr int PIECE_A = BMT * ROWB;               // the X operand of a slot
@@ -246,7 +245,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // and pad MFMA results -> VALU reads (inline asm is not padded)
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
-  if constexpr (EPS) {
+  {
     // ---- staged epilogue.  The direct one below stores 8 B per lane in
     //      32-B row pieces (the MFMA layout: lane = 4 columns of one row); at
     //      one workgroup per CU nothing hides those stores and they cost
@@ -365,43 +364,6 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
         *reinterpret_cast<bf16x8*>(Y + off) = v;
       }
     }
-    return;
-  }
-
-  // ---- direct epilogue: lane holds Y[m][n .. n+3] of each 16x16 tile
-#pragma unroll
-  for (int mt = 0; mt < MTW; ++mt) {
-    const int m = m0 + wm * WROWS + mt * 16 + fr;
-    if (m >= M) continue;
-    if constexpr (EPI == 2) {
-      const int F2 = N >> 1;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int f = ((n0 + wn * 128) >> 1) + p * 16 + fq * 4;
-        if (f >= F2) continue;
-        const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
-        *reinterpret_cast<bf16x4*>(Y + (size_t)m * F2 + f) = o;
-      }
-      continue;
-    }
-#pragma unroll
-    for (int nt_ = 0; nt_ < 8; ++nt_) {
-      const int n = n0 + wn * 128 + nt_ * 16 + fq * 4;
-      if (n >= N) continue;
-      f32x4 v = acc[mt][nt_];
-      if (EPI == 1) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-      *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
-    }
   }
 }
 
@@ -496,7 +458,6 @@ static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R
     }
   }
   switch (epi) {
-    case 9: gemm_tn_256d<0, 256, 0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;   // direct epilogue (A/B)
     case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
     case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
     case 2: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;

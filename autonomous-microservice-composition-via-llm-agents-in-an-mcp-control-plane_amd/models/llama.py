@@ -84,6 +84,10 @@ class LlamaConfig:
         per_layer = H * (hq + 2 * self.kv_heads) * D + hq * D * H + 3 * H * self.ffn + 2 * H
         return self.layers * per_layer + (1 if self.tie_embeddings else 2) * self.vocab_size * H + H
 
+    def kv_bytes_per_token(self, tp: int = 1) -> int:
+        """bf16 K + V bytes one token occupies in the paged cache of one TP rank."""
+        return self.layers * 2 * (self.kv_heads // tp) * self.head_dim * 2
+
 
 def padded_group(group: int) -> int:
     """Smallest divisor of 16 (the MFMA row count attention packs heads into)
@@ -131,9 +135,6 @@ def unpad_q_rows(w: torch.Tensor, cfg: "LlamaConfig") -> torch.Tensor:
 
 def unpad_o_cols(w: torch.Tensor, cfg: "LlamaConfig") -> torch.Tensor:
     return w if not cfg.q_heads_true else unpad_q_rows(w.t().contiguous(), cfg).t().contiguous()
-
-    def kv_bytes_per_token(self, tp: int = 1) -> int:
-        return self.layers * 2 * (self.kv_heads // tp) * self.head_dim * 2
 
 
 _LLAMA31_ROPE = (8.0, 1.0, 4.0, 8192)

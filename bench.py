@@ -4,7 +4,9 @@ Llama-3-8B planner at TP=1 (BASELINE.json ``metric``; configs 2 and 5).
 
 One *step* = one batch of ``--batch`` synthetic intents per GPU planned end to
 end on that GPU's replica (data parallel: one process and one TP=1
-Llama-3-8B per GPU, launched by torchrun for N > 1).  By default the batches
+Llama-3-8B per GPU).  ``--gpus N`` with N > 1 starts the N ranks itself
+(parallel.launch: fresh child processes, one per GPU, before anything touches
+HIP); under torchrun the ranks come from the launcher instead.  By default the batches
 run strictly one after another; ``--overlap F`` admits batch k+1 once at most
 a fraction F of batch k is still decoding (continuous batching, the serving
 engine's normal mode): the GPU no longer idles through a batch's tail of short
@@ -19,7 +21,10 @@ Everything a request needs happens inside the timed step, including the
 prefill of the shared registry prompt (the prefix cache is dropped after each
 batch).  Weights are random-init bf16 of the exact Llama-3-8B architecture
 (no checkpoints offline); intents are synthetic.  The value reported is the
-whole-job aggregate: sum over ranks of plans / max-over-ranks step time.
+whole-job aggregate: sum over ranks of plans / max-over-ranks timed span; the
+p50 is the median over ALL ranks' timed requests of each request's own
+submit -> DAG time (``t_done - t_submit``).  ``--device cpu`` runs the same
+code on CPU ranks over gloo (the launcher's CPU test).
 """
 from __future__ import annotations
 
@@ -30,18 +35,7 @@ import statistics
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-import mcp_amd  # noqa: E402
-from mcp_amd.engine.engine import LLMEngine  # noqa: E402
-from mcp_amd.models.llama import LlamaModel  # noqa: E402
-from mcp_amd.orchestrator import validate_dag  # noqa: E402
-from mcp_amd.planner.local import LocalPlanner  # noqa: E402
-from mcp_amd.planner.prompt import synthetic_intent  # noqa: E402
-from mcp_amd.registry import MemoryRegistry, synthetic_registry  # noqa: E402
 
 METRIC = "plans/sec (whole node) + p50 intent->DAG latency, Llama-3-8B planner TP=1"
 
@@ -62,13 +56,17 @@ def _pin_cpus(local_rank: int, local_world: int):
         os.sched_setaffinity(0, cpus[local_rank * n:(local_rank + 1) * n])
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU) on this node; N > 1 self-launches N processes "
+                         "unless already started by torchrun")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=256, help="concurrent intents per GPU per step")
     ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the same code path on CPU ranks over gloo (launcher tests)")
     ap.add_argument("--services", type=int, default=10)
     ap.add_argument("--min-nodes", type=int, default=5,
                     help="plans have between min and max nodes; min == max fixes the DAG size so "
@@ -80,24 +78,56 @@ def main():
     ap.add_argument("--overlap", type=float, default=0.0,
                     help="submit the next batch once this fraction of the current one is still "
                          "running (0: closed batches)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    from mcp_amd.parallel.launch import check_devices, self_launch
+    rc = self_launch(args.gpus)          # parent of N ranks: never touches the GPU
+    if rc is not None:
+        sys.exit(rc)
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != args.gpus:
+        log(f"[rank {rank}] --gpus {args.gpus} but the launcher started {world} ranks: using {world}")
+    cuda = args.device == "cuda"
+    if cuda:
+        check_devices(local_world, local_rank)
     if world > 1:
-        _pin_cpus(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        _pin_cpus(local_rank, local_world)
+        if cuda:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    from mcp_amd.engine.engine import LLMEngine
+    from mcp_amd.models.llama import LlamaModel
+    from mcp_amd.orchestrator import validate_dag
+    from mcp_amd.planner.local import LocalPlanner
+    from mcp_amd.planner.prompt import synthetic_intent
+    from mcp_amd.registry import MemoryRegistry, synthetic_registry
 
     t0 = time.time()
     model = LlamaModel.random(args.model, dev, seed=args.seed)
-    torch.cuda.synchronize()
+    sync()
     log(f"[rank {rank}] {args.model} random-init on {dev} in {time.time() - t0:.1f}s "
         f"({model.cfg.params() / 1e9:.2f}B params)")
+    kw = {} if cuda else {"num_blocks": 64 + 8 * args.batch}
     engine = LLMEngine(model, max_batch=2 * args.batch + 8, max_step_tokens=args.max_step_tokens,
-                       temperature=0.2, seed=args.seed + rank)
+                       temperature=0.2, seed=args.seed + rank, **kw)
     log(f"[rank {rank}] KV cache: {engine.kv.num_blocks} blocks x 64 tokens "
         f"({engine.kv.data.numel() * 2 / 1e9:.1f} GB)")
     reg = MemoryRegistry(synthetic_registry(args.services, seed=1))
@@ -105,26 +135,28 @@ def main():
     names = [s.name for s in reg.list_services()]
 
     def one_step(step_idx):
+        """One closed batch: submit every intent, run the engine dry."""
         base = (step_idx * world + rank) * args.batch
         intents = [synthetic_intent(base + i) for i in range(args.batch)]
-        seqs_before = engine.stats["tokens"]
+        tok0 = engine.stats["tokens"]
         t = time.perf_counter()
-        dags = planner.plan_many(intents)
-        return dags, time.perf_counter() - t, engine.stats["tokens"] - seqs_before
+        seqs = planner.submit_many(intents)
+        engine.run()
+        return seqs, time.perf_counter() - t, engine.stats["tokens"] - tok0
 
     for w in range(args.warmup):
-        dags, dt, toks = one_step(-1 - w)
+        _, dt, toks = one_step(-1 - w)
         log(f"[rank {rank}] warmup {w}: {dt * 1e3:.0f} ms, {toks} tokens")
-    dags_all = []
+    seqs_all = []
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     tok0, steps0 = engine.stats["tokens"], engine.stats["steps"]
     if args.overlap <= 0:
         for s in range(args.steps):
-            dags, dt, toks = one_step(s)
-            dags_all += dags
+            seqs, dt, toks = one_step(s)
+            seqs_all += seqs
             log(f"[rank {rank}] step {s}: {dt * 1e3:.0f} ms, {toks} tokens")
     else:
         # continuous batching: drive the engine here; admit batch k+1 once at
@@ -153,46 +185,37 @@ def main():
                 if any(not q.pending for q in engine.running):
                     raise RuntimeError("engine stalled with sequences that have no pending tokens")
         for k, b in enumerate(batches):
-            for q in b:
-                if q.error:
-                    raise RuntimeError(q.error)
-            dags_all += [q.result for q in b]
+            seqs_all += b
             log(f"[rank {rank}] batch {k}: done {max(q.t_done for q in b) - t_sub[k]:.3f} s after submit")
     tokens = engine.stats["tokens"] - tok0
     log(f"[rank {rank}] {engine.stats['steps'] - steps0} engine steps, {tokens} tokens")
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     st = engine.stats
     log(f"[rank {rank}] engine totals: " + ", ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}"
                                                   for k, v in st.items()))
-    # per-request latencies were recorded by the engine's sequences via METRICS
-    from mcp_amd.utils.metrics import METRICS
-    w = METRICS.windows["plan_latency_s"]
-    lats = list(w.samples)[-args.steps * args.batch:]
-    p50_local = statistics.median(lats) if lats else float("nan")
     # correctness after timing: every plan is a valid T2 DAG over the registry
-    for d in dags_all:
-        validate_dag(d, names)
-    ms_per_step = elapsed / args.steps * 1e3
-    plans_local = args.steps * args.batch
+    for q in seqs_all:
+        if q.error:
+            raise RuntimeError(q.error)
+        validate_dag(q.result, names)
+    # each timed request's own intent -> DAG latency (not a bounded metrics window)
+    lats = [q.t_done - q.t_submit for q in seqs_all]
+    mine = {"elapsed": elapsed, "plans": len(seqs_all), "tokens": tokens, "lats": lats}
     if world > 1:
-        t = torch.tensor([ms_per_step, p50_local, float(plans_local), float(tokens)], device=dev,
-                         dtype=torch.float64)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        ms_per_step = float(mx[0])
-        p50 = float(mx[1])
-        plans_total = float(sm[2])
-        tokens_total = float(sm[3])
+        every = [None] * world
+        dist.all_gather_object(every, mine)
     else:
-        p50 = p50_local
-        plans_total = float(plans_local)
-        tokens_total = float(tokens)
-    value = plans_total / (ms_per_step * args.steps / 1e3)
+        every = [mine]
+    elapsed_max = max(e["elapsed"] for e in every)
+    plans_total = sum(e["plans"] for e in every)
+    tokens_total = sum(e["tokens"] for e in every)
+    all_lats = [x for e in every for x in e["lats"]]
+    p50 = statistics.median(all_lats) if all_lats else float("nan")
+    ms_per_step = elapsed_max / args.steps * 1e3
+    value = plans_total / elapsed_max
     if rank == 0:
         print(json.dumps({
             "metric": METRIC, "value": round(value, 3), "unit": "plans/s",
@@ -201,12 +224,15 @@ def main():
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic intents, random-init weights",
             "p50_latency_ms": round(p50 * 1e3, 2),
-            "tokens_per_s": round(tokens_total / (ms_per_step * args.steps / 1e3), 1),
+            "p99_latency_ms": round(statistics.quantiles(all_lats, n=100)[98] * 1e3, 2)
+            if len(all_lats) >= 2 else None,
+            "tokens_per_s": round(tokens_total / elapsed_max, 1),
             "batching": "continuous" if args.overlap > 0 else "closed",
+            "device": args.device,
             "config": {"model": args.model, "global_batch": args.batch * world,
                        "seq_len": None, "parallelism": f"dp{world}", "tp": 1,
                        "services": args.services, "nodes_per_plan": [args.min_nodes, args.max_nodes],
-                       "tokens_per_plan": round(tokens_total / plans_total, 1),
+                       "tokens_per_plan": round(tokens_total / max(1, plans_total), 1),
                        "temperature": 0.2},
         }), flush=True)
     if world > 1:

@@ -9,8 +9,10 @@
   the continuously-batching engine (requests join and leave the running batch
   every step; small steps replay captured hipGraphs).  Reports achieved
   plans/s, p50 / p99 intent -> DAG latency (arrival to DAG) and batch stats.
-  For N GPUs run it under torchrun: every rank serves ``--qps`` on its own
-  replica (data parallel), the JSON line aggregates the node.
+  ``--gpus N`` starts N ranks itself (parallel.launch; or run it under
+  torchrun): every rank serves ``--qps`` on its own replica (data parallel),
+  the JSON line aggregates the node (plans/s summed, p50 / p99 over every
+  rank's requests).
 
 Synthetic intents, random-init weights (no checkpoints offline).
 """
@@ -100,11 +102,17 @@ def main():
     ap.add_argument("--max-nodes", type=int, default=5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); N > 1 self-launches")
     args = ap.parse_args()
+    from mcp_amd.parallel.launch import check_devices, self_launch
+    rc = self_launch(args.gpus)
+    if rc is not None:
+        sys.exit(rc)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    check_devices(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))), local_rank)
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -137,16 +145,16 @@ def main():
         lat, dags, elapsed, n, bs = run_qps(planner, engine, args.qps, args.duration, args.seed, rank)
         for d in dags:
             validate_dag(d, names)
-        v = torch.tensor([len(lat) / elapsed, statistics.median(lat), pct(lat, 99),
-                          float(np.mean(bs)) if bs else 0.0], dtype=torch.float64, device=dev)
+        mine = {"rate": len(lat) / elapsed, "lat": lat, "bs": float(np.mean(bs)) if bs else 0.0}
+        every = [None] * world
         if world > 1:
-            tot = v.clone()
-            dist.all_reduce(tot)
-            mx = v.clone()
-            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            plans_s, p50, p99, mean_b = float(tot[0]), float(mx[1]), float(mx[2]), float(tot[3]) / world
+            dist.all_gather_object(every, mine)
         else:
-            plans_s, p50, p99, mean_b = (float(x) for x in v)
+            every = [mine]
+        all_lat = [x for e in every for x in e["lat"]]
+        plans_s = sum(e["rate"] for e in every)
+        p50, p99 = statistics.median(all_lat), pct(all_lat, 99)
+        mean_b = sum(e["bs"] for e in every) / world
         out.update(metric="plans/sec at fixed QPS (config 5)", offered_qps=args.qps * world,
                    value=round(plans_s, 2), unit="plans/s", p50_latency_ms=round(p50 * 1e3, 1),
                    p99_latency_ms=round(p99 * 1e3, 1), mean_running_batch=round(mean_b, 1),

@@ -2,8 +2,9 @@
 """BASELINE config 4: Llama-3-70B planner at TP=8 over xGMI, 50-service
 registry, execution with retries + ordered fallbacks.
 
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
-        --master-addr 127.0.0.1 --master-port 29511 bench_tp.py --model llama3-70b
+    python bench_tp.py --gpus 8 --model llama3-70b
+
+(``--gpus N`` starts the N ranks itself, parallel.launch; torchrun works too.)
 
 One process per GPU.  Rank 0 is the TP driver (scheduler, grammar, sampling);
 ranks 1..7 mirror the sharded forward from broadcast step descriptors
@@ -47,7 +48,14 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--seq-parallel", action="store_true",
                     help="Megatron sequence parallelism (reduce-scatter / all-gather) for TP > 1")
+    ap.add_argument("--gpus", type=int, default=1, help="TP degree = ranks (one per GPU); N > 1 self-launches")
     args = ap.parse_args()
+    from mcp_amd.parallel.launch import check_devices, self_launch
+    rc = self_launch(args.gpus)
+    if rc is not None:
+        sys.exit(rc)
+    check_devices(int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))),
+                  int(os.environ.get("LOCAL_RANK", "0")))
 
     from mcp_amd.engine.engine import LLMEngine
     from mcp_amd.engine.kv_cache import KVCache
@@ -99,7 +107,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t
     eng.shutdown_workers()
-    lats = list(METRICS.windows["plan_latency_s"].samples)[-len(dags):]
+    lats = list(METRICS.windows["plan_latency_s"].samples)[-min(len(dags), 4096):]
     for d in dags:
         validate_dag(d, names)
 

@@ -8,7 +8,7 @@ L = ops.lib()
 dev = 'cuda'
 shapes = [(4096, 6144, 4096), (4096, 4096, 4096), (4096, 28672, 4096), (4096, 4096, 14336),
           (3584, 6144, 4096), (1792, 6144, 4096)]
-variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [8, 24, 30, 31, 32, 33]
+variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [8, 25, 30, 31, 32, 33]
 if len(sys.argv) > 2:                      # "M,N,K;M,N,K;..."
     shapes = [tuple(int(x) for x in sh.split(",")) for sh in sys.argv[2].split(";")]
 rounds = 3
