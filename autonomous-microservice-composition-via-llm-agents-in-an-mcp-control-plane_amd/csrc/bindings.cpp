@@ -409,6 +409,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_splitk_init", [](int64_t bytes) { return gemm_splitk_init((size_t)bytes); },
         "allocate the split-K fp32 workspace (call outside graph capture)");
   m.def("gemm128_splits", &gemm128_splits);
+  m.def("gemm_stream_force_splits", &gemm_stream_force_splits, "split count of the K2 stream kernel: 0 auto");
+  m.def("gemm_stream_splits", &gemm_stream_splits);
+  m.def("gemm_splitk_force", &gemm_splitk_force, "split-K count of the 128^2 path: -1 auto, <= 1 off, S forced");
   m.def("gemm_silu", &gemm_silu);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);

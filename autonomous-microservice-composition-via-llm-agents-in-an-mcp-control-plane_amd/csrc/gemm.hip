@@ -271,7 +271,29 @@ int gemm_select(int M, int N, int K) {
 namespace {
 float* g_splitk_ws = nullptr;
 size_t g_splitk_ws_bytes = 0;
+int* g_splitk_tickets = nullptr;       // per-tile arrival tickets (gemm_stream.hip)
+constexpr size_t MAX_SPLIT_TILES = 1 << 16;
+int g_split_force = -1;                // gemm_splitk_force (tests, tuning)
 }  // namespace
+
+void gemm_splitk_force(int S) { g_split_force = S; }
+
+bool gemm_splitk_workspace(float** ws, int** tickets, size_t bytes, size_t tiles) {
+  if (!g_splitk_ws || !g_splitk_tickets || bytes > g_splitk_ws_bytes || tiles > MAX_SPLIT_TILES)
+    return false;
+  *ws = g_splitk_ws;
+  *tickets = g_splitk_tickets;
+  return true;
+}
+
+int gemm_stream_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("MCP_GEMM_STREAM");
+    on = e ? atoi(e) : 1;
+  }
+  return on;
+}
 
 int gemm256sk_prealloc();
 
@@ -279,6 +301,14 @@ int gemm_splitk_init(size_t bytes) {
   // the stream-K tail's slabs / counters too (gemm256sk.hip): both are
   // allocated here, at library load, never inside a hipGraph capture
   if (gemm256sk_prealloc() != 0) return 2;
+  if (!g_splitk_tickets) {
+    if (hipMalloc(&g_splitk_tickets, MAX_SPLIT_TILES * sizeof(int)) != hipSuccess) {
+      g_splitk_tickets = nullptr;
+      return 1;
+    }
+    if (hipMemset(g_splitk_tickets, 0, MAX_SPLIT_TILES * sizeof(int)) != hipSuccess) return 1;
+    (void)hipDeviceSynchronize();
+  }
   if (g_splitk_ws_bytes >= bytes) return 0;
   if (g_splitk_ws) (void)hipFree(g_splitk_ws);
   g_splitk_ws = nullptr;
@@ -301,6 +331,11 @@ int gemm128_splits(int M, int N, int K) {
     enabled = e ? atoi(e) : 1;
   }
   if (!enabled || !g_splitk_ws) return 1;
+  if (g_split_force >= 0) {
+    const int S = g_split_force, nkt = K / BK;
+    return (S > 1 && nkt % S == 0 && nkt / S >= 4 &&
+            (size_t)S * M * N * sizeof(float) <= g_splitk_ws_bytes) ? S : 1;
+  }
   const int G = gemm256_num_cus();
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (enabled > 1) {                                 // MCP_GEMM_SPLITK128=S forces S (tuning)
@@ -373,6 +408,9 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
 
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s) {
+  if (gemm_stream_enabled() && gemm_stream_pick(M, N, K, R ? 1 : 0) &&
+      launch_gemm_stream(X, W, Y, R, M, N, K, R ? 1 : 0, RopeArgs{}, s) == 0)
+    return;
   // M <= 128: split-K over the 128^2 kernel beats the weight-streaming skinny
   // kernel wherever it applies (tools/bench_small_m.py: 1.5-4x at N, K >= 4096)
   if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
@@ -387,6 +425,7 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                          int algo, hipStream_t s) {
   if (algo < 0) launch_gemm_tn(X, W, Y, R, M, N, K, s);
+  else if (algo == 3 && launch_gemm_stream(X, W, Y, R, M, N, K, R ? 1 : 0, RopeArgs{}, s) == 0) return;
   else if (algo == 2 && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;
   else if (algo == 1) launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
   else launch_gemm_tn_128(X, W, Y, R, M, N, K, s);
@@ -397,6 +436,9 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
                              hipStream_t s);
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (N % 64) return 1;
+  if (gemm_stream_enabled() && gemm_stream_pick(M, N, K, 2) &&
+      launch_gemm_stream(X, W, Y, nullptr, M, N, K, 2, RopeArgs{}, s) == 0)
+    return 0;
   if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
       launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0)
     return 0;

@@ -476,6 +476,9 @@ int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R,
 void launch_qkv_rope(const void* X, const void* W, void* qkv, int M, int N, int K, int D,
                      const RopeArgs& ra, hipStream_t s) {
   static const int fused = getenv("MCP_QKV_ROPE_FUSED") ? atoi(getenv("MCP_QKV_ROPE_FUSED")) : 1;
+  if (fused && gemm_stream_enabled() && gemm_stream_pick(M, N, K, 3) &&
+      launch_gemm_stream(X, W, nullptr, nullptr, M, N, K, 3, ra, s) == 0)
+    return;
   if (fused && D == 128 && N == (ra.Hq + 2 * ra.Hkv) * 128 && M > SKINNY_MAX_M &&
       gemm_select(M, N, K) == 1 && gemm256d_ok(M, N, K) == 0 &&
       launch_256d_impl(X, W, nullptr, nullptr, M, N, K, 3, 0, ra, s) == 0)

@@ -39,7 +39,24 @@ int skinny_ok(int M, int N, int K, int epi);
 int launch_gemm_skinny(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                        int epi, hipStream_t s);
 
+// gemm_stream.hip (K2 proper): weight streaming for M <= 128, register-ring
+// prefetch, fused split-K reduction; epi 0 plain, 1 +R, 2 SwiGLU, 3 QKV+RoPE+KV
+#define GEMM_STREAM_MAX_M 128
+int gemm_stream_ok(int M, int N, int K, int epi, int D, int Hq, int Hkv);
+int gemm_stream_splits(int M, int N, int K, int epi);
+void gemm_stream_force_splits(int S);   // 0 = auto
+int launch_gemm_stream(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                       int epi, const RopeArgs& ra, hipStream_t s);
+int gemm_stream_enabled();
+// production routing: the measured (M, N, K, epi) range where it beats the
+// 128^2 split-K path (profiles/gemm_stream_sweep.md)
+bool gemm_stream_pick(int M, int N, int K, int epi);
+
 // gemm.hip
+int gemm256_num_cus();
+// the split-K workspace (fp32 partial tiles) and per-tile tickets, allocated at
+// library load; false when a launch would not fit
+bool gemm_splitk_workspace(float** ws, int** tickets, size_t bytes, size_t tiles);
 int gemm_tn_check(int M, int N, int K);
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s);
@@ -50,6 +67,7 @@ int gemm_select(int M, int N, int K);
 int gemm_plan_lookup(int M, int N, int K);
 int gemm_splitk_init(size_t bytes);
 int gemm128_splits(int M, int N, int K);
+void gemm_splitk_force(int S);   // -1 auto, 0/1 off, S > 1 forced where admissible
 void gemm_plan_set(int N, int K, const int* codes, int n);
 void gemm_plan_clear();
 int gemm256d_ok(int M, int N, int K);

@@ -189,6 +189,11 @@ class LLMEngine:
                on_done: Optional[Callable] = None) -> Sequence:
         """Queue one grammar-constrained generation.  ``prefix_tokens`` is the
         shareable leading part of the prompt (registry section)."""
+        total = len(prefix_tokens or ()) + len(prompt_tokens)
+        max_pos = getattr(self.model.cfg, "max_pos", None)
+        if max_pos is not None and total >= max_pos:
+            raise ValueError(f"prompt of {total} tokens does not fit the model's "
+                             f"{max_pos}-token context")
         prefix = self.get_prefix(prefix_tokens) if prefix_tokens else None
         if prefix is not None:
             self.alloc.incref(prefix.blocks)
@@ -201,6 +206,39 @@ class LLMEngine:
             self.last_progress = time.perf_counter()
         self.waiting.append(seq)
         return seq
+
+    def abort_all(self, reason: str = "aborted") -> int:
+        """Fail every queued and running request (their blocks go back to the
+        allocator) and forget the prefix cache: the planner's recovery after a
+        stalled step.  Launches still in flight are waited for first.  Returns
+        the number of requests failed."""
+        for L in self.inflight.values():
+            if L.event is not None:
+                L.event.synchronize()
+        self.inflight.clear()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        n = 0
+        now = time.perf_counter()
+        for seq in self.running + self.waiting:
+            if seq.done:
+                continue
+            if seq.materialized or seq.is_prefix_job:
+                self.alloc.free(seq.blocks)
+            else:                                   # still holds its prefix reference
+                self.alloc.free(seq.prefix.blocks)
+            seq.blocks = []
+            seq.done, seq.t_done = True, now
+            if seq.is_prefix_job:
+                continue
+            seq.error = reason
+            n += 1
+            if seq.on_done is not None:
+                seq.on_done(seq)
+        self.running, self.waiting = [], []
+        self.drop_prefixes()
+        self.last_progress = time.perf_counter()
+        return n
 
     def has_work(self) -> bool:
         return bool(self.running or self.waiting or self.inflight)

@@ -42,7 +42,7 @@ def lib():
         if torch.cuda.is_available() and hasattr(mod, "gemm_splitk_init"):
             # fp32 split-K partials of small-M projections (gemm.hip); allocated
             # here, never inside a hipGraph capture
-            mod.gemm_splitk_init(int(os.environ.get("MCP_GEMM_SPLITK_MB", "64")) << 20)
+            mod.gemm_splitk_init(int(os.environ.get("MCP_GEMM_SPLITK_MB", "256")) << 20)
         _LIB = mod
     return _LIB
 

@@ -1,28 +1,40 @@
 """Data-parallel planner replicas behind one API (SURVEY §2.3 "request-level DP",
-§5.3 "the router drains a failed DP replica").
+§5.3 "the router drains a failed DP replica" / "restart the replica").
 
 The reference is a single process with module singletons
-(control_plane.py:135-138).  Here ``ReplicaRouter`` spawns one engine process
-per GPU (``replicas`` of them, each a TP=1 Llama-3 replica pinned to its own
-device, or a TP group launched separately), and implements the planner
-interface:
+(control_plane.py:135-138) that re-reads the Redis registry on every /plan
+(control_plane.py:58 via :30-35).  Here ``ReplicaRouter`` spawns one engine
+process per GPU (``replicas`` of them, each a TP=1 Llama-3 replica pinned to
+its own device) and implements the planner interface:
 
 * dispatch: least in-flight requests first (ties -> lowest index);
-* results come back on one queue drained by a router thread that resolves the
-  asyncio futures;
-* failure handling: a replica whose process exits is marked dead and every
-  request it had in flight is re-dispatched to a live replica; a request that
-  exceeds ``request_timeout`` fails with TimeoutError (HTTP 500 at the API).
+* registry freshness: a replica plans against the registry as it is when the
+  request is dispatched.  With a Redis registry every replica opens its own
+  ``RedisRegistry`` and re-reads it per request, exactly like the reference;
+  with the in-memory registry the router compares ``registry.version`` at
+  every dispatch and, when it changed, sends the new records down every
+  replica's queue ahead of the request (queues are FIFO, so no request sees
+  an older registry than the one current at its dispatch);
+* retrieval-bounded prompts: every replica owns a ``SchemaIndex`` on its
+  device (HBM-resident top-k cosine, the role of control_plane.py:51-55), so a
+  registry larger than ``retrieval_threshold`` contributes only the ``topk``
+  most similar services to the prompt;
+* failure handling: a replica whose process exits, or that stops sending
+  heartbeats for ``watchdog_s`` while it has requests in flight (a hung GPU
+  step), is killed, every request it had in flight is re-dispatched to a live
+  replica, and a fresh replica process is spawned in its place (at most
+  ``max_respawns`` times per slot); a request that exceeds
+  ``request_timeout`` fails with TimeoutError (HTTP 500 at the API).
 
-Queues carry only intent strings and DAG dicts produced by this process
-tree.
+Queues carry only intent strings, registry records and DAG dicts produced by
+this process tree.
 """
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import itertools
 import multiprocessing as mp
-import os
 import queue
 import threading
 import time
@@ -31,36 +43,66 @@ from typing import Dict, List, Optional
 from ..planner.base import Planner
 
 
-def _replica_main(idx: int, device: str, model: str, registry_records: list, inq, outq,
-                  max_batch: int, max_nodes: int, seed: int, num_blocks: Optional[int]):
+@dataclasses.dataclass
+class ReplicaConfig:
+    model: str
+    max_batch: int = 256
+    max_nodes: int = 6
+    seed: int = 0
+    num_blocks: Optional[int] = None
+    max_step_tokens: int = 8192
+    temperature: float = 0.2
+    retrieval_threshold: int = 48
+    topk: int = 32
+    embed_dim: int = 1024
+    redis_url: Optional[str] = None     # replicas read Redis themselves when set
+    services_prefix: Optional[str] = None
+    heartbeat_s: float = 0.5
+
+
+def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, version: int,
+                  inq, outq):
     """Replica process: owns one engine; plans batches of whatever is queued."""
     import torch
     from ..engine.engine import LLMEngine
     from ..models.llama import LlamaModel
-    from ..registry import MemoryRegistry
-    from .. planner.local import LocalPlanner
+    from ..planner.local import LocalPlanner
+    from ..registry import MemoryRegistry, RedisRegistry
+    from ..retrieval.store import SchemaIndex
     if device.startswith("cuda"):
         torch.cuda.set_device(torch.device(device))
-    m = LlamaModel.random(model, device, seed=seed)
-    kw = {"num_blocks": num_blocks} if num_blocks else {}
-    eng = LLMEngine(m, max_batch=max_batch, temperature=0.2, seed=seed + idx, **kw)
-    planner = LocalPlanner(eng, MemoryRegistry(registry_records), max_nodes=max_nodes)
+    m = LlamaModel.random(cfg.model, device, seed=cfg.seed)
+    kw = {"num_blocks": cfg.num_blocks} if cfg.num_blocks else {}
+    eng = LLMEngine(m, max_batch=cfg.max_batch, max_step_tokens=cfg.max_step_tokens,
+                    temperature=cfg.temperature, seed=cfg.seed + idx, **kw)
+    if cfg.redis_url:
+        registry = RedisRegistry(cfg.redis_url, **({"prefix": cfg.services_prefix}
+                                                   if cfg.services_prefix else {}))
+    else:
+        registry = _VersionedMemoryRegistry(records, version)
+    retriever = SchemaIndex(registry, dim=cfg.embed_dim, device=device)
+    planner = LocalPlanner(eng, registry, max_nodes=cfg.max_nodes, retriever=retriever,
+                           retrieval_threshold=cfg.retrieval_threshold, topk=cfg.topk)
     outq.put(("ready", idx, None))
     pending = {}
+    last_hb = time.monotonic()
     while True:
         try:
-            item = inq.get(timeout=0.05 if eng.has_work() else 1.0)
+            item = inq.get(timeout=0.01 if eng.has_work() else cfg.heartbeat_s)
         except queue.Empty:
             item = None
         while item is not None:
             if item == "stop":
                 return
-            rid, intent = item
-            try:
-                dec, ptoks, stoks = planner.prepare(intent)
-                pending[rid] = eng.submit(dec, stoks, prefix_tokens=ptoks)
-            except Exception as e:  # noqa: BLE001
-                outq.put(("err", rid, repr(e)))
+            if item[0] == "registry":                  # ("registry", version, records)
+                registry.replace(item[2], item[1])
+            else:
+                rid, intent = item
+                try:
+                    dec, ptoks, stoks = planner.prepare(intent)
+                    pending[rid] = eng.submit(dec, stoks, prefix_tokens=ptoks)
+                except Exception as e:  # noqa: BLE001
+                    outq.put(("err", rid, repr(e)))
             try:
                 item = inq.get_nowait()
             except queue.Empty:
@@ -70,47 +112,101 @@ def _replica_main(idx: int, device: str, model: str, registry_records: list, inq
         for rid in [r for r, s in pending.items() if s.done]:
             s = pending.pop(rid)
             outq.put(("err", rid, s.error) if s.error else ("ok", rid, s.result))
+        now = time.monotonic()
+        if now - last_hb >= cfg.heartbeat_s:          # liveness for the router's watchdog
+            outq.put(("hb", idx, None))
+            last_hb = now
+
+
+class _VersionedMemoryRegistry:
+    """The replica-side copy of an in-memory registry: the router's records
+    and version, replaced wholesale when the router pushes a newer version."""
+
+    def __init__(self, records, version: int):
+        from ..registry import MemoryRegistry
+        self._mk = MemoryRegistry
+        self.replace(records, version)
+
+    def replace(self, records, version: int):
+        self._reg = self._mk(records)
+        self._version = version
+
+    @property
+    def version(self) -> int:
+        return self._version
+
+    def list_services(self):
+        return self._reg.list_services()
+
+    def get(self, name):
+        return self._reg.get(name)
 
 
 class ReplicaRouter(Planner):
     def __init__(self, devices: List[str], model: str, registry, max_batch: int = 256,
                  max_nodes: int = 6, seed: int = 0, num_blocks: Optional[int] = None,
-                 request_timeout: float = 120.0, start_timeout: float = 600.0):
+                 request_timeout: float = 120.0, start_timeout: float = 600.0,
+                 watchdog_s: float = 60.0, max_respawns: int = 3,
+                 config: Optional[ReplicaConfig] = None):
         self.registry = registry
         self.request_timeout = request_timeout
-        ctx = mp.get_context("spawn")
-        self._outq = ctx.Queue()
-        self._inqs = []
-        self._procs = []
-        recs = [dict(s) for s in registry.list_services()]
-        for i, dev in enumerate(devices):
-            q = ctx.Queue()
-            p = ctx.Process(target=_replica_main, daemon=True,
-                            args=(i, dev, model, recs, q, self._outq, max_batch, max_nodes, seed,
-                                  num_blocks))
-            p.start()
-            self._inqs.append(q)
-            self._procs.append(p)
-        self.alive = [True] * len(devices)
-        self.inflight: Dict[int, Dict[int, str]] = {i: {} for i in range(len(devices))}
+        self.start_timeout = start_timeout
+        self.watchdog_s = watchdog_s
+        self.max_respawns = max_respawns
+        self.devices = list(devices)
+        cfg = config or ReplicaConfig(model=model, max_batch=max_batch, max_nodes=max_nodes,
+                                      seed=seed, num_blocks=num_blocks)
+        from ..registry import RedisRegistry
+        if isinstance(registry, RedisRegistry) and not cfg.redis_url:
+            cfg = dataclasses.replace(cfg, redis_url=registry.client.url, services_prefix=registry.prefix)
+        self.cfg = cfg
+        self._ctx = mp.get_context("spawn")
+        self._outq = self._ctx.Queue()
+        n = len(devices)
+        self._inqs: List = [None] * n
+        self._procs: List = [None] * n
+        self.alive = [False] * n
+        self.respawns = [0] * n
+        self._last_msg = [time.monotonic()] * n
+        self.inflight: Dict[int, Dict[int, str]] = {i: {} for i in range(n)}
         self._futs: Dict[int, tuple] = {}
         self._ids = itertools.count()
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()
         self._stop = threading.Event()
-        ready, t0 = set(), time.time()
-        while len(ready) < len(devices):
+        self._pushed_version = None
+        for i in range(n):
+            self._spawn(i)
+        t0 = time.time()
+        while not all(self.alive):
             if time.time() - t0 > start_timeout:
                 raise TimeoutError("replicas did not start")
             try:
                 kind, idx, _ = self._outq.get(timeout=1.0)
                 if kind == "ready":
-                    ready.add(idx)
+                    self.alive[idx] = True
+                    self._last_msg[idx] = time.monotonic()
             except queue.Empty:
                 for i, p in enumerate(self._procs):
                     if not p.is_alive():
                         raise RuntimeError(f"replica {i} died during start-up")
         self._thread = threading.Thread(target=self._pump, daemon=True, name="mcp-router")
         self._thread.start()
+
+    # ------------------------------------------------------------ replicas
+    def _snapshot(self):
+        """(version, records) of the in-memory registry (Redis replicas read it themselves)."""
+        if self.cfg.redis_url:
+            return 0, []
+        return self.registry.version, [dict(s) for s in self.registry.list_services()]
+
+    def _spawn(self, i: int):
+        version, recs = self._snapshot()
+        q = self._ctx.Queue()
+        p = self._ctx.Process(target=_replica_main, daemon=True,
+                              args=(i, self.devices[i], self.cfg, recs, version, q, self._outq))
+        p.start()
+        self._inqs[i], self._procs[i] = q, p
+        self._last_msg[i] = time.monotonic()
 
     # -------------------------------------------------------------- routing
     def _pick(self) -> int:
@@ -119,11 +215,25 @@ class ReplicaRouter(Planner):
             raise RuntimeError("no live planner replicas")
         return min(live, key=lambda i: (len(self.inflight[i]), i))
 
+    def _sync_registry(self):
+        """Push the in-memory registry to every replica when its version moved."""
+        if self.cfg.redis_url:
+            return
+        v = self.registry.version
+        if v == self._pushed_version:
+            return
+        _, recs = self._snapshot()
+        for i, q in enumerate(self._inqs):
+            if q is not None:
+                q.put(("registry", v, recs))
+        self._pushed_version = v
+
     def _dispatch(self, rid: int, intent: str):
         with self._lock:
+            self._sync_registry()
             i = self._pick()
             self.inflight[i][rid] = intent
-        self._inqs[i].put((rid, intent))
+            self._inqs[i].put((rid, intent))
 
     def _pump(self):
         while not self._stop.is_set():
@@ -131,10 +241,17 @@ class ReplicaRouter(Planner):
                 kind, rid, val = self._outq.get(timeout=0.2)
             except queue.Empty:
                 kind = None
-            if kind in ("ok", "err"):
+            if kind in ("ready", "hb"):
+                idx = rid
                 with self._lock:
-                    for d in self.inflight.values():
-                        d.pop(rid, None)
+                    self._last_msg[idx] = time.monotonic()
+                    if kind == "ready" and self._procs[idx].is_alive():
+                        self.alive[idx] = True
+            elif kind in ("ok", "err"):
+                with self._lock:
+                    for i, d in self.inflight.items():
+                        if d.pop(rid, None) is not None:
+                            self._last_msg[i] = time.monotonic()
                     entry = self._futs.pop(rid, None)
                 if entry is not None:
                     loop, fut = entry
@@ -145,19 +262,37 @@ class ReplicaRouter(Planner):
             self._check_health()
 
     def _check_health(self):
+        now = time.monotonic()
         for i, p in enumerate(self._procs):
-            if self.alive[i] and not p.is_alive():
-                with self._lock:
-                    self.alive[i] = False
-                    orphans = list(self.inflight[i].items())
-                    self.inflight[i].clear()
-                for rid, intent in orphans:       # drain: re-dispatch to live replicas
-                    try:
-                        self._dispatch(rid, intent)
-                    except RuntimeError as e:
-                        entry = self._futs.pop(rid, None)
-                        if entry:
-                            entry[0].call_soon_threadsafe(_resolve, entry[1], None, e)
+            if p is None:
+                continue
+            dead = not p.is_alive()
+            hung = (not dead and self.alive[i] and self.inflight[i]
+                    and now - self._last_msg[i] > self.watchdog_s)
+            if not dead and not hung:
+                continue
+            if hung:                                  # stalled GPU step: replace the process
+                p.kill()
+                p.join(timeout=10)
+            was_live = self.alive[i]
+            with self._lock:
+                self.alive[i] = False
+                orphans = list(self.inflight[i].items())
+                self.inflight[i].clear()
+            if not was_live and not orphans and self._procs[i] is not p:
+                continue
+            for rid, intent in orphans:       # drain: re-dispatch to live replicas
+                try:
+                    self._dispatch(rid, intent)
+                except RuntimeError as e:
+                    entry = self._futs.pop(rid, None)
+                    if entry:
+                        entry[0].call_soon_threadsafe(_resolve, entry[1], None, e)
+            if self.respawns[i] < self.max_respawns and not self._stop.is_set():
+                self.respawns[i] += 1
+                self._spawn(i)                # 'ready' marks it live again
+            else:
+                self._procs[i] = None
 
     async def plan(self, intent: str) -> dict:
         loop = asyncio.get_running_loop()
@@ -176,9 +311,11 @@ class ReplicaRouter(Planner):
     async def aclose(self):
         self._stop.set()
         for q, p in zip(self._inqs, self._procs):
-            if p.is_alive():
+            if p is not None and p.is_alive():
                 q.put("stop")
         for p in self._procs:
+            if p is None:
+                continue
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()

@@ -35,7 +35,13 @@ from .tokenizer import get_tokenizer
 
 class EngineStalled(RuntimeError):
     """The engine made no progress for ``watchdog_s`` with requests pending
-    (e.g. a hung GPU step); the API answers 503 and the router drains the replica."""
+    (e.g. a hung GPU step); the API answers 503 and the router drains the replica.
+
+    Recovery: the watchdog fails the pending requests at once; when the stuck
+    step returns, the scheduler thread aborts everything the engine still
+    holds (``LLMEngine.abort_all``) and clears ``stalled``, so new requests are
+    served again.  A step that never returns needs a process restart (the DP
+    router respawns its replicas; a lone server reports 503 on /healthz)."""
 
 
 class LocalPlanner(Planner):
@@ -219,6 +225,12 @@ class LocalPlanner(Planner):
             if eng.has_work():
                 with self._lock:
                     eng.step()
+            if self.stalled:                  # the stuck step returned: start over
+                with self._lock:
+                    n = eng.abort_all("planner engine stalled; request aborted")
+                METRICS.inc("engine_recoveries")
+                METRICS.inc("aborted_requests", n)
+                self.stalled = False
 
     async def plan(self, intent: str) -> dict:
         if self.stalled:

@@ -402,8 +402,83 @@ def test_gemm_splitk128(M, N, K):
     assert rel_err(y, e) < 2e-2
 
 
+@pytest.mark.parametrize("S", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("M", [1, 9, 16, 33, 64, 100, 128])
+def test_gemm_stream(M, S):
+    """K2 weight-streaming kernel (gemm_stream.hip, algo 3): register-ring
+    prefetch, 4-wave LDS reduction, fused split-K (S forced; 0 = auto) -
+    plain, residual in place, SwiGLU, against fp32; repeated launches reuse
+    the split tickets."""
+    torch.manual_seed(12)
+    L = ops.lib()
+    try:
+        L.gemm_stream_force_splits(S)
+        for (N, K) in [(1024, 4096), (2048, 1536)]:
+            X = torch.randn(M, K, device=DEV).bfloat16()
+            W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+            e = ref.gemm(X, W)
+            for _ in range(2):
+                assert rel_err(ops.gemm(X, W, algo=3), e) < 1e-2
+            assert rel_err(ops.gemm(X, W), e) < 1e-2       # production path picks it too
+            R = torch.randn(M, N, device=DEV).bfloat16()
+            R2 = R.clone()
+            ops.gemm(X, W, R=R2, out=R2, algo=3)
+            assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+            g, u = W[: N // 2], W[N // 2:]
+            Wi = ref.interleave_gate_up(g, u).contiguous()
+            es = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+            assert rel_err(ops.gemm_silu(X, Wi), es) < 2e-2
+    finally:
+        L.gemm_stream_force_splits(0)
+
+
+@pytest.mark.parametrize("S", [2, 3, 4, 8, 16])
+def test_gemm_splitk_forced(S):
+    """Split-K of the 128^2 kernel at forced split counts: back-to-back
+    launches sharing the load-time workspace and replay of a captured
+    hipGraph, against fp32."""
+    torch.manual_seed(11)
+    L = ops.lib()
+    try:
+        L.gemm_splitk_force(S)
+        ran = 0
+        for (M, N, K) in [(48, 4096, 4096), (200, 6144, 4096), (130, 2048, 3072)]:
+            if (K // 64) % S or (K // 64) // S < 4:
+                continue
+            assert L.gemm128_splits(M, N, K) == S
+            ran += 1
+            X = torch.randn(M, K, device=DEV).bfloat16()
+            W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+            e = ref.gemm(X, W)
+            for _ in range(3):
+                assert rel_err(ops.gemm(X, W, algo=0), e) < 1e-2
+            R = torch.randn(M, N, device=DEV).bfloat16()
+            R2 = R.clone()
+            ops.gemm(X, W, R=R2, out=R2, algo=0)
+            assert rel_err(R2, ref.gemm(X, W, R)) < 1e-2
+            g, u = W[: N // 2], W[N // 2:]
+            Wi = ref.interleave_gate_up(g, u).contiguous()
+            es = torch.nn.functional.silu(X.float() @ g.float().t()) * (X.float() @ u.float().t())
+            assert rel_err(ops.gemm_silu(X, Wi), es) < 2e-2
+            out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(X, W, out=out, algo=0)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                ops.gemm(X, W, out=out, algo=0)
+            out.zero_()
+            for _ in range(2):
+                graph.replay()
+            torch.cuda.synchronize()
+            assert rel_err(out, e) < 1e-2
+        assert ran > 0
+    finally:
+        L.gemm_splitk_force(-1)
+
+
 @pytest.mark.parametrize("M,long_ctx", [(1500, False), (3000, False), (200, False),
-                                         (1500, True), (200, True)])
+                                         (1500, True), (200, True), (64, False), (5, True),
+                                         (128, False), (77, True)])
 def test_qkv_rope_fused(M, long_ctx):
     """QKV GEMM with RoPE + paged K/V write in its epilogue (AGPR path; M = 200
     takes the GEMM + rope_kv fallback) against fp32 GEMM + reference rope_kv,

@@ -1,17 +1,25 @@
-"""DP replica router on CPU: least-loaded dispatch over 2 replica processes,
-and draining a killed replica."""
+"""DP replica router on CPU (SURVEY §2.3 request-level DP, §5.3 failure
+handling): least-loaded dispatch over 2 replica processes, draining AND
+respawning a killed replica, registry freshness (the reference re-reads the
+registry on every /plan, control_plane.py:58), and retrieval-bounded prompts
+for a registry far larger than the model context."""
 import asyncio
+import time
 
 import pytest
 
 from mcp_amd.orchestrator import validate_dag
-from mcp_amd.parallel.router import ReplicaRouter
+from mcp_amd.parallel.router import ReplicaConfig, ReplicaRouter
 from mcp_amd.planner.prompt import synthetic_intent
 from mcp_amd.registry import MemoryRegistry, synthetic_registry
 
 
+def _names(dag):
+    return {n["name"] for n in dag["nodes"]}
+
+
 @pytest.mark.timeout(600)
-def test_router_dispatch_and_failover():
+def test_router_dispatch_failover_and_respawn():
     reg = MemoryRegistry(synthetic_registry(4, seed=11))
     names = [s.name for s in reg.list_services()]
     router = ReplicaRouter(["cpu", "cpu"], "tiny", reg, max_batch=8, max_nodes=3, num_blocks=256,
@@ -26,6 +34,61 @@ def test_router_dispatch_and_failover():
         more = await asyncio.gather(*[router.plan(synthetic_intent(10 + i)) for i in range(3)])
         for d in more:
             validate_dag(d, names)
-        assert router.alive == [False, True]
+        # the dead replica is replaced by a fresh process that serves again
+        t0 = time.time()
+        while not all(router.alive) and time.time() - t0 < 240:
+            await asyncio.sleep(0.2)
+        assert router.alive == [True, True] and router.respawns == [1, 0]
+        router.inflight[1]["pin"] = "x"     # make replica 0 the least loaded
+        d = await router.plan(synthetic_intent(99))
+        router.inflight[1].pop("pin")
+        validate_dag(d, names)
+        await router.aclose()
+    asyncio.run(go())
+
+
+@pytest.mark.timeout(600)
+def test_router_sees_late_registrations():
+    """A service registered after the router started must be plannable; one
+    removed must disappear - replicas never plan against a stale snapshot."""
+    reg = MemoryRegistry(synthetic_registry(3, seed=5))
+    router = ReplicaRouter(["cpu", "cpu"], "tiny", reg, max_batch=8, max_nodes=2, num_blocks=256,
+                           request_timeout=300)
+
+    async def go():
+        first = await asyncio.gather(*[router.plan(synthetic_intent(i)) for i in range(2)])
+        old = {s.name for s in reg.list_services()}
+        for d in first:
+            assert _names(d) <= old
+        late = dict(synthetic_registry(1, seed=77)[0])
+        late["name"] = "late-registered-svc"
+        late["endpoint"] = "http://late/api"
+        for n in old:
+            reg.unregister(n)
+        reg.register(late)
+        dags = await asyncio.gather(*[router.plan(synthetic_intent(20 + i)) for i in range(4)])
+        for d in dags:                      # both replicas plan with the new registry only
+            validate_dag(d, ["late-registered-svc"])
+            assert _names(d) == {"late-registered-svc"}
+        await router.aclose()
+    asyncio.run(go())
+
+
+@pytest.mark.timeout(900)
+def test_router_large_registry_is_retrieval_bounded():
+    """1,000 services (~64k prompt tokens in the reference's all-services
+    prompt) through the router: every replica keeps only the top-k services
+    (HBM top-k cosine index), so the prompt fits the 8k context and plans name
+    only registry services."""
+    reg = MemoryRegistry(synthetic_registry(1000, seed=3))
+    names = [s.name for s in reg.list_services()]
+    cfg = ReplicaConfig(model="tiny", max_batch=4, max_nodes=2, num_blocks=512, topk=8,
+                        retrieval_threshold=48)
+    router = ReplicaRouter(["cpu", "cpu"], "tiny", reg, request_timeout=600, config=cfg)
+
+    async def go():
+        dags = await asyncio.gather(*[router.plan(synthetic_intent(i)) for i in range(2)])
+        for d in dags:
+            validate_dag(d, names)
         await router.aclose()
     asyncio.run(go())
