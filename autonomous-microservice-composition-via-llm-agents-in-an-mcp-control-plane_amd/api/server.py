@@ -81,6 +81,11 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
         if planner is not None:
             return planner
         if settings.planner_backend == "local":
+            if settings.tp > 1:
+                # this process becomes TP rank 0 (driver); ranks 1..tp-1 are
+                # spawned worker processes (parallel/tp_serve.py)
+                from ..parallel.tp_serve import TPPlanner
+                return TPPlanner.launch(settings, registry)
             if settings.replicas > 1:
                 from ..parallel.router import ReplicaRouter, default_devices
                 return ReplicaRouter(default_devices(settings.replicas), settings.model, registry,

@@ -38,7 +38,7 @@ class Settings:
     remote_model: str = "gpt-4o-mini"        # control_plane.py:70
     plan_cache: int = 0                      # >0: LRU plan cache entries (intent, registry version)
     model: str = "llama3-8b"                 # llama3-8b | llama3-70b | tiny
-    tp: int = 1
+    tp: int = 1                              # >1: this process is TP rank 0, workers spawned (parallel.tp_serve)
     replicas: int = 1
     max_batch: int = 256
     max_step_tokens: int = 8192

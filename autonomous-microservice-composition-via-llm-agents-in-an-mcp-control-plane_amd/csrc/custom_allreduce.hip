@@ -22,7 +22,10 @@
 // barrier is needed: a rank can only overwrite a buffer two calls later, after
 // every peer has passed the next call's start barrier (stream order).
 // Every wait has a wall-clock timeout (no hang if a peer dies): the kernel
-// records an error code the host checks and gives up instead of spinning.
+// records an error code and gives up instead of spinning.  The code lives in
+// coherent host memory, so ``car_error`` is a plain host read (no HIP call,
+// no sync) that the engine makes after every step: a timed-out step is a hard
+// failure, never silently reduced stale data (parallel/comm.py).
 #include <string.h>
 
 #include "common.h"
@@ -66,7 +69,7 @@ DEV void block_barrier(const CarArgs& a, int phase) {
     const long long t0 = wall_clock64();
     while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
       if (wall_clock64() - t0 > CAR_TIMEOUT_TICKS) {
-        atomicExch(a.err, 1);
+        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -175,17 +178,17 @@ void* car_create(int rank, int world, size_t buf_bytes, void* handles_out) {
   bool ok = hipMalloc(&st->data, 2 * st->buf_bytes) == hipSuccess &&
             hipExtMallocWithFlags((void**)&st->sig, SIG_BYTES, hipDeviceMallocUncached) ==
                 hipSuccess &&
-            hipMalloc(&st->err, sizeof(int)) == hipSuccess &&
+            hipHostMalloc((void**)&st->err, sizeof(int), hipHostMallocCoherent) == hipSuccess &&
             hipMemset(st->sig, 0, SIG_BYTES) == hipSuccess &&
-            hipMemset(st->err, 0, sizeof(int)) == hipSuccess &&
             hipDeviceSynchronize() == hipSuccess;
+  if (ok) *st->err = 0;
   hipIpcMemHandle_t h[2];
   ok = ok && hipIpcGetMemHandle(&h[0], st->data) == hipSuccess &&
        hipIpcGetMemHandle(&h[1], st->sig) == hipSuccess;
   if (!ok) {
     if (st->data) (void)hipFree(st->data);
     if (st->sig) (void)hipFree(st->sig);
-    if (st->err) (void)hipFree(st->err);
+    if (st->err) (void)hipHostFree(st->err);
     delete st;
     return nullptr;
   }
@@ -248,9 +251,7 @@ int car_allreduce(void* state, const void* inp, void* out, long long n_elems, in
 
 int car_error(void* state) {
   CarState* st = (CarState*)state;
-  int e = 0;
-  if (hipMemcpy(&e, st->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return e;
+  return __atomic_load_n(st->err, __ATOMIC_ACQUIRE);
 }
 
 void car_destroy(void* state) {
@@ -264,6 +265,6 @@ void car_destroy(void* state) {
     }
   (void)hipFree(st->data);
   (void)hipFree(st->sig);
-  (void)hipFree(st->err);
+  (void)hipHostFree(st->err);
   delete st;
 }

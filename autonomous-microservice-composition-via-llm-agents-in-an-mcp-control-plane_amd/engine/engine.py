@@ -422,6 +422,8 @@ class LLMEngine:
             new_tokens = L.tokens.tolist() if L.tokens is not None else []
         t2 = time.perf_counter()
         self.stats["sample_s"] += t2 - t1
+        if self.bcast is not None:          # TP: a collective that timed out fails the step
+            self.model.comm_check()
         batch_seqs, sample_seqs = L.batch_seqs, L.sample_seqs
         # ---- bookkeeping
         for seq, take in batch_seqs:

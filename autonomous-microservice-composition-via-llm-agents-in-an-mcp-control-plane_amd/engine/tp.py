@@ -29,7 +29,8 @@ def agree_num_blocks(kv_bytes_per_block: int, device, group, reserve_frac: float
         n = 512
     if cap is not None:
         n = min(n, cap)
-    t = torch.tensor([n], dtype=torch.int64, device=dev if dev.type == "cuda" else "cpu")
+    gloo = group is not None and dist.is_initialized() and dist.get_backend(group) == "gloo"
+    t = torch.tensor([n], dtype=torch.int64, device=dev if dev.type == "cuda" and not gloo else "cpu")
     if group is not None and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return int(t.item())
@@ -48,4 +49,5 @@ def worker_loop(model, kv, bcast: StepBroadcaster) -> int:
             ops.copy_blocks(kv.data, csrc, cdst)
         if dstep.token_ids.numel():
             model.forward(dstep, kv)
+        model.comm_check()          # K12 peer timeout -> hard failure (lags <= 1 step)
         n += 1

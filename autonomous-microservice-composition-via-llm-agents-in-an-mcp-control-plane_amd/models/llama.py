@@ -285,6 +285,12 @@ class LlamaModel:
         return cls(cfg, random_weights(cfg, device, seed=seed, tp_rank=tp_rank, tp=tp), device,
                    tp_rank, tp, tp_group)
 
+    def comm_check(self) -> None:
+        """Raise if a collective of an earlier step failed (K12 peer timeout)."""
+        chk = getattr(self._allreduce, "check", None)
+        if chk is not None:
+            chk()
+
     # --------------------------------------------------------------- forward
     def _residual_gemm(self, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
         """x + a w^T with the residual add fused in the GEMM epilogue; for TP the

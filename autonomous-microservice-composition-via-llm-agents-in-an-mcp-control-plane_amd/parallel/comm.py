@@ -8,12 +8,11 @@ uses ``gloo`` with the same code paths.
 * ``NativeComm``        – K13: an RCCL communicator driven directly through
   ``rccl.h`` (``csrc/rccl_comm.hip``) on the caller's HIP stream; the
   ncclUniqueId is bootstrapped over the torch process group (C5).
-* ``make_allreduce``    – in-place sum for the row-parallel projections
+* ``AllReduce``         – in-place sum for the row-parallel projections
   (C1 after Wo, C2 after Wdown).  GPU: the xGMI peer-to-peer kernel of
-  ``parallel.custom_allreduce`` for decode-sized messages when enabled
-  (``MCP_CUSTOM_ALLREDUCE=1``), else the native RCCL communicator
-  (``MCP_COMM=native``, default) or torch.distributed's (``MCP_COMM=torch``);
-  CPU: gloo in fp32.
+  ``parallel.custom_allreduce`` for decode-sized messages (default on), the
+  native RCCL communicator above its size limit (``MCP_COMM=native``,
+  default) or torch.distributed's (``MCP_COMM=torch``); CPU: gloo in fp32.
 * ``StepBroadcaster``   – C4: the driver rank broadcasts each step's packed
   int32 descriptor (tokens, positions, slots, block tables, work lists, KV
   copy-on-write pairs) to the TP worker ranks.
@@ -86,28 +85,63 @@ class NativeComm:
             self._comm = 0
 
 
-def make_allreduce(group, device) -> Callable[[torch.Tensor], None]:
-    device = torch.device(device)
-    if device.type != "cuda":
-        def cpu_allreduce(t: torch.Tensor):
-            tf = t.float()
-            dist.all_reduce(tf, group=group)
-            t.copy_(tf.to(t.dtype))
-        return cpu_allreduce
-    custom = None
-    if os.environ.get("MCP_CUSTOM_ALLREDUCE", "0") == "1":
-        from .custom_allreduce import CustomAllReduce
-        custom = CustomAllReduce(group, device)
-    native = NativeComm(group, device) if os.environ.get("MCP_COMM", "native") == "native" else None
+class AllReduce:
+    """In-place sum over the TP group for the row-parallel projections (C1, C2).
 
-    def gpu_allreduce(t: torch.Tensor):
-        if custom is not None and custom.eligible(t):
-            custom(t)
-        elif native is not None:
-            native.all_reduce(t)
+    GPU: K12 (``parallel.custom_allreduce``, xGMI peer reads) for messages up
+    to ``MCP_CAR_MAX_BYTES`` (default 8 MiB: decode steps of up to 512 tokens
+    at H = 8192), the native RCCL communicator above that (``MCP_COMM=native``,
+    default) or torch.distributed's (``MCP_COMM=torch``).  ``MCP_CUSTOM_ALLREDUCE``
+    = auto (default: on for GPU groups of 2-8 ranks) | 1 | 0.
+    CPU: gloo in fp32.
+
+    ``check()`` raises when a K12 barrier timed out (a peer never arrived): the
+    engine calls it after every step, so a lost peer is a hard failure instead
+    of activations summed from stale staging buffers."""
+
+    def __init__(self, group, device):
+        self.group = group
+        self.device = torch.device(device)
+        self.custom = None
+        self.native = None
+        if self.device.type != "cuda":
+            return
+        world = dist.get_world_size(group)
+        mode = os.environ.get("MCP_CUSTOM_ALLREDUCE", "auto")
+        if mode == "1" or (mode == "auto" and 2 <= world <= 8):
+            from .custom_allreduce import CustomAllReduce
+            self.custom = CustomAllReduce(group, self.device,
+                                          max_bytes=int(os.environ.get("MCP_CAR_MAX_BYTES",
+                                                                       str(8 << 20))))
+        if os.environ.get("MCP_COMM", "native") == "native":
+            self.native = NativeComm(group, self.device)
+
+    def __call__(self, t: torch.Tensor) -> None:
+        if self.device.type != "cuda":
+            tf = t.float()
+            dist.all_reduce(tf, group=self.group)
+            t.copy_(tf.to(t.dtype))
+        elif self.custom is not None and self.custom.eligible(t):
+            self.custom(t)
+        elif self.native is not None:
+            self.native.all_reduce(t)
         else:
-            dist.all_reduce(t, group=group)
-    return gpu_allreduce
+            dist.all_reduce(t, group=self.group)
+
+    def check(self) -> None:
+        if self.custom is not None:
+            self.custom.check()
+
+
+def make_allreduce(group, device) -> AllReduce:
+    return AllReduce(group, device)
+
+
+def _is_gloo(group) -> bool:
+    try:
+        return dist.get_backend(group) == "gloo"
+    except Exception:  # noqa: BLE001
+        return False
 
 
 def make_sp_collectives(group, device):
@@ -162,8 +196,14 @@ class StepBroadcaster:
 
     def __init__(self, group, device, src: int = 0):
         self.group, self.device, self.src = group, torch.device(device), src
+        self._gloo = _is_gloo(group)
 
     def _bcast(self, t: torch.Tensor):
+        if t.is_cuda and self._gloo:               # gloo moves host tensors only
+            h = t.cpu()
+            dist.broadcast(h, src=self.src, group=self.group)
+            t.copy_(h)
+            return
         dist.broadcast(t, src=self.src, group=self.group)
 
     def send(self, payload: torch.Tensor, layout) -> None:

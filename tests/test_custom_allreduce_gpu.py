@@ -96,3 +96,61 @@ def test_custom_allreduce_two_ranks_one_gpu():
     for rank, (errs, times) in results.items():
         assert not errs, f"rank {rank}: {errs}"
         print(f"rank {rank} custom all-reduce us/call: {times}")
+
+
+def _missing_peer_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        import mcp_amd  # noqa: F401
+        from mcp_amd.parallel.custom_allreduce import CustomAllReduce
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        car = CustomAllReduce(dist.group.WORLD, "cuda:0", max_bytes=1 << 20)
+        x = torch.ones(8192, device="cuda", dtype=torch.bfloat16)
+        car(x.clone())                    # both ranks: a healthy call
+        torch.cuda.synchronize()
+        car.check()
+        dist.barrier()
+        raised = None
+        if rank == 0:                     # rank 1 never arrives for this call
+            car(x.clone())
+            torch.cuda.synchronize()      # the kernel gives up after its ~2 s timeout
+            try:
+                car.check()
+                raised = False
+            except RuntimeError:
+                raised = True
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put((rank, raised))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_custom_allreduce_missing_peer_is_a_hard_error():
+    """A peer that never joins a K12 call: the waiting rank's kernel times out
+    instead of hanging, and ``check()`` (called by the engine after every TP
+    step) raises instead of letting stale staging data pass as a sum."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_missing_peer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, v = q.get(timeout=240)
+            results[rank] = v
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert results[0] is True, results
+    assert results[1] is None, results

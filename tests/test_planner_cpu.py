@@ -248,3 +248,44 @@ def test_engine_stall_watchdog_returns_503():
         assert r.status_code == 503
         assert c.get("/healthz").status_code == 503
     planner._stop.set()
+
+
+def test_engine_stall_recovers_after_the_step_returns():
+    """Stall recovery: the hung step's requests fail with 503, and once the
+    step returns the planner aborts what the engine still holds (blocks back
+    to the allocator) and serves new requests again - not 503 forever."""
+    import time as _time
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    eng = LLMEngine(model, num_blocks=128, max_batch=4)
+    reg = MemoryRegistry(synthetic_registry(3, seed=5))
+    planner = LocalPlanner(eng, reg, max_nodes=2, watchdog_s=0.3)
+    real_step = eng.step
+    hang = {"left": 1}
+
+    def step_once_hung():
+        if hang["left"]:
+            hang["left"] -= 1
+            _time.sleep(1.5)
+        return real_step()
+    eng.step = step_once_hung
+    free0 = eng.alloc.num_free
+
+    def h(request):
+        return httpx.Response(200, json={})
+    app = create_app(Settings(), registry=reg, planner=planner, transport=httpx.MockTransport(h))
+    names = [s.name for s in reg.list_services()]
+    with TestClient(app) as c:
+        assert c.post("/plan", json={"intent": "charge the order"}).status_code == 503
+        t0 = _time.time()
+        while planner.stalled and _time.time() - t0 < 30:
+            _time.sleep(0.05)
+        assert not planner.stalled
+        r = c.post("/plan", json={"intent": "refund the order"})
+        assert r.status_code == 200, r.text
+        validate_dag(r.json()["graph"], names)
+        assert c.get("/healthz").status_code == 200
+    planner._stop.set()
+    assert not eng.has_work()
+    if free0 is not None:
+        eng.drop_prefixes()                 # the cached registry prefix is the only holder left
+        assert eng.alloc.num_free == free0

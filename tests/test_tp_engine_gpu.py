@@ -1,0 +1,55 @@
+"""TP=2 planner engine as two processes on the box's one GPU, every
+row-parallel all-reduce through K12 (the xGMI peer-read kernel; here the
+"peer" buffer is the same HBM), against the TP=1 engine over the same
+weights: greedy (temperature 0) plans must be identical.  The driver runs in
+this process (TPPlanner, as behind the API with MCP_TP=2), the worker rank is
+a spawned process; the group is gloo (RCCL refuses two ranks on one device),
+so MCP_COMM=torch and a K12 staging buffer large enough for every message."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(600)
+def test_tp2_two_processes_one_gpu_matches_tp1(monkeypatch):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    monkeypatch.setenv("MCP_COMM", "torch")
+    monkeypatch.setenv("MCP_CUSTOM_ALLREDUCE", "1")
+    monkeypatch.setenv("MCP_CAR_MAX_BYTES", str(64 << 20))
+    from mcp_amd.config import Settings
+    from mcp_amd.engine.engine import LLMEngine
+    from mcp_amd.models.llama import LlamaModel, get_config, random_weights
+    from mcp_amd.orchestrator import validate_dag
+    from mcp_amd.parallel.tp_serve import TPPlanner
+    from mcp_amd.planner.local import LocalPlanner
+    from mcp_amd.planner.prompt import synthetic_intent
+    from mcp_amd.registry import MemoryRegistry, synthetic_registry
+
+    reg = MemoryRegistry(synthetic_registry(10, seed=1))
+    names = [s.name for s in reg.list_services()]
+    intents = [synthetic_intent(i) for i in range(4)]
+    st = Settings(planner_backend="local", model="llama3-1b-ish", tp=2, max_batch=8,
+                  max_step_tokens=2048, max_nodes=4, kv_blocks=512, seed=0)
+    tp = TPPlanner.launch(st, reg, devices=["cuda:0", "cuda:0"], backend="gloo",
+                          full_weights_seed=5, temperature=0.0)
+    try:
+        ar = tp.engine.model._allreduce
+        assert ar.custom is not None and ar.native is None
+        dags_tp = tp.plan_many(intents)
+        tp.engine.model.comm_check()
+        steps_tp = tp.engine.stats["steps"]
+    finally:
+        tp.shutdown()
+    assert steps_tp > 0
+    for d in dags_tp:
+        validate_dag(d, names)
+
+    cfg = get_config("llama3-1b-ish")
+    m1 = LlamaModel(cfg, random_weights(cfg, "cuda:0", seed=5), "cuda:0")
+    eng1 = LLMEngine(m1, num_blocks=512, max_batch=8, max_step_tokens=2048, temperature=0.0)
+    dags_1 = LocalPlanner(eng1, reg, max_nodes=4).plan_many(intents)
+    assert dags_tp == dags_1
