@@ -19,6 +19,13 @@
 //      operand") and V^T read with ds_read_b64_tr_b16 (T10).
 // K/V tiles: global_load_lds_dwordx4 into a double-buffered LDS ring with the
 // 256-B-row XOR swizzle chunk ^= row&15 on source and read (tools/lds_banks.py).
+//
+// Split-KV (K6, KSPLIT): a decode step of few sequences with long contexts has
+// few work items (one 1-wave item per sequence and kv head: batch 1 on 8B is 8
+// workgroups on 256 CUs).  Such steps split each item's key range over
+// gridDim.z workgroups; each writes its normalised fp32 partial O and its
+// log2-sum-exp (split 0 folds in the cascade prefix partial), and
+// attn_split_combine merges the splits with LSE weights.
 #include <stdlib.h>
 
 #include "common.h"
@@ -56,6 +63,10 @@ struct AttnArgs {
   const bf16* pre_o;       // MODE 0: normalised prefix partial O [T, Hq, D] to merge
   const float* pre_lse;    // MODE 0: its log2-sum-exp [T, Hq]
   float* lse_out;          // MODE 1: log2-sum-exp of the prefix partial
+  // split-KV (KSPLIT): partials [nsplit][rows][D] fp32 and [nsplit][rows] LSE
+  float* split_o;
+  float* split_lse;
+  int rows;                // T * Hq
   const int* pre_bt;       // MODE 1: block table of the shared prefix
   int pre_keys;            // MODE 1: prefix keys (multiple of 64)
   int pre_tokens;          // MODE 1: query tokens [0, pre_tokens) of the flat batch
@@ -67,7 +78,7 @@ struct AttnArgs {
 //         sequence that shares one registry prefix, 16-token tiles that mix
 //         sequences (they attend to the same K/V), no mask (every query sits
 //         after the prefix).  Writes normalised O and its LSE.
-template <int NW, int G, int MODE, int NBUF_ = 0>
+template <int NW, int G, int MODE, int NBUF_ = 0, bool KSPLIT = false>
 __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   constexpr int TPW = 16 / G;                 // tokens per wave
   constexpr int QT = NW * TPW;                // tokens per work item
@@ -111,6 +122,12 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
     const int kv_end = cl - ql + last_tok + 1;
     ntiles = (kv_end + KT - 1) / KT;
     kt0 = a.kv_begin ? a.kv_begin[s] / KT : 0;
+    if constexpr (KSPLIT) {                               // this split's share of the tiles
+      const int span = max(ntiles - kt0, 0), z = blockIdx.z, nz = gridDim.z;
+      const int b0 = kt0 + span * z / nz, b1 = kt0 + span * (z + 1) / nz;
+      kt0 = b0;
+      ntiles = b1;
+    }
   }
 
   // Q fragments (B operand): lane holds Q[row fr][d = 32ks + 8fq + j]
@@ -230,6 +247,36 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   if (!qvalid) return;
   const size_t row = (size_t)(qs + tok) * Hq + head;
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if constexpr (KSPLIT) {
+    // normalised partial + its LSE; split 0 also carries the cascade prefix
+    float lse = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
+    float wa = 0.f, wb = 1.f;
+    const bf16* pp = nullptr;
+    if (blockIdx.z == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
+      const float lse_a = a.pre_lse[row];
+      const float mx = fmaxf(lse_a, lse);
+      const float ea = exp2f(lse_a - mx), eb = lse == -INFINITY ? 0.f : exp2f(lse - mx);
+      wa = ea / (ea + eb);
+      wb = eb / (ea + eb);
+      lse = mx + __log2f(ea + eb);
+      pp = a.pre_o + row * D + 4 * fq;
+    }
+    float* po32 = a.split_o + ((size_t)blockIdx.z * a.rows + row) * D + 4 * fq;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      f32x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = o[dt][r] * inv * wb;
+      if (pp) {
+        const bf16x4 pa = *reinterpret_cast<const bf16x4*>(pp + dt * 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] += (float)pa[r] * wa;
+      }
+      *reinterpret_cast<f32x4*>(po32 + dt * 16) = w;
+    }
+    if (fq == 0) a.split_lse[(size_t)blockIdx.z * a.rows + row] = lse;
+    return;
+  }
   float wa = 0.f, wb = 1.f;
   const bf16* po = nullptr;
   if (MODE == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
@@ -261,8 +308,90 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   }
 }
 
+// Merge of the split-KV partials of 1-wave items: one workgroup per (item,
+// kv head) = 16 rows (TPW tokens x G heads).  Wave w takes splits w, w + 4,
+// ...; lane = (row l & 15, 32-wide d slice).  Each wave keeps its own running
+// max / weighted sum (loads of 4 splits in flight), then the 4 waves' partial
+// results are merged through LDS.
 template <int G>
-void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s) {
+__global__ __launch_bounds__(256) void attn_split_combine(const AttnArgs a, int nsplit) {
+  constexpr int CW = 4;
+  __shared__ float red_m[CW][64], red_d[CW][64];
+  __shared__ float red_o[CW][32][65];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, dq = lane >> 4;
+  const int s = a.work_seq[blockIdx.x];
+  const int tok = a.work_q0[blockIdx.x] + fr / G;
+  const bool valid = tok < a.q_len[s];
+  const int head = blockIdx.y * G + fr % G;
+  const size_t row = (size_t)(a.q_start[s] + (valid ? tok : 0)) * a.Hq + head;
+  float m = -INFINITY;
+#pragma unroll 4
+  for (int z = wave; z < nsplit; z += CW) m = fmaxf(m, a.split_lse[(size_t)z * a.rows + row]);
+  float acc[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) acc[j] = 0.f;
+  float den = 0.f;
+  const float mu = m == -INFINITY ? 0.f : m;
+#pragma unroll 4
+  for (int z = wave; z < nsplit; z += CW) {
+    const float w = exp2f(a.split_lse[(size_t)z * a.rows + row] - mu);   // 0 for empty splits
+    den += w;
+    const f32x4* p = reinterpret_cast<const f32x4*>(a.split_o + ((size_t)z * a.rows + row) * D + 32 * dq);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 v = p[j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[4 * j + r] += w * v[r];
+    }
+  }
+  red_m[wave][lane] = m;
+  red_d[wave][lane] = den;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) red_o[wave][j][lane] = acc[j];
+  __syncthreads();
+  if (wave != 0 || !valid) return;
+  float mt = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < CW; ++w) mt = fmaxf(mt, red_m[w][lane]);
+  const float mtu = mt == -INFINITY ? 0.f : mt;
+  float sc[CW], dt = 0.f;
+#pragma unroll
+  for (int w = 0; w < CW; ++w) {
+    const float mw = red_m[w][lane];
+    sc[w] = mw == -INFINITY ? 0.f : exp2f(mw - mtu);
+    dt += sc[w] * red_d[w][lane];
+  }
+  const float inv = dt > 0.f ? 1.f / dt : 0.f;
+  bf16* op = a.out + row * D + 32 * dq;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bf16x8 o;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < CW; ++w) v += sc[w] * red_o[w][8 * j + r][lane];
+      o[r] = (bf16)(v * inv);
+    }
+    *reinterpret_cast<bf16x8*>(op + 8 * j) = o;
+  }
+}
+
+template <int G>
+void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s, int nsplit = 1) {
+  // split items double-buffer their K/V tiles (one tile in flight while the
+  // previous is consumed): 10-25 % faster than the single-buffer decode form
+  // at 8k-128k (profiles/attention_splitkv.md)
+  static const int split_bufs = getenv("MCP_ATTN_SPLIT_BUFS") ? atoi(getenv("MCP_ATTN_SPLIT_BUFS")) : 2;
+  if (nw == 1 && nsplit > 1) {
+    if (split_bufs == 2)
+      attn_kernel<1, G, 0, 2, true><<<dim3(nwork, a.Hkv, nsplit), 64, 0, s>>>(a);
+    else
+      attn_kernel<1, G, 0, 0, true><<<dim3(nwork, a.Hkv, nsplit), 64, 0, s>>>(a);
+    attn_split_combine<G><<<dim3(nwork, a.Hkv), 256, 0, s>>>(a, nsplit);
+    return;
+  }
   const dim3 grid(nwork, a.Hkv);
   static const int nw1_bufs = getenv("MCP_ATTN_NW1_BUFS") ? atoi(getenv("MCP_ATTN_NW1_BUFS")) : 1;
   if (nw == 1 && nw1_bufs == 2)
@@ -317,10 +446,12 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            const int* block_table, int max_blocks, const int* work_seq,
                            const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
                            float scale, const int* kv_begin, const void* pre_o,
-                           const float* pre_lse, hipStream_t s) {
+                           const float* pre_lse, hipStream_t s, int nsplit, float* split_o,
+                           float* split_lse, int rows) {
   if (head_dim != D) return 1;
   if (nw != 1 && nw != 4) return 2;
   if (nwork <= 0) return 0;
+  if (nsplit > 1 && (nw != 1 || !split_o || !split_lse)) return 4;
   AttnArgs a{};
   a.q = (const bf16*)q;
   a.kc = (const bf16*)k_cache;
@@ -339,7 +470,10 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
   a.kv_begin = kv_begin;
   a.pre_o = (const bf16*)pre_o;
   a.pre_lse = pre_lse;
-  ATTN_SWITCH_G(Hq / Hkv, attn_dispatch<GG>(nw, a, nwork, s))
+  a.split_o = split_o;
+  a.split_lse = split_lse;
+  a.rows = rows;
+  ATTN_SWITCH_G(Hq / Hkv, attn_dispatch<GG>(nw, a, nwork, s, nsplit))
   return 0;
 }
 

@@ -209,7 +209,9 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
                      const at::Tensor& work_seq, const at::Tensor& work_q0, int64_t nw,
                      double scale, const c10::optional<at::Tensor>& kv_begin,
                      const c10::optional<at::Tensor>& pre_o,
-                     const c10::optional<at::Tensor>& pre_lse) {
+                     const c10::optional<at::Tensor>& pre_lse, int64_t nsplit,
+                     const c10::optional<at::Tensor>& split_o,
+                     const c10::optional<at::Tensor>& split_lse) {
   CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
   CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
   CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq); CHECK_I32_TENSOR(work_q0);
@@ -220,6 +222,14 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
   TORCH_CHECK(block_table.dim() == 2, "block_table [S, max_blocks]");
   TORCH_CHECK(work_seq.numel() == work_q0.numel(), "work list");
+  if (nsplit > 1) {
+    TORCH_CHECK(nw == 1, "split-KV serves the 1-wave (decode) items");
+    TORCH_CHECK(split_o.has_value() && split_lse.has_value(), "split-KV needs split_o / split_lse");
+    TORCH_CHECK(split_o->scalar_type() == at::kFloat && split_o->is_contiguous() &&
+                split_o->numel() >= nsplit * q.numel(), "split_o [nsplit, T, Hq, D] f32");
+    TORCH_CHECK(split_lse->scalar_type() == at::kFloat && split_lse->is_contiguous() &&
+                split_lse->numel() >= nsplit * q.size(0) * Hq, "split_lse [nsplit, T, Hq] f32");
+  }
   const int* kb = nullptr;
   const void* po = nullptr;
   const float* pl = nullptr;
@@ -238,7 +248,9 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
       q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
       q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
       block_table.size(1), work_seq.data_ptr<int>(), work_q0.data_ptr<int>(), work_seq.numel(), nw,
-      Hq, Hkv, D, (float)scale, kb, po, pl, stream());
+      Hq, Hkv, D, (float)scale, kb, po, pl, stream(), (int)nsplit,
+      nsplit > 1 ? split_o->data_ptr<float>() : nullptr,
+      nsplit > 1 ? split_lse->data_ptr<float>() : nullptr, (int)(q.size(0) * Hq));
   TORCH_CHECK(rc == 0, "paged_attention: unsupported config (code ", rc, ")");
   check_launch("paged_attention");
 }
@@ -421,7 +433,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"),
         py::arg("block_table"), py::arg("work_seq"), py::arg("work_q0"), py::arg("nw"),
         py::arg("scale"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
-        py::arg("pre_lse") = py::none());
+        py::arg("pre_lse") = py::none(), py::arg("nsplit") = 1, py::arg("split_o") = py::none(),
+        py::arg("split_lse") = py::none());
   m.def("prefix_attention", &prefix_attention);
   m.def("attn_tokens_per_item", &attn_tokens_per_item);
   m.def("sample_allowed", &sample_allowed, py::arg("hidden"), py::arg("W"), py::arg("allow_ptr"),

@@ -92,7 +92,8 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            const int* block_table, int max_blocks, const int* work_seq,
                            const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
                            float scale, const int* kv_begin, const void* pre_o,
-                           const float* pre_lse, hipStream_t s);
+                           const float* pre_lse, hipStream_t s, int nsplit = 1,
+                           float* split_o = nullptr, float* split_lse = nullptr, int rows = 0);
 int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
                             float* lse_out, const int* pre_bt, int pre_keys, int pre_tokens,
                             int Hq, int Hkv, int head_dim, float scale, hipStream_t s);

@@ -125,3 +125,156 @@ int launch_segment_topk(const float* vals, const int* idx_in, int B, int L, int 
   segment_topk_kernel<<<dim3(nseg, B), NT, 0, s>>>(vals, idx_in, L, seg_len, k, out_v, out_i);
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Fused scoring + per-segment top-k (the production K11 path): scores never
+// touch HBM.  Workgroup = ceil(B / 16) waves on one segment of SEGR corpus
+// rows; wave w owns queries 16 w .. 16 w + 15, all waves stream the same
+// rows (HBM once, the other reads hit L1/L2).
+//  * S^T[row][query] per 16-row block by v_mfma_f32_16x16x32_bf16: corpus rows
+//    are the A operand (a 16-step register ring of direct loads keeps ~16 KiB
+//    per wave in flight), the wave's 16 query vectors stay in registers as the
+//    B operand (D/32 fragments).  Lane (r, g) holds rows 4 g + i of query r.
+//  * per query a candidate list in LDS (CAP entries) behind a running
+//    threshold tau = the k-th best so far: scores >= tau are appended (LDS
+//    atomic slot), and a list close to full is compacted by the whole wave to
+//    its k best by exact rank (score desc, row index asc), which raises tau.
+//    After the first few blocks almost nothing passes tau.
+//  * the segment's top k per query (rank order) go to cand[B][nseg][k]; the
+//    hierarchical segment_topk above merges the segments.
+namespace {
+constexpr int FT_CAP = 128;
+constexpr int FT_SEGR = 4096;
+
+template <int NS>
+__global__ __launch_bounds__(256) void topk_fused_kernel(const bf16* __restrict__ Q,
+                                                          const bf16* __restrict__ E, int B,
+                                                          int N, int k, float* __restrict__ cand_v,
+                                                          int* __restrict__ cand_i) {
+  constexpr int D = NS * 32;
+  // per wave (dynamic LDS, so a 1-wave workgroup takes 16.5 KiB, not 66):
+  // candidate values [16][CAP], indices [16][CAP], counts [16], thresholds [16]
+  extern __shared__ __attribute__((aligned(16))) char ft_smem[];
+  constexpr int WAVE_BYTES = 16 * FT_CAP * 8 + 16 * 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int seg = blockIdx.x, nseg = gridDim.x;
+  const int row0 = seg * FT_SEGR;
+  const int rows = min(FT_SEGR, N - row0);
+  const int q = wave * 16 + r;                        // this lane's query
+  char* wbase = ft_smem + wave * WAVE_BYTES;
+  float (*BV)[FT_CAP] = reinterpret_cast<float (*)[FT_CAP]>(wbase);
+  int (*BI)[FT_CAP] = reinterpret_cast<int (*)[FT_CAP]>(wbase + 16 * FT_CAP * 4);
+  int* cntw = reinterpret_cast<int*>(wbase + 16 * FT_CAP * 8);
+  float* tauw = reinterpret_cast<float*>(wbase + 16 * FT_CAP * 8 + 64);
+
+  // query fragments: step s covers d = 32 s + {8 g .. 8 g + 7}
+  bf16x8 qf[NS];
+  {
+    const bf16* qp = Q + (size_t)min(q, B - 1) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
+  }
+  if (lane < 16) {
+    cntw[lane] = 0;
+    tauw[lane] = -INFINITY;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  float tau = -INFINITY;
+
+  // compaction of query qq's list to its k best (whole wave, uniform)
+  auto compact = [&](int qq) {
+    const int n = cntw[qq];
+    float v0 = -INFINITY, v1 = -INFINITY;
+    int i0 = 0x7fffffff, i1 = 0x7fffffff;
+    if (lane < n) { v0 = BV[qq][lane]; i0 = BI[qq][lane]; }
+    if (lane + 64 < n) { v1 = BV[qq][lane + 64]; i1 = BI[qq][lane + 64]; }
+    int r0 = 0, r1 = 0;
+    for (int j = 0; j < n; ++j) {
+      const float vj = BV[qq][j];
+      const int ij = BI[qq][j];
+      r0 += (vj > v0 || (vj == v0 && ij < i0)) ? 1 : 0;
+      r1 += (vj > v1 || (vj == v1 && ij < i1)) ? 1 : 0;
+    }
+    if (lane < n && r0 < k) { BV[qq][r0] = v0; BI[qq][r0] = i0; }
+    if (lane + 64 < n && r1 < k) { BV[qq][r1] = v1; BI[qq][r1] = i1; }
+    if (lane < n && r0 == k - 1) tauw[qq] = v0;
+    if (lane + 64 < n && r1 == k - 1) tauw[qq] = v1;
+    if (lane == 0) cntw[qq] = min(n, k);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  };
+
+  const int nblk = (rows + 15) / 16;
+  // A-operand ring: 16 d-steps in flight; step t = NS b + s, the loop is
+  // unrolled by NS so that s (the query fragment) and the ring slot are static
+  static_assert(NS % 16 == 0, "ring of 16 d-steps");
+  bf16x8 ring[16];
+  auto load = [&](int slot, int t) {
+    const int b = t / NS, s = t % NS;
+    if (b < nblk)
+      ring[slot] = *reinterpret_cast<const bf16x8*>(
+          E + (size_t)(row0 + min(16 * b + r, rows - 1)) * D + 8 * g + 32 * s);
+  };
+#pragma unroll
+  for (int j = 0; j < 16; ++j) load(j, j);
+  for (int b = 0; b < nblk; ++b) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      acc = mfma16x16x32(ring[s % 16], qf[s], acc);
+      load(s % 16, b * NS + s + 16);
+    }
+    // block b done: lane holds rows 4 g + i of query r
+    if (q < B) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int lr = 16 * b + 4 * g + i;
+        if (lr < rows && acc[i] >= tau) {
+          const int pos = atomicAdd(&cntw[r], 1);
+          BV[r][pos] = acc[i];
+          BI[r][pos] = row0 + lr;
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    // compact the lists that could overflow on the next block (<= 16 adds each)
+    unsigned long long need = __ballot(lane < 16 && cntw[lane] > FT_CAP - 16);
+    while (need) {
+      const int qq = __ffsll((long long)need) - 1;
+      need &= need - 1;
+      compact(qq);
+    }
+    tau = tauw[r];
+  }
+  // final: every list to its k best, in rank order
+  for (int qq = 0; qq < 16; ++qq) compact(qq);
+  if (wave * 16 >= B) return;
+  for (int qq = 0; qq < 16; ++qq) {
+    const int qg = wave * 16 + qq;
+    if (qg >= B) break;
+    const int n = cntw[qq];
+    float* ov = cand_v + ((size_t)qg * nseg + seg) * k;
+    int* oi = cand_i + ((size_t)qg * nseg + seg) * k;
+    for (int j = lane; j < k; j += 64) {
+      ov[j] = j < n ? BV[qq][j] : -INFINITY;
+      oi[j] = j < n ? BI[qq][j] : 0x7fffffff;
+    }
+  }
+}
+}  // namespace
+
+int topk_fused_segments(int N) { return (N + FT_SEGR - 1) / FT_SEGR; }
+
+// cand_v / cand_i: [B, topk_fused_segments(N), k]; returns nonzero if unsupported
+int launch_topk_fused(const void* Q, const void* E, int B, int N, int D, int k, float* cand_v,
+                      int* cand_i, hipStream_t s) {
+  if (B <= 0 || B > 64 || N <= 0 || k <= 0 || k > 64) return 1;
+  const int nseg = topk_fused_segments(N);
+  const int waves = (B + 15) / 16;
+  const size_t lds = (size_t)waves * (16 * FT_CAP * 8 + 16 * 8);
+  switch (D) {
+    case 1024: topk_fused_kernel<32><<<nseg, 64 * waves, lds, s>>>((const bf16*)Q, (const bf16*)E, B, N, k, cand_v, cand_i); return 0;
+    case 512: topk_fused_kernel<16><<<nseg, 64 * waves, lds, s>>>((const bf16*)Q, (const bf16*)E, B, N, k, cand_v, cand_i); return 0;
+    default: return 2;
+  }
+}

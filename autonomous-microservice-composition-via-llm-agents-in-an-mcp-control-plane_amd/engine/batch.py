@@ -37,12 +37,50 @@ class AttnMeta:
     pre_bt: Optional[torch.Tensor] = None     # block ids of the shared prefix
     pre_keys: int = 0                         # shared prefix keys (multiple of 64)
     pre_tokens: int = 0                       # flat tokens [0, pre_tokens) attend to it
+    kv_splits: int = 1                        # split-KV factor of the 1-wave items (K6)
 
     def work_lists(self):
         return self.work
 
 
 _XCD_ORDER = os.environ.get("MCP_ATTN_XCD_ORDER", "1") == "1"
+N_SIZES = 19            # packed segments of pack_host (the layout's leading entries)
+
+
+def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
+                     max_bytes: int = 64 << 20, hq: int = 32) -> int:
+    """Split-KV factor for the 1-wave (decode-sized) attention items of a step
+    (csrc/attention.hip KSPLIT).  A step of few sequences with long contexts has
+    few work items (one per sequence and kv head) on 256 CUs - batch-1 decode
+    on 8B is 8 workgroups walking the whole context.  Split each item's own key
+    range (``kv_lens`` = keys it attends itself, after any cascade prefix) so
+    the grid reaches ~2 workgroups per CU, keeping >= 4 key tiles per split.
+    ``MCP_KV_SPLIT``: 0 disables, N > 1 forces N."""
+    forced = int(os.environ.get("MCP_KV_SPLIT", "-1"))
+    if forced == 0:
+        return 1
+    t1 = tokens_per_item(1, group)
+    cutoff = int(os.environ.get("MCP_ATTN_NW1_CUTOFF", str(t1 * 2)))
+    items, tiles, rows = 0, 0, 0
+    for ql, kl in zip(q_lens, kv_lens):
+        if 0 < ql <= cutoff:
+            items += -(-ql // t1)
+            tiles = max(tiles, -(-kl // 64))
+            rows += ql
+    if items == 0:
+        return 1
+    if forced > 1:
+        return forced
+    work = items * hkv
+    if work >= num_cus or tiles < 16:
+        return 1
+    # ~2 workgroups per CU (measured best at batch 1 / 4 and 8k-128k contexts,
+    # profiles/attention_splitkv.jsonl)
+    ns = min(tiles // 4, -(-2 * num_cus // work), 128)
+    sum_tokens = max(sum(q_lens), 1)
+    while ns > 1 and ns * sum_tokens * hq * 128 * 4 > max_bytes:
+        ns //= 2
+    return max(ns, 1)
 
 
 def build_work(q_len: Sequence[int], group: int, small_cutoff: Optional[int] = None):
@@ -251,7 +289,7 @@ def pack_step(entries, block_size: int, group: int, copies=None, pre_bt=None, pr
 def step_from_host(host: np.ndarray, layout) -> StepInputs:
     """``StepInputs`` of numpy views into a packed host buffer (the inverse of
     ``pack_host`` on the host side; used by the hipGraph bucket packer)."""
-    sizes, S, pre_tokens = layout[:-2], layout[-2], layout[-1]
+    sizes, S, pre_tokens = layout[:N_SIZES], layout[N_SIZES], layout[N_SIZES + 1]
     vs, off = [], 0
     for n in sizes:
         vs.append(host[off:off + n])
@@ -278,7 +316,7 @@ def to_device(host: np.ndarray, device, pin: bool = True) -> torch.Tensor:
 def views(t: torch.Tensor, layout):
     """Inverse of ``pack_host`` on an (already transferred) int32 tensor.
     Returns (DeviceStep, copy_src, copy_dst)."""
-    sizes, S, pre_tokens = layout[:-2], layout[-2], layout[-1]
+    sizes, S, pre_tokens = layout[:N_SIZES], layout[N_SIZES], layout[N_SIZES + 1]
     vs, off = [], 0
     for n in sizes:
         vs.append(t[off:off + n])
@@ -289,7 +327,8 @@ def views(t: torch.Tensor, layout):
         ws, wq = vs[8 + 2 * i], vs[9 + 2 * i]
         if ws.numel():
             work_l.append((nw, ws, wq))
-    meta = AttnMeta(q_start=vs[4], q_len=vs[5], ctx_len=vs[6], block_table=bt, work=work_l)
+    meta = AttnMeta(q_start=vs[4], q_len=vs[5], ctx_len=vs[6], block_table=bt, work=work_l,
+                    kv_splits=int(layout[N_SIZES + 2]) if len(layout) > N_SIZES + 2 else 1)
     if pre_tokens > 0:
         meta.kv_begin, meta.pre_bt = vs[14], vs[15]
         meta.pre_keys, meta.pre_tokens = int(vs[15].numel()) * BLOCK_SIZE, pre_tokens

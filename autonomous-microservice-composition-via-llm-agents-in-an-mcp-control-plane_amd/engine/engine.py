@@ -33,7 +33,7 @@ import torch
 from .. import ops
 from ..utils.metrics import METRICS
 from ..utils.tracing import span
-from .batch import BLOCK_SIZE, HostStager, pack_step, step_from_host, views
+from .batch import BLOCK_SIZE, HostStager, choose_kv_splits, pack_step, step_from_host, views
 from .kv_cache import KVCache
 
 _uid = itertools.count(1)
@@ -129,7 +129,7 @@ class LLMEngine:
         if self._graphs_wanted:
             from .graphs import GraphRunner
             self.graphs = GraphRunner(model, self.kv, temperature, seed)
-        self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0,
+        self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "kv_split_steps": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
@@ -354,7 +354,13 @@ class LLMEngine:
                     counts[id(e)] = counts.get(id(e), 0) + 1
             if counts:
                 best = max(counts, key=counts.get)
+                n_share = counts[best]
                 casc = next(q.prefix for q in pool if q.prefix is not None and id(q.prefix) == best)
+                # the prefix pass has ~(sharing tokens / 32) x Hkv workgroups: for a
+                # long prefix shared by few sequences that underfills the chip,
+                # while per-sequence attention can split the key range (split-KV)
+                if n_share < 2 or (casc.length >= 16 * BLOCK_SIZE and n_share < 16):
+                    casc = None
         order = pool
         if casc is not None:
             order = [q for q in pool if q.prefix is casc and q.materialized] + \
@@ -390,13 +396,22 @@ class LLMEngine:
         if sample_seqs:            # grammar masks go in the same single H2D copy
             allowed = [q.decoder.allowed() for q in sample_seqs]
             ctr = [(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF for q in sample_seqs]
+        # split-KV for few long-context decode sequences (K6); such steps run
+        # eager (the captured buckets use the unsplit kernel)
+        kv_splits = choose_kv_splits(
+            [e[1] for e in entries],
+            [e[2] + e[1] - (e[4] if pre_tokens else 0) for e in entries],
+            group, self.model.hkv, hq=self.model.hq) if self.device.type == "cuda" else 1
         use_graph = (self.graphs is not None and not copies and T <= self.graphs.buckets[-1]
-                     and self.temperature == self.graphs.temperature)
+                     and self.temperature == self.graphs.temperature and kv_splits == 1)
         cascade = pre_tokens > 0 and not use_graph
         with span("sched.pack"):
             host, layout = pack_step(entries, BLOCK_SIZE, group, copies,
                                      casc.blocks[:casc_keys // BLOCK_SIZE] if cascade else None,
                                      pre_tokens if cascade else 0, allowed, ctr)
+            if kv_splits > 1:
+                layout = list(layout) + [kv_splits]
+                self.stats["kv_split_steps"] += 1
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
         tok_dev = self.graphs.run(step_from_host(host, layout)) if use_graph else None

@@ -100,7 +100,7 @@ def test_rope_kv(Hq, Hkv):
     assert torch.equal(vc.cpu(), vc2_cpu)
 
 
-def _attn_case(q_lens, ctx_lens, Hq, Hkv, seed=0):
+def _attn_case(q_lens, ctx_lens, Hq, Hkv, seed=0, kv_splits=1):
     torch.manual_seed(seed)
     D, BS = 128, 64
     S = len(q_lens)
@@ -122,6 +122,7 @@ def _attn_case(q_lens, ctx_lens, Hq, Hkv, seed=0):
                       q_len=np.asarray(q_lens, np.int32), ctx_len=np.asarray(ctx_lens, np.int32),
                       block_table=bt, logit_rows=np.zeros(0, np.int32))
     dev = pack(step, Hq // Hkv, DEV)
+    dev.attn.kv_splits = kv_splits
     out = ops.paged_attention(q, kc, vc, dev.attn, 1 / math.sqrt(D))
     exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), torch.from_numpy(qs),
                               torch.tensor(q_lens), torch.tensor(ctx_lens), torch.from_numpy(bt),
@@ -136,6 +137,32 @@ def test_paged_attention_mixed(Hq, Hkv):
     out, exp = _attn_case(q_lens, ctx_lens, Hq, Hkv)
     assert rel_err(out, exp) < 2e-2
     assert torch.isfinite(out.float()).all()
+
+
+@pytest.mark.parametrize("ctx", [8192, 32768, 131072])
+@pytest.mark.parametrize("batch", [1, 4])
+def test_paged_attention_split_kv_long_context(ctx, batch):
+    """Split-KV decode (K6): 1-wave items whose key range is split over
+    workgroups (fp32 partials + LSE, merged by attn_split_combine), at 8k-128k
+    contexts, batch 1 and 4 (one decode token each, plus a 3-token
+    jump-forward span), against fp32; the engine's split rule too."""
+    from mcp_amd.engine.batch import choose_kv_splits
+    q_lens = [1] * batch
+    q_lens[-1] = 3
+    ctx_lens = [ctx - 37 * i for i in range(batch)]
+    ns = choose_kv_splits(q_lens, ctx_lens, 4, 8, hq=32)
+    assert ns > 1
+    out, exp = _attn_case(q_lens, ctx_lens, 32, 8, seed=6, kv_splits=ns)
+    assert rel_err(out, exp) < 2e-2
+    assert torch.isfinite(out.float()).all()
+
+
+def test_paged_attention_split_kv_uneven():
+    """Split counts that do not divide the tiles, splits with no tiles (short
+    contexts), mixed with 4-wave items of the same step."""
+    for ns in (3, 7, 32):
+        out, exp = _attn_case([1, 1, 1, 70, 2], [5000, 65, 900, 700, 64], 32, 8, seed=7, kv_splits=ns)
+        assert rel_err(out, exp) < 2e-2
 
 
 def test_paged_attention_spike():
@@ -223,8 +250,10 @@ def test_topk_cosine(B, N, D, k):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
-def test_cascade_prefix_attention(Hq, Hkv):
-    """Shared-prefix pass + per-sequence pass with LSE merge == full attention."""
+@pytest.mark.parametrize("kv_splits", [1, 4])
+def test_cascade_prefix_attention(Hq, Hkv, kv_splits):
+    """Shared-prefix pass + per-sequence pass with LSE merge == full attention
+    (also with split-KV: split 0 folds the prefix partial in)."""
     torch.manual_seed(5)
     D, BS = 128, 64
     P_full = 640                                   # 10 shared blocks
@@ -255,6 +284,7 @@ def test_cascade_prefix_attention(Hq, Hkv):
                       kv_begin=np.full(len(q_lens), P_full, np.int32),
                       pre_bt=np.asarray(pre, np.int32), pre_tokens=T)
     dev = pack(step, Hq // Hkv, DEV)
+    dev.attn.kv_splits = kv_splits
     assert dev.attn.pre_tokens == T and dev.attn.pre_keys == P_full
     out = ops.paged_attention(q, kc, vc, dev.attn, 1 / math.sqrt(D)).cpu()
     exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), torch.from_numpy(qs),
