@@ -359,7 +359,7 @@ class LLMEngine:
                 # the prefix pass has ~(sharing tokens / 32) x Hkv workgroups: for a
                 # long prefix shared by few sequences that underfills the chip,
                 # while per-sequence attention can split the key range (split-KV)
-                if n_share < 2 or (casc.length >= 16 * BLOCK_SIZE and n_share < 16):
+                if casc.length >= 16 * BLOCK_SIZE and n_share < 16:
                     casc = None
         order = pool
         if casc is not None:
