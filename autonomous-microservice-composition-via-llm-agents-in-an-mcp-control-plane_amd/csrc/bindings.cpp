@@ -203,6 +203,22 @@ void segment_topk(const at::Tensor& vals, const c10::optional<at::Tensor>& idx, 
   check_launch("segment_topk");
 }
 
+void topk_fused(const at::Tensor& Q, const at::Tensor& E, int64_t k, at::Tensor& cand_v,
+                at::Tensor& cand_i) {
+  CHECK_BF16_TENSOR(Q); CHECK_BF16_TENSOR(E);
+  TORCH_CHECK(Q.dim() == 2 && E.dim() == 2 && Q.size(1) == E.size(1), "Q [B, D], E [N, D]");
+  const int B = Q.size(0), N = E.size(0), D = Q.size(1);
+  const int nseg = topk_fused_segments(N);
+  TORCH_CHECK(cand_v.scalar_type() == at::kFloat && cand_v.is_contiguous() &&
+              cand_v.numel() == (int64_t)B * nseg * k, "cand_v [B, nseg, k] f32");
+  CHECK_I32_TENSOR(cand_i);
+  TORCH_CHECK(cand_i.numel() == cand_v.numel(), "cand_i shape");
+  const int rc = launch_topk_fused(Q.data_ptr(), E.data_ptr(), B, N, D, (int)k,
+                                   cand_v.data_ptr<float>(), cand_i.data_ptr<int>(), stream());
+  TORCH_CHECK(rc == 0, "topk_fused: B <= 64, k <= 64, D in {512, 1024} (code ", rc, ")");
+  check_launch("topk_fused");
+}
+
 void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                      at::Tensor& out, const at::Tensor& q_start, const at::Tensor& q_len,
                      const at::Tensor& ctx_len, const at::Tensor& block_table,
@@ -427,6 +443,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_silu", &gemm_silu);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);
+  m.def("topk_fused", &topk_fused, py::arg("Q"), py::arg("E"), py::arg("k"), py::arg("cand_v"),
+        py::arg("cand_i"));
+  m.def("topk_fused_segments", &topk_fused_segments);
   m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),
         py::arg("k"), py::arg("out_v"), py::arg("out_i"));
   m.def("paged_attention", &paged_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),

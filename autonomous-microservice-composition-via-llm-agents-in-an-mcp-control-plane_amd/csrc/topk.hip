@@ -6,6 +6,8 @@
 //     scores into LDS and extracts the k largest by repeated block argmax in
 //     which only the owning thread of the last winner rescans its 16 values.
 //     Applied hierarchically (N -> N/4096*k -> ... -> k) it handles 10^8 rows.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -142,6 +144,11 @@ int launch_segment_topk(const float* vals, const int* idx_in, int B, int L, int 
 //    After the first few blocks almost nothing passes tau.
 //  * the segment's top k per query (rank order) go to cand[B][nseg][k]; the
 //    hierarchical segment_topk above merges the segments.
+// Measured (profiles/config3_topk.md): 10M x 1024 rows in 3.9 / 4.2 / 10.0 ms
+// for 1 / 16 / 64 queries.  At 64 queries the 4 waves of a workgroup each
+// pull the same rows through L1/L2; a barrier per block to keep them in step
+// was slower (11.7 ms).  Sharing the rows through an LDS ring is the next
+// step for wide query batches.
 namespace {
 constexpr int FT_CAP = 128;
 constexpr int FT_SEGR = 4096;
@@ -150,7 +157,7 @@ template <int NS>
 __global__ __launch_bounds__(256) void topk_fused_kernel(const bf16* __restrict__ Q,
                                                           const bf16* __restrict__ E, int B,
                                                           int N, int k, float* __restrict__ cand_v,
-                                                          int* __restrict__ cand_i) {
+                                                          int* __restrict__ cand_i, int sync_waves) {
   constexpr int D = NS * 32;
   // per wave (dynamic LDS, so a 1-wave workgroup takes 16.5 KiB, not 66):
   // candidate values [16][CAP], indices [16][CAP], counts [16], thresholds [16]
@@ -209,20 +216,25 @@ __global__ __launch_bounds__(256) void topk_fused_kernel(const bf16* __restrict_
   // unrolled by NS so that s (the query fragment) and the ring slot are static
   static_assert(NS % 16 == 0, "ring of 16 d-steps");
   bf16x8 ring[16];
-  auto load = [&](int slot, int t) {
-    const int b = t / NS, s = t % NS;
-    if (b < nblk)
-      ring[slot] = *reinterpret_cast<const bf16x8*>(
-          E + (size_t)(row0 + min(16 * b + r, rows - 1)) * D + 8 * g + 32 * s);
+  auto rowp = [&](int b) {                             // this lane's row of block b
+    return E + (size_t)(row0 + min(16 * b + r, rows - 1)) * D + 8 * g;
   };
+  {
+    const bf16* p0 = rowp(0);
+    const bf16* p1 = rowp(1);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) load(j, j);
+    for (int j = 0; j < 16; ++j)
+      ring[j] = *reinterpret_cast<const bf16x8*>((j < NS ? p0 + 32 * j : p1 + 32 * (j - NS)));
+  }
   for (int b = 0; b < nblk; ++b) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16* pc = rowp(b);
+    const bf16* pn = rowp(min(b + 1, nblk - 1));      // past the end: re-read, unused
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       acc = mfma16x16x32(ring[s % 16], qf[s], acc);
-      load(s % 16, b * NS + s + 16);
+      const int sn = s + 16;                         // prefetch 16 d-steps ahead
+      ring[s % 16] = *reinterpret_cast<const bf16x8*>(sn < NS ? pc + 32 * sn : pn + 32 * (sn - NS));
     }
     // block b done: lane holds rows 4 g + i of query r
     if (q < B) {

@@ -266,26 +266,48 @@ def l2norm_rows(x):
     return x
 
 
-def topk_cosine(queries, corpus, k: int, seg_len: int = 4096):
+def topk_cosine(queries, corpus, k: int, seg_len: int = 4096, n_valid: Optional[int] = None,
+                fused: bool = True):
     """Top-k cosine similarity of unit-norm ``queries`` [B, D] against unit-norm
-    ``corpus`` [N, D] (both bf16).  Returns (scores [B, k] f32, index [B, k] int32).
+    ``corpus`` [N, D] (both bf16).  Returns (scores [B, k] f32, index [B, k] int32),
+    best first (ties: lower row first).
 
-    GPU: fp32-output MFMA GEMM for the scores, then hierarchical segmented
-    top-k selection (csrc/topk.hip) until one segment remains."""
+    GPU, B <= 64, k <= 64, D in {512, 1024}: the fused kernel (csrc/topk.hip
+    ``topk_fused``) scores 4096-row segments with MFMA and keeps each
+    segment's k best per query in LDS - no [B, N] score matrix, no padding of
+    the corpus - then the hierarchical segmented top-k merges the
+    ``N / 4096 x k`` candidates.  Other shapes: fp32-output scoring GEMM +
+    segmented top-k (the scoring GEMM needs N % 4: such corpora are padded at
+    index build, ``retrieval.store``; ``n_valid`` = the real rows, the rest
+    are never returned)."""
+    use_fused = fused and queries.shape[0] <= 64 and k <= 64 and queries.shape[1] in (512, 1024)
+    if n_valid is not None and n_valid < corpus.shape[0] and (not queries.is_cuda or use_fused):
+        corpus = corpus[:n_valid]                  # a row prefix: contiguous, no copy
+        n_valid = None
     B, N = queries.shape[0], corpus.shape[0]
     k = min(k, N)
     if not queries.is_cuda:
         v, i = torch.topk(queries.float() @ corpus.float().t(), k=k, dim=-1)
         return v, i.int()
     L_ = lib()
-    N4 = (N + 3) // 4 * 4                 # the scoring GEMM writes 16-B column groups
-    if N4 != N:
-        corpus = torch.nn.functional.pad(corpus, (0, 0, 0, N4 - N))
-    scores = torch.empty(B, N4, device=queries.device, dtype=torch.float32)
-    L_.gemm_f32out(queries, corpus, scores)
-    if N4 != N:
-        scores[:, N:] = float("-inf")
-    vals, idx, L = scores, None, N4
+    D = queries.shape[1]
+    if use_fused:
+        nseg = L_.topk_fused_segments(N)
+        vals = torch.empty(B, nseg * k, device=queries.device, dtype=torch.float32)
+        idx = torch.empty(B, nseg * k, device=queries.device, dtype=torch.int32)
+        L_.topk_fused(queries.contiguous(), corpus, k, vals, idx)
+        L = nseg * k
+        if nseg == 1:
+            return vals, idx
+    else:
+        if N % 4:
+            raise ValueError("unfused top-k path: pad the corpus rows to a multiple of 4 "
+                             "once at index build (retrieval.store.SchemaIndex does)")
+        vals = torch.empty(B, N, device=queries.device, dtype=torch.float32)
+        L_.gemm_f32out(queries, corpus, vals)
+        if n_valid is not None and n_valid < N:
+            vals[:, n_valid:] = float("-inf")
+        idx, L = None, N
     while True:
         sl = min(seg_len, max(L, k))
         nseg = (L + sl - 1) // sl

@@ -46,7 +46,11 @@ class ShardedIndex:
             shard, offset = full_or_shard[lo:hi], lo
         else:
             shard = full_or_shard
-        v = shard.to(self.device, torch.bfloat16).contiguous()
+        v = shard.to(self.device, torch.bfloat16)
+        self.n_local = int(v.shape[0])
+        if self.n_local % 4:                      # pad once here, never per query
+            v = torch.cat([v, v.new_zeros(4 - self.n_local % 4, v.shape[1])])
+        v = v.contiguous()
         self.vectors = ops.l2norm_rows(v) if v.shape[0] else v
         self.offset, self.total = int(offset), int(total)
 
@@ -56,11 +60,11 @@ class ShardedIndex:
         q = queries.to(self.device, torch.bfloat16).contiguous()
         B = q.shape[0]
         k = min(k, self.total)
-        kl = min(k, self.vectors.shape[0])
+        kl = min(k, self.n_local)
         vals = torch.full((B, k), float("-inf"), device=self.device, dtype=torch.float32)
         ids = torch.full((B, k), -1, device=self.device, dtype=torch.int64)
         if kl > 0:
-            v, i = ops.topk_cosine(q, self.vectors, kl)
+            v, i = ops.topk_cosine(q, self.vectors, kl, n_valid=self.n_local)
             vals[:, :kl] = v
             ids[:, :kl] = i.long() + self.offset
         if self.world == 1:

@@ -53,7 +53,14 @@ class SchemaIndex:
         self.vectors: Optional[torch.Tensor] = None     # [N, dim] bf16, unit rows
 
     def set_vectors(self, names: Sequence[str], vectors) -> None:
-        v = torch.as_tensor(vectors).to(self.device, torch.bfloat16).contiguous()
+        """Upload and normalise the corpus once.  Rows are padded to a multiple
+        of 4 here (zero rows, never returned: ``n_valid``) so no query ever
+        copies the corpus (the unfused scoring GEMM writes 16-B column groups)."""
+        v = torch.as_tensor(vectors).to(self.device, torch.bfloat16)
+        n = v.shape[0]
+        if n % 4:
+            v = torch.cat([v, v.new_zeros(4 - n % 4, v.shape[1])])
+        v = v.contiguous()
         ops.l2norm_rows(v)
         self.names, self.vectors = list(names), v
 
@@ -72,7 +79,8 @@ class SchemaIndex:
         return ops.l2norm_rows(q.contiguous())
 
     def search_names(self, intents: Sequence[str], k: int):
-        vals, idx = ops.topk_cosine(self.embed_queries(intents), self.vectors, k)
+        vals, idx = ops.topk_cosine(self.embed_queries(intents), self.vectors, k,
+                                    n_valid=len(self.names))
         idx = idx.cpu().tolist()
         return [[self.names[i] for i in row if 0 <= i < len(self.names)] for row in idx], vals.cpu()
 

@@ -232,14 +232,25 @@ def test_copy_blocks():
     assert torch.equal(data, exp)
 
 
-@pytest.mark.parametrize("B,N,D,k", [(1, 10000, 1024, 32), (4, 70000, 256, 64), (3, 50, 128, 8)])
+@pytest.mark.parametrize("B,N,D,k", [(1, 10000, 1024, 32), (4, 70000, 256, 64), (3, 50, 128, 8),
+                                     (64, 1_000_003, 1024, 32), (16, 300001, 512, 64),
+                                     (5, 4095, 1024, 10), (64, 4097, 1024, 64), (17, 9000, 1024, 1),
+                                     (33, 20000, 512, 64)])
 def test_topk_cosine(B, N, D, k):
+    """Fused scoring + per-segment top-k (B <= 64, D in {512, 1024}) and the
+    unfused GEMM path (other D; corpus padded to a multiple of 4 once, the pad
+    rows never returned): values equal torch's top-k, indices point at rows
+    with those scores (ties may pick another row), best first."""
     torch.manual_seed(2)
-    corpus = torch.randn(N, D, device=DEV).bfloat16()
+    Np = (N + 3) // 4 * 4 if D not in (512, 1024) else N
+    corpus = torch.randn(Np, D, device=DEV).bfloat16()
+    corpus[N:] = 0
     ops.l2norm_rows(corpus)
     q = torch.randn(B, D, device=DEV).bfloat16()
     ops.l2norm_rows(q)
-    vals, idx = ops.topk_cosine(q, corpus, k)
+    vals, idx = ops.topk_cosine(q, corpus, k, n_valid=N)
+    corpus = corpus[:N]
+    assert int(idx.max()) < N and int(idx.min()) >= 0
     ref_s = q.float() @ corpus.float().t()
     rv, ri = torch.topk(ref_s, k=min(k, N), dim=-1)
     assert torch.allclose(vals, rv, atol=1e-4)
