@@ -157,7 +157,7 @@ template <int NS>
 __global__ __launch_bounds__(256) void topk_fused_kernel(const bf16* __restrict__ Q,
                                                           const bf16* __restrict__ E, int B,
                                                           int N, int k, float* __restrict__ cand_v,
-                                                          int* __restrict__ cand_i, int sync_waves) {
+                                                          int* __restrict__ cand_i) {
   constexpr int D = NS * 32;
   // per wave (dynamic LDS, so a 1-wave workgroup takes 16.5 KiB, not 66):
   // candidate values [16][CAP], indices [16][CAP], counts [16], thresholds [16]
