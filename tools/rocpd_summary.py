@@ -13,7 +13,8 @@ from collections import defaultdict
 
 CATS = [("gemm (MFMA 256x256, AGPR 1 wave/SIMD)", r"gemm_tn_256d"),
         ("gemm (MFMA 256x256)", r"gemm_tn_256"), ("gemm (MFMA 128x128)", r"gemm_tn_128"),
-        ("gemm (skinny K2)", r"gemm_skinny"), ("attention", r"attn_"),
+        ("gemm (skinny K2)", r"gemm_skinny"), ("gemm (K2 weight-streaming)", r"gemm_stream|stream_"),
+        ("split-K reduce", r"splitk_reduce"), ("attention", r"attn_"),
         ("sampling", r"sample_"), ("rmsnorm", r"rmsnorm"), ("rope+kv write", r"rope"),
         ("embedding", r"embedding"), ("top-k", r"topk|l2norm"), ("kv copy", r"copy_blocks"),
         ("all-reduce", r"car_|nccl|rccl"), ("torch/other", r".")]
