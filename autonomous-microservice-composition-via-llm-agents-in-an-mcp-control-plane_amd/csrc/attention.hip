@@ -70,6 +70,10 @@ struct AttnArgs {
   const int* pre_bt;       // MODE 1: block table of the shared prefix
   int pre_keys;            // MODE 1: prefix keys (multiple of 64)
   int pre_tokens;          // MODE 1: query tokens [0, pre_tokens) of the flat batch
+  // MODE 1 inside a captured hipGraph: device [pre_tokens, pre_keys] read by
+  // the kernel (the grid covers the bucket's token capacity; items past
+  // pre_tokens exit, pre_tokens = 0 = no cascade this step)
+  const int* pre_dims;
 };
 
 // MODE 0: per (sequence, q-tile) work item, causal over keys
@@ -99,14 +103,17 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   bool qvalid;
   const int* bt;
   if (MODE == 1) {
+    const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
+    const int pre_keys = a.pre_dims ? a.pre_dims[1] : a.pre_keys;
+    if ((int)blockIdx.x * QT >= pre_tokens) return;      // whole block idle (before any barrier)
     tok = blockIdx.x * QT + wave * TPW + fr / G;          // flat token index
-    qvalid = tok < a.pre_tokens;
+    qvalid = tok < pre_tokens;
     qs = 0;
-    ql = a.pre_tokens;
-    cl = a.pre_keys;
+    ql = pre_tokens;
+    cl = pre_keys;
     qpos = 1 << 30;                                       // no causal limit inside the prefix
     kt0 = 0;
-    ntiles = a.pre_keys / KT;
+    ntiles = pre_keys / KT;
     bt = a.pre_bt;
   } else {
     s = a.work_seq[blockIdx.x];
@@ -479,10 +486,13 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
 
 int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
                             float* lse_out, const int* pre_bt, int pre_keys, int pre_tokens,
-                            int Hq, int Hkv, int head_dim, float scale, hipStream_t s) {
+                            int Hq, int Hkv, int head_dim, float scale, hipStream_t s,
+                            const int* pre_dims) {
+  // pre_dims != null: pre_tokens is the grid's token capacity, the actual
+  // [pre_tokens, pre_keys] are read on the device (hipGraph replay)
   if (head_dim != D) return 1;
-  if (pre_keys % KT) return 2;
-  if (pre_tokens <= 0 || pre_keys <= 0) return 0;
+  if (!pre_dims && pre_keys % KT) return 2;
+  if (pre_tokens <= 0 || (!pre_dims && pre_keys <= 0)) return 0;
   AttnArgs a{};
   a.q = (const bf16*)q;
   a.kc = (const bf16*)k_cache;
@@ -495,6 +505,7 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
   a.pre_bt = pre_bt;
   a.pre_keys = pre_keys;
   a.pre_tokens = pre_tokens;
+  a.pre_dims = pre_dims;
   ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s))
   return 0;
 }

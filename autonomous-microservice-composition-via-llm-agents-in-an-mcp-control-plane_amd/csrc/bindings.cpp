@@ -273,17 +273,26 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
 
 void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                       at::Tensor& out, at::Tensor& lse, const at::Tensor& pre_bt, int64_t pre_keys,
-                      int64_t pre_tokens, double scale) {
+                      int64_t pre_tokens, double scale,
+                      const c10::optional<at::Tensor>& pre_dims) {
   CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
   CHECK_I32_TENSOR(pre_bt); CHECK_DEV(lse); CHECK_CONTIG(lse);
   TORCH_CHECK(lse.scalar_type() == at::kFloat, "lse f32");
   const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
   TORCH_CHECK(out.sizes() == q.sizes() && lse.numel() == q.size(0) * Hq, "prefix attention shapes");
   TORCH_CHECK(pre_tokens <= q.size(0) && pre_bt.numel() * 64 >= pre_keys, "prefix ranges");
+  const int* dims = nullptr;
+  if (pre_dims.has_value()) {
+    // device-side [pre_tokens, pre_keys]: the kernel trusts pre_keys <= 64 *
+    // pre_bt.numel(); the graph packer (engine/graphs.py) guarantees it
+    CHECK_I32_TENSOR((*pre_dims));
+    TORCH_CHECK(pre_dims->numel() == 2, "pre_dims [2]");
+    dims = pre_dims->data_ptr<int>();
+  }
   const int rc = launch_prefix_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                          out.data_ptr(), lse.data_ptr<float>(),
                                          pre_bt.data_ptr<int>(), pre_keys, pre_tokens, Hq, Hkv, D,
-                                         (float)scale, stream());
+                                         (float)scale, stream(), dims);
   TORCH_CHECK(rc == 0, "prefix_attention: unsupported config (code ", rc, ")");
   check_launch("prefix_attention");
 }
@@ -454,7 +463,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
         py::arg("pre_lse") = py::none(), py::arg("nsplit") = 1, py::arg("split_o") = py::none(),
         py::arg("split_lse") = py::none());
-  m.def("prefix_attention", &prefix_attention);
+  m.def("prefix_attention", &prefix_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("out"), py::arg("lse"), py::arg("pre_bt"), py::arg("pre_keys"),
+        py::arg("pre_tokens"), py::arg("scale"), py::arg("pre_dims") = py::none());
   m.def("attn_tokens_per_item", &attn_tokens_per_item);
   m.def("sample_allowed", &sample_allowed, py::arg("hidden"), py::arg("W"), py::arg("allow_ptr"),
         py::arg("allow_ids"), py::arg("ctr"), py::arg("temperature"), py::arg("seed"),

@@ -222,13 +222,17 @@ void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s) {
 
 // ------------------------------------------------------- KV block copy (CoW)
 // data: [L, 2, num_blocks, block_elems]; copies block src[i] -> dst[i] for every
-// layer and K/V (prefix-cache tail blocks).  16 B per lane.
+// layer and K/V (prefix-cache tail blocks).  16 B per lane; pairs with a
+// negative block id are skipped.
 __global__ __launch_bounds__(256) void copy_blocks_kernel(bf16* __restrict__ data,
                                                           const int* __restrict__ src,
                                                           const int* __restrict__ dst, int npairs,
                                                           int nb, int block_vecs) {
   const int pair = blockIdx.x % npairs;
   const int lk = blockIdx.x / npairs;           // layer * 2 + kv
+  // a negative pair is padding (the fixed-capacity copy list of a captured
+  // hipGraph step): the whole workgroup skips it
+  if (src[pair] < 0 || dst[pair] < 0) return;
   bf16x8* base = reinterpret_cast<bf16x8*>(data) + (size_t)lk * nb * block_vecs;
   const bf16x8* s = base + (size_t)src[pair] * block_vecs;
   bf16x8* d = base + (size_t)dst[pair] * block_vecs;

@@ -38,6 +38,9 @@ class AttnMeta:
     pre_keys: int = 0                         # shared prefix keys (multiple of 64)
     pre_tokens: int = 0                       # flat tokens [0, pre_tokens) attend to it
     kv_splits: int = 1                        # split-KV factor of the 1-wave items (K6)
+    # hipGraph steps: device [pre_tokens, pre_keys] (the host ints above are
+    # then the bucket's capacities, engine/graphs.py)
+    pre_dims: Optional[torch.Tensor] = None
 
     def work_lists(self):
         return self.work
@@ -332,6 +335,11 @@ def views(t: torch.Tensor, layout):
     if pre_tokens > 0:
         meta.kv_begin, meta.pre_bt = vs[14], vs[15]
         meta.pre_keys, meta.pre_tokens = int(vs[15].numel()) * BLOCK_SIZE, pre_tokens
+    elif pre_tokens < 0:
+        # static (hipGraph) layout: segment 15 = [pre_tokens, pre_keys, blocks...]
+        # read on the device; capacities: the step's token count and the blocks
+        meta.kv_begin, meta.pre_dims, meta.pre_bt = vs[14], vs[15][:2], vs[15][2:]
+        meta.pre_keys, meta.pre_tokens = int(vs[15].numel() - 2) * BLOCK_SIZE, int(vs[0].numel())
     d = DeviceStep(token_ids=vs[0], positions=vs[1], slots=vs[2], logit_rows=vs[3], attn=meta)
     d.allow_ptr, d.allow_ids, d.sample_ctr = vs[16], vs[17], vs[18]
     return d, vs[12], vs[13]

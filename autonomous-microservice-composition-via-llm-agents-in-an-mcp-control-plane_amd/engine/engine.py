@@ -96,11 +96,14 @@ class LLMEngine:
         self.device = model.device
         self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
         self.cascade = cascade      # shared-prefix (cascade) attention
-        # two launch cohorts in flight: the host schedules / updates one cohort
-        # while the GPU runs the other's forward (no idle GPU between steps)
+        # optional two launch cohorts in flight: the host schedules / updates one
+        # cohort while the GPU runs the other's forward.  Off by default: every
+        # cohort step streams all the weights again, so a request waits two
+        # weight-bound steps per sampled token; measured on one MI355X at 40 / 80
+        # / 160 intents/s (config 5) p50 368 / 464 / 594 ms with cohorts against
+        # 194 / 242 / 572 ms without (profiles/config5_pipeline_ab.jsonl)
         if pipeline is None:
-            env = os.environ.get("MCP_PIPELINE", "auto")
-            pipeline = self.device.type == "cuda" if env == "auto" else env == "1"
+            pipeline = os.environ.get("MCP_PIPELINE", "0") == "1"
         self.pipeline = pipeline
         self.inflight: Dict[int, _Launch] = {}
         self.last_progress = time.perf_counter()   # watched by the planner's stall watchdog
@@ -128,8 +131,9 @@ class LLMEngine:
         self.steps = 0
         if self._graphs_wanted:
             from .graphs import GraphRunner
-            self.graphs = GraphRunner(model, self.kv, temperature, seed)
-        self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "kv_split_steps": 0,
+            self.graphs = GraphRunner(model, self.kv, temperature, seed, max_seqs=max_batch)
+        self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "graph_cow_steps": 0,
+                      "graph_split_steps": 0, "kv_split_steps": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
@@ -396,15 +400,17 @@ class LLMEngine:
         if sample_seqs:            # grammar masks go in the same single H2D copy
             allowed = [q.decoder.allowed() for q in sample_seqs]
             ctr = [(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF for q in sample_seqs]
-        # split-KV for few long-context decode sequences (K6); such steps run
-        # eager (the captured buckets use the unsplit kernel)
+        # a step that fits a captured bucket replays its hipGraph (prefix
+        # copy-on-write, cascade and split-KV attention included)
+        use_graph = (self.graphs is not None and T <= self.graphs.buckets[-1]
+                     and self.temperature == self.graphs.temperature)
+        cascade = pre_tokens > 0
+        # split-KV for few long-context decode sequences (K6), over the keys
+        # each sequence attends itself (after the cascade prefix, if any)
         kv_splits = choose_kv_splits(
             [e[1] for e in entries],
-            [e[2] + e[1] - (e[4] if pre_tokens else 0) for e in entries],
+            [e[2] + e[1] - (e[4] if cascade else 0) for e in entries],
             group, self.model.hkv, hq=self.model.hq) if self.device.type == "cuda" else 1
-        use_graph = (self.graphs is not None and not copies and T <= self.graphs.buckets[-1]
-                     and self.temperature == self.graphs.temperature and kv_splits == 1)
-        cascade = pre_tokens > 0 and not use_graph
         with span("sched.pack"):
             host, layout = pack_step(entries, BLOCK_SIZE, group, copies,
                                      casc.blocks[:casc_keys // BLOCK_SIZE] if cascade else None,
@@ -414,15 +420,21 @@ class LLMEngine:
                 self.stats["kv_split_steps"] += 1
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched
-        tok_dev = self.graphs.run(step_from_host(host, layout)) if use_graph else None
+        tok_dev = self.graphs.run(step_from_host(host, layout), copies, kv_splits) \
+            if use_graph else None
         if tok_dev is not None:            # replayed hipGraph: forward + sampling
             self.stats["graph_steps"] += 1
+            self.stats["graph_cow_steps"] += bool(copies)
+            self.stats["graph_split_steps"] += kv_splits > 1
             self.stats["samples"] += len(sample_seqs)
             tokens, event = self._fetch(tok_dev[:len(sample_seqs)])
         else:
             hidden, dstep = self._launch(host, layout)
             tokens, event = self._sample(hidden, dstep, len(sample_seqs))
         self.stats["launch_s"] += time.perf_counter() - t0
+        if self.graphs is not None:
+            self.stats["graph_captures"] = self.graphs.captures
+            self.stats["graph_capture_s"] = round(self.graphs.capture_s, 3)
         self.stats["tokens"] += T
         self.stats["steps"] += 1
         self.steps += 1
@@ -502,6 +514,13 @@ class LLMEngine:
         ev = torch.cuda.Event()
         ev.record()
         return host, ev
+
+    def warm_graphs(self, max_tokens: Optional[int] = None, contexts=(2048,)) -> int:
+        """Capture the hipGraph buckets ahead of serving (server start-up);
+        0 when graphs are off."""
+        if self.graphs is None:
+            return 0
+        return self.graphs.warm(max_tokens, contexts)
 
     # -------------------------------------------------------------- driver
     def run(self, max_steps: int = 1_000_000):

@@ -1,33 +1,43 @@
-"""hipGraph capture of small engine steps (SURVEY §2.6 "hipGraph bucket
-capture", BASELINE config 5: continuous-batching decode, hipGraph).
+"""hipGraph capture of engine steps (SURVEY §2.6 "hipGraph bucket capture",
+BASELINE config 5: continuous-batching decode, hipGraph).
 
-A small step (a few concurrent requests, a decode / jump-forward span each)
-costs ~2.5 ms of weight streaming on the GPU but ~260 kernel launches
-(32 layers x 8 ops + sampling); issued one by one from Python the launches,
-not the GPU, set the step time.  Steps with at most ``max(BUCKETS)`` tokens are
-therefore replayed from a captured hipGraph (``torch.cuda.CUDAGraph`` is the
-HIP graph API on ROCm):
+A serving step (tens of concurrent requests, a decode / jump-forward span
+each, a few hundred tokens) costs a few ms of weight streaming on the GPU but
+~300 kernel launches (32 layers x 9 ops + sampling); issued one by one from
+Python the launches, not the GPU, set the step time.  Steps with at most
+``max(BUCKETS)`` tokens are therefore replayed from a captured hipGraph
+(``torch.cuda.CUDAGraph`` is the HIP graph API on ROCm).  A graph is keyed by
+(token bucket, block-table width class, split-KV factor) and captured lazily
+on first use, after one eager warm-up of the same static step.  Every step of
+a key uses ONE fixed int32 layout (``pack_static``):
 
-* every step of a bucket uses ONE fixed int32 layout (``pack_static``):
-  tokens padded to the bucket size (padding writes no KV: slot -1), sequence
-  arrays padded with empty dummy sequences, attention work lists padded with
-  work items of an empty sequence (the kernel's early exit), a block table of
-  fixed width, grammar-allowed sets padded to empty rows;
-* the per-step H2D copy lands in the bucket's static device buffer, then the
-  graph replays forward + fused LM-head/grammar/sampling (K9) and leaves the
-  tokens in a static output;
-* the sampler's RNG counter (request uid, sample index) travels in the
-  buffer and the seed is constant, so nothing in the graph changes per step.
-
-Cascade attention and KV copy-on-write are eager-only: a step that needs them
-(a large batch sharing a prefix, or a request just attached to its prefix)
-runs eagerly.  The capture happens lazily on first use of a bucket, after one
-eager warm-up of the same static step.
+* tokens padded to the bucket size (padding writes no KV: slot -1), sequence
+  arrays padded with empty dummy sequences (at most ``max_seqs`` real ones),
+  attention work lists padded with work items of an empty sequence (the
+  kernel's early exit), a block table of the class width (32, 128, 512, ...
+  blocks: a long-context step does not make every short step ship a
+  128k-position table), grammar-allowed sets padded to empty rows;
+* prefix copy-on-write block pairs padded with (-1, -1) (the copy kernel skips
+  them), copied inside the graph ahead of the forward - a step that attaches
+  new requests to a shared prefix replays like any other;
+* long-context low-batch steps keep their split-KV decode attention (K6): the
+  split factor is part of the key and its fp32 partials live in the graph pool;
+* the per-step H2D copy lands in the key's static device buffer, then the
+  graph replays copies + forward + fused LM-head/grammar/sampling (K9) and
+  leaves the tokens in a static output; the sampler's RNG counter (request
+  uid, sample index) travels in the buffer and the seed is constant, so
+  nothing in the graph changes per step;
+* cascade (shared-prefix) attention replays too: the prefix pass is launched
+  over the bucket's token capacity and reads [pre_tokens, pre_keys] from the
+  buffer (pre_tokens 0 = no cascade this step, every item exits at once),
+  the per-sequence first own key (kv_begin) and the prefix block ids travel
+  in it as well.
 """
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Optional
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -35,50 +45,76 @@ import torch
 from .. import ops
 from .batch import BLOCK_SIZE, HostStager, StepInputs, build_work, tokens_per_item, views
 
-BUCKETS = (16, 32, 64, 128, 256)
+# token buckets: every 64 rows above 64 (the GEMM tile plan's M granularity,
+# so padding a step to its bucket adds no MFMA tiles), finer below (the
+# weight-streaming kernel's M classes); measured at 80 intents/s, power-of-two
+# buckets padded a 300-token step to 512 and cost 12 % of p50
+BUCKETS = (8, 16, 32, 48, 64) + tuple(range(128, 1025, 64))
 ALLOWED_PER_ROW = 64
+MAX_COPIES = 64
+MIN_WIDTH = 32                 # block-table width classes: 32, 128, 512, ... blocks (x4)
 
 
 @dataclasses.dataclass
 class _Bucket:
-    size: int
+    key: Tuple[int, int, int]
     sizes: List[int]
     S: int
     buf: torch.Tensor
     graph: object = None
     tokens: Optional[torch.Tensor] = None
     dstep: object = None
+    csrc: Optional[torch.Tensor] = None
+    cdst: Optional[torch.Tensor] = None
 
 
 class GraphRunner:
-    def __init__(self, model, kv, temperature: float, seed: int, buckets=BUCKETS):
+    def __init__(self, model, kv, temperature: float, seed: int, buckets=BUCKETS,
+                 max_seqs: int = 256):
         self.model, self.kv = model, kv
         self.device = model.device
         self.group = model.cfg.group
         self.mblk = (model.cfg.max_pos + BLOCK_SIZE - 1) // BLOCK_SIZE
         self.temperature, self.seed = float(temperature), int(seed)
         self.buckets = tuple(sorted(buckets))
-        self._b: Dict[int, _Bucket] = {}
+        self.max_seqs = int(max_seqs)
+        self._b: Dict[Tuple[int, int, int], _Bucket] = {}
         self._pool = None
         self.stager = HostStager(self.device)
         self.replays = 0
+        self.captures = 0
+        self.capture_s = 0.0
 
     # ---------------------------------------------------------------- layout
     def _caps(self, b: int):
         t1 = tokens_per_item(1, self.group)
         t4 = tokens_per_item(4, self.group)
-        S = b + 1                          # >= one empty dummy sequence
+        S = min(b, self.max_seqs) + 1      # >= one empty dummy sequence
         cap1 = b
         cap4 = b // t4 + b // (2 * t1) + 1
         return S, cap1, cap4, S * ALLOWED_PER_ROW
 
-    def _sizes(self, b: int) -> List[int]:
-        S, cap1, cap4, A = self._caps(b)
-        # same part order as batch.pack_host / views
-        return [b, b, b, S, S, S, S, S * self.mblk, cap1, cap1, cap4, cap4, 0, 0, 0, 0,
-                S + 1, A, S]
+    def _ncopy(self, b: int) -> int:
+        return min(self._caps(b)[0], MAX_COPIES)
 
-    def bucket_for(self, step: StepInputs) -> Optional[int]:
+    def _sizes(self, b: int, width: Optional[int] = None) -> List[int]:
+        S, cap1, cap4, A = self._caps(b)
+        w = self.mblk if width is None else width
+        C = self._ncopy(b)
+        # same part order as batch.pack_host / views
+        return [b, b, b, S, S, S, S, S * w, cap1, cap1, cap4, cap4, C, C, S, 2 + w, S + 1, A, S]
+
+    def width_for(self, need: int) -> Optional[int]:
+        """Block-table width class for a step whose longest table has ``need``
+        blocks (None past the model's context)."""
+        if need > self.mblk:
+            return None
+        w = MIN_WIDTH
+        while w < need:
+            w *= 4
+        return min(w, self.mblk)
+
+    def bucket_for(self, step: StepInputs, ncopies: int = 0) -> Optional[int]:
         T = step.num_tokens
         S = int(step.q_len.shape[0])
         A = int(step.allow_ids.shape[0]) if step.allow_ids is not None else 0
@@ -86,12 +122,15 @@ class GraphRunner:
             return None
         for b in self.buckets:
             Sb, _, _, Acap = self._caps(b)
-            if T <= b and S < Sb and A <= Acap:
+            if T <= b and S < Sb and A <= Acap and ncopies <= self._ncopy(b):
                 return b
         return None
 
-    def pack_static(self, step: Optional[StepInputs], b: int) -> Optional[np.ndarray]:
+    def pack_static(self, step: Optional[StepInputs], b: int, width: Optional[int] = None,
+                    copies: Sequence = ()) -> Optional[np.ndarray]:
         S_b, cap1, cap4, A_cap = self._caps(b)
+        w = self.mblk if width is None else width
+        C = self._ncopy(b)
         T = step.num_tokens if step is not None else 0
         S = int(step.q_len.shape[0]) if step is not None else 0
         ids = np.zeros(b, np.int32)
@@ -99,15 +138,25 @@ class GraphRunner:
         slots = np.full(b, -1, np.int32)
         rows = np.zeros(S_b, np.int32)
         qs, ql, cl = (np.zeros(S_b, np.int32) for _ in range(3))
-        bt = np.zeros((S_b, self.mblk), np.int32)
+        bt = np.zeros((S_b, w), np.int32)
         ws1 = np.full(cap1, S_b - 1, np.int32)
         wq1 = np.zeros(cap1, np.int32)
         ws4 = np.full(cap4, S_b - 1, np.int32)
         wq4 = np.zeros(cap4, np.int32)
+        csrc = np.full(C, -1, np.int32)
+        cdst = np.full(C, -1, np.int32)
+        kvb = np.zeros(S_b, np.int32)
+        pre = np.zeros(2 + w, np.int32)            # [pre_tokens, pre_keys, prefix blocks]
         aptr = np.zeros(S_b + 1, np.int32)
         aids = np.zeros(A_cap, np.int32)
         ctr = np.zeros(S_b, np.int32)
+        if len(copies) > C:
+            return None
+        for i, (s_, d_) in enumerate(copies):
+            csrc[i], cdst[i] = s_, d_
         if step is not None:
+            if step.block_table.shape[1] > w:
+                return None
             ids[:T], pos[:T], slots[:T] = step.token_ids, step.positions, step.slots
             R = int(step.logit_rows.shape[0])
             rows[:R] = step.logit_rows
@@ -118,6 +167,13 @@ class GraphRunner:
                 return None
             ws1[:len(work[1][0])], wq1[:len(work[1][1])] = work[1][0], work[1][1]
             ws4[:len(work[4][0])], wq4[:len(work[4][1])] = work[4][0], work[4][1]
+            if step.pre_tokens > 0 and step.pre_bt is not None and len(step.pre_bt):
+                nb = len(step.pre_bt)
+                if nb > w:
+                    return None
+                kvb[:S] = step.kv_begin
+                pre[0], pre[1] = step.pre_tokens, nb * BLOCK_SIZE
+                pre[2:2 + nb] = step.pre_bt
             if R:
                 aptr[:R + 1] = step.allow_ptr
                 aptr[R + 1:] = step.allow_ptr[-1]
@@ -126,27 +182,30 @@ class GraphRunner:
                     return None
                 aids[:A] = step.allow_ids
                 ctr[:R] = step.sample_ctr
-        z = np.zeros(0, np.int32)
         return np.concatenate([ids, pos, slots, rows, qs, ql, cl, bt.reshape(-1), ws1, wq1, ws4,
-                               wq4, z, z, z, z, aptr, aids, ctr])
+                               wq4, csrc, cdst, kvb, pre, aptr, aids, ctr])
 
     # ---------------------------------------------------------------- graphs
     def _body(self, e: _Bucket):
+        ops.copy_blocks(self.kv.data, e.csrc, e.cdst)
         hidden = self.model.forward(e.dstep, self.kv)
         return ops.sample_allowed(hidden, self.model.w.lm_head, e.dstep.allow_ptr,
                                   e.dstep.allow_ids, e.dstep.sample_ctr, self.temperature,
                                   self.seed)
 
-    def _get(self, b: int) -> _Bucket:
-        e = self._b.get(b)
+    def _get(self, key: Tuple[int, int, int]) -> _Bucket:
+        e = self._b.get(key)
         if e is not None:
             return e
-        sizes = self._sizes(b)
+        t0 = time.perf_counter()
+        b, w, ns = key
+        sizes = self._sizes(b, w)
         S_b = self._caps(b)[0]
         buf = torch.zeros(sum(sizes), dtype=torch.int32, device=self.device)
-        e = _Bucket(size=b, sizes=sizes, S=S_b, buf=buf)
-        buf.copy_(torch.from_numpy(self.pack_static(None, b)))
-        e.dstep = views(buf, sizes + [S_b, 0])[0]
+        e = _Bucket(key=key, sizes=sizes, S=S_b, buf=buf)
+        buf.copy_(torch.from_numpy(self.pack_static(None, b, w)))
+        # pre_tokens -1: cascade sizes live on the device (batch.views)
+        e.dstep, e.csrc, e.cdst = views(buf, sizes + [S_b, -1, ns])
         self._body(e)                                   # eager warm-up (lazy allocations)
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
@@ -154,20 +213,42 @@ class GraphRunner:
             e.tokens = self._body(e)
         self._pool = g.pool()
         e.graph = g
-        self._b[b] = e
+        self._b[key] = e
+        self.captures += 1
+        self.capture_s += time.perf_counter() - t0
         return e
 
-    def run(self, step: StepInputs) -> Optional[torch.Tensor]:
-        """Replays the bucket's graph for ``step``; returns the device tensor
-        of sampled tokens (first ``len(step.logit_rows)`` entries valid), or
-        None when the step does not fit a bucket."""
-        b = self.bucket_for(step)
+    def warm(self, max_tokens: Optional[int] = None, contexts: Sequence[int] = (2048,),
+             kv_splits: Sequence[int] = (1,)) -> int:
+        """Capture every bucket up to ``max_tokens`` for the block-table width
+        classes of ``contexts`` (tokens) ahead of serving, so no request waits
+        on a lazy capture.  Returns the number of graphs captured."""
+        n0 = self.captures
+        widths = sorted({self.width_for((c + BLOCK_SIZE - 1) // BLOCK_SIZE) or self.mblk
+                         for c in contexts})
+        for b in self.buckets:
+            if max_tokens is not None and b > max_tokens:
+                break
+            for w in widths:
+                for ns in kv_splits:
+                    self._get((b, w, int(ns)))
+        return self.captures - n0
+
+    def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1) -> Optional[torch.Tensor]:
+        """Replays the graph for ``step`` (after the prefix copy-on-write
+        ``copies``); returns the device tensor of sampled tokens (first
+        ``len(step.logit_rows)`` entries valid), or None when the step does
+        not fit a bucket (the caller runs it eagerly)."""
+        b = self.bucket_for(step, len(copies))
         if b is None:
             return None
-        host = self.pack_static(step, b)
+        w = self.width_for(int(step.block_table.shape[1]))
+        if w is None:
+            return None
+        host = self.pack_static(step, b, w, copies)
         if host is None:
             return None
-        e = self._get(b)
+        e = self._get((b, w, int(kv_splits)))
         self.stager.to_device(host, out=e.buf)
         e.graph.replay()
         self.replays += 1

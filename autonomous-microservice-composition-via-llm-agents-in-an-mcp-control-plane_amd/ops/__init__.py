@@ -198,13 +198,15 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
         out = torch.empty_like(q) if out is None else out
         L = lib()
         kw = {}
+        pre_dims = getattr(meta, "pre_dims", None)
         if meta.pre_tokens > 0:
             # cascade: all requests' query tokens vs the shared prefix K/V in full
-            # MFMA tiles, then each request's own keys + LSE merge (csrc/attention.hip)
+            # MFMA tiles, then each request's own keys + LSE merge (csrc/attention.hip);
+            # with device pre_dims (hipGraph) the sizes are read on the device
             pre_o = torch.empty_like(q)
             pre_lse = torch.empty(q.shape[0], q.shape[1], device=q.device, dtype=torch.float32)
             L.prefix_attention(q, k_cache, v_cache, pre_o, pre_lse, meta.pre_bt, meta.pre_keys,
-                               meta.pre_tokens, scale)
+                               meta.pre_tokens, scale, pre_dims=pre_dims)
             kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         ns = int(getattr(meta, "kv_splits", 1))
         for nw, ws, wq in meta.work_lists():
@@ -324,5 +326,6 @@ def copy_blocks(kv_data, src, dst):
     if kv_data.is_cuda:
         lib().copy_blocks(kv_data, src, dst)
     else:
-        kv_data[:, :, dst.long()] = kv_data[:, :, src.long()]
+        keep = (src >= 0) & (dst >= 0)          # negative pairs are padding
+        kv_data[:, :, dst[keep].long()] = kv_data[:, :, src[keep].long()]
     return kv_data

@@ -87,6 +87,9 @@ class LocalPlanner(Planner):
             kw["num_blocks"] = settings.kv_blocks
         eng = LLMEngine(model, max_batch=settings.max_batch, max_step_tokens=settings.max_step_tokens,
                         temperature=settings.temperature, seed=settings.seed, **kw)
+        if os.environ.get("MCP_GRAPH_WARM", "1") == "1":
+            # capture the hipGraph buckets at start-up, not under the first requests
+            eng.warm_graphs(max_tokens=settings.max_step_tokens)
         retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)
         return cls(eng, registry, max_nodes=settings.max_nodes, retriever=retr,
                    retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)

@@ -123,6 +123,9 @@ def main():
     reg = MemoryRegistry(synthetic_registry(args.services, seed=1))
     names = [s.name for s in reg.list_services()]
     planner = LocalPlanner(engine, reg, max_nodes=args.max_nodes, min_nodes=args.min_nodes)
+    t_w = time.perf_counter()
+    ncap = engine.warm_graphs(contexts=(2048,))            # server start-up: capture the buckets
+    warm_s = time.perf_counter() - t_w
     planner.plan_many([synthetic_intent(-1 - i) for i in range(max(1, args.warmup))])
 
     out = {"n_gpus": world, "model": args.model, "services": args.services, "dtype": "bf16",
@@ -159,6 +162,8 @@ def main():
                    value=round(plans_s, 2), unit="plans/s", p50_latency_ms=round(p50 * 1e3, 1),
                    p99_latency_ms=round(p99 * 1e3, 1), mean_running_batch=round(mean_b, 1),
                    graph_steps=engine.stats["graph_steps"], steps=engine.stats["steps"],
+                   graph_captures_startup=ncap, graph_warm_s=round(warm_s, 2),
+                   graph_captures_total=engine.stats.get("graph_captures", 0),
                    duration_s=args.duration,
                    # per-request phases on this rank, p50 in ms
                    phases_p50_ms={k: round(METRICS.windows[k].quantile(0.5) * 1e3, 3)

@@ -22,13 +22,18 @@ def _plans(model, reg, intents, **kw):
     return out, eng
 
 
-def test_graph_replay_matches_eager():
+@pytest.mark.parametrize("cascade", [False, True])
+def test_graph_replay_matches_eager(cascade):
     model = LlamaModel.random("tiny", "cuda", seed=3)
     reg = MemoryRegistry(synthetic_registry(8, seed=2))
     intents = [synthetic_intent(i) for i in range(6)]
-    eager, e1 = _plans(model, reg, intents, graphs=False, cascade=False, pipeline=False)
-    graph, e2 = _plans(model, reg, intents, graphs=True, cascade=False, pipeline=False)
+    eager, e1 = _plans(model, reg, intents, graphs=False, cascade=cascade, pipeline=False)
+    graph, e2 = _plans(model, reg, intents, graphs=True, cascade=cascade, pipeline=False)
     assert e2.stats["graph_steps"] > 0 and e1.stats["graph_steps"] == 0
+    # prefix copy-on-write steps (requests attaching to the shared registry
+    # prefix) replay too, and nearly every step is graphed
+    assert e2.stats["graph_cow_steps"] > 0
+    assert e2.stats["graph_steps"] >= 0.8 * e2.stats["steps"], e2.stats
     assert graph == eager
     names = [s.name for s in reg.list_services()]
     for d in graph:
@@ -149,3 +154,19 @@ def test_gqa_padded_group3_model_on_gpu_matches_cpu_and_plans():
     for d in eager + graph:
         validate_dag(d, names)
     assert e2.stats["graph_steps"] > 0
+
+
+def test_graph_replay_split_kv_matches_eager(monkeypatch):
+    """Split-KV decode attention (K6, forced to 4 splits) inside captured
+    hipGraphs: same greedy plans as the eager split path and as no split."""
+    model = LlamaModel.random("tiny", "cuda", seed=3)
+    reg = MemoryRegistry(synthetic_registry(8, seed=2))
+    intents = [synthetic_intent(i) for i in range(4)]
+    plain, _ = _plans(model, reg, intents, graphs=False, cascade=False, pipeline=False)
+    monkeypatch.setenv("MCP_KV_SPLIT", "4")
+    eager, e1 = _plans(model, reg, intents, graphs=False, cascade=False, pipeline=False)
+    graph, e2 = _plans(model, reg, intents, graphs=True, cascade=False, pipeline=False)
+    assert e1.stats["kv_split_steps"] > 0 and e2.stats["graph_split_steps"] > 0
+    assert graph == eager
+    same = sum(x == y for x, y in zip(plain, eager))
+    assert same >= len(plain) - 1, same

@@ -223,6 +223,19 @@ def test_graph_static_layout_matches_dynamic():
     assert torch.allclose(h_st[:3].float(), h_dyn.float(), atol=1e-5)
     assert t_st[:3].tolist() == t_dyn.tolist()
     assert (t_st[3:] == -1).all()          # padded rows have empty allowed sets
+    # the narrow block-table width class + a padded copy-on-write list: the
+    # real pair is copied, the (-1, -1) padding is skipped, same forward
+    eng.kv.data.copy_(kv0)
+    w = gr.width_for(int(step.block_table.shape[1]))
+    assert w == 32
+    host = gr.pack_static(step, b, w, [(5, 6)])
+    ds, csrc, cdst = views(torch.from_numpy(host), gr._sizes(b, w) + [gr._caps(b)[0], 0])
+    assert csrc.numel() == gr._ncopy(b) and (csrc[1:] == -1).all()
+    ops.copy_blocks(eng.kv.data, csrc, cdst)
+    assert torch.equal(eng.kv.data[:, :, 6], kv0[:, :, 5])
+    assert torch.equal(eng.kv.data[:, :, 7:], kv0[:, :, 7:])
+    h_w = model.forward(ds, eng.kv)
+    assert torch.allclose(h_w[:3].float(), h_dyn.float(), atol=1e-5)
 
 
 def test_engine_stall_watchdog_returns_503():
