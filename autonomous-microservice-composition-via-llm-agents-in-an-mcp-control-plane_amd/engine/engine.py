@@ -95,7 +95,7 @@ class LLMEngine:
         cfg = model.cfg
         self.device = model.device
         self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
-        self.cascade = cascade      # shared-prefix (cascade) attention
+        self.cascade = cascade and os.environ.get("MCP_CASCADE", "1") == "1"   # shared-prefix attention
         # optional two launch cohorts in flight: the host schedules / updates one
         # cohort while the GPU runs the other's forward.  Off by default: every
         # cohort step streams all the weights again, so a request waits two

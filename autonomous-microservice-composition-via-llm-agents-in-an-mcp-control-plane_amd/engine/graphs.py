@@ -7,8 +7,9 @@ each, a few hundred tokens) costs a few ms of weight streaming on the GPU but
 Python the launches, not the GPU, set the step time.  Steps with at most
 ``max(BUCKETS)`` tokens are therefore replayed from a captured hipGraph
 (``torch.cuda.CUDAGraph`` is the HIP graph API on ROCm).  A graph is keyed by
-(token bucket, block-table width class, split-KV factor) and captured lazily
-on first use, after one eager warm-up of the same static step.  Every step of
+(token bucket, sequence-capacity class, block-table width class, split-KV
+factor), captured at start-up (``warm``) or lazily on first use, after one
+eager warm-up of the same static step.  Every step of
 a key uses ONE fixed int32 layout (``pack_static``):
 
 * tokens padded to the bucket size (padding writes no KV: slot -1), sequence
@@ -36,6 +37,7 @@ a key uses ONE fixed int32 layout (``pack_static``):
 from __future__ import annotations
 
 import dataclasses
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -50,6 +52,9 @@ from .batch import BLOCK_SIZE, HostStager, StepInputs, build_work, tokens_per_it
 # weight-streaming kernel's M classes); measured at 80 intents/s, power-of-two
 # buckets padded a 300-token step to 512 and cost 12 % of p50
 BUCKETS = (8, 16, 32, 48, 64) + tuple(range(128, 1025, 64))
+# sequence-capacity classes: a step of 6 requests does not carry (and launch
+# empty attention work items for) 128 dummy sequences
+SEQ_CLASSES = (8, 32, 128, 512, 2048)
 ALLOWED_PER_ROW = 64
 MAX_COPIES = 64
 MIN_WIDTH = 32                 # block-table width classes: 32, 128, 512, ... blocks (x4)
@@ -57,7 +62,7 @@ MIN_WIDTH = 32                 # block-table width classes: 32, 128, 512, ... bl
 
 @dataclasses.dataclass
 class _Bucket:
-    key: Tuple[int, int, int]
+    key: Tuple[int, int, int, int]
     sizes: List[int]
     S: int
     buf: torch.Tensor
@@ -66,6 +71,11 @@ class _Bucket:
     dstep: object = None
     csrc: Optional[torch.Tensor] = None
     cdst: Optional[torch.Tensor] = None
+
+
+def _nw1_cutoff(t1: int) -> int:
+    # the same cutoff batch.build_work uses to route a sequence to 1-wave items
+    return int(os.environ.get("MCP_ATTN_NW1_CUTOFF", str(t1 * 2)))
 
 
 class GraphRunner:
@@ -78,7 +88,7 @@ class GraphRunner:
         self.temperature, self.seed = float(temperature), int(seed)
         self.buckets = tuple(sorted(buckets))
         self.max_seqs = int(max_seqs)
-        self._b: Dict[Tuple[int, int, int], _Bucket] = {}
+        self._b: Dict[Tuple[int, int, int, int], _Bucket] = {}
         self._pool = None
         self.stager = HostStager(self.device)
         self.replays = 0
@@ -86,21 +96,26 @@ class GraphRunner:
         self.capture_s = 0.0
 
     # ---------------------------------------------------------------- layout
-    def _caps(self, b: int):
+    def _seq_cap(self, b: int, sb: Optional[int]) -> int:
+        return min(b, self.max_seqs if sb is None else sb)
+
+    def _caps(self, b: int, sb: Optional[int] = None):
         t1 = tokens_per_item(1, self.group)
         t4 = tokens_per_item(4, self.group)
-        S = min(b, self.max_seqs) + 1      # >= one empty dummy sequence
-        cap1 = b
-        cap4 = b // t4 + b // (2 * t1) + 1
+        n = self._seq_cap(b, sb)
+        S = n + 1                          # >= one empty dummy sequence
+        cutoff = _nw1_cutoff(t1)
+        cap1 = min(b, n * -(-cutoff // t1))              # 1-wave items: ql <= cutoff
+        cap4 = min(b // t4 + n, b) + 1                   # 4-wave items: ceil(ql / t4)
         return S, cap1, cap4, S * ALLOWED_PER_ROW
 
-    def _ncopy(self, b: int) -> int:
-        return min(self._caps(b)[0], MAX_COPIES)
+    def _ncopy(self, b: int, sb: Optional[int] = None) -> int:
+        return min(self._caps(b, sb)[0], MAX_COPIES)
 
-    def _sizes(self, b: int, width: Optional[int] = None) -> List[int]:
-        S, cap1, cap4, A = self._caps(b)
+    def _sizes(self, b: int, width: Optional[int] = None, sb: Optional[int] = None) -> List[int]:
+        S, cap1, cap4, A = self._caps(b, sb)
         w = self.mblk if width is None else width
-        C = self._ncopy(b)
+        C = self._ncopy(b, sb)
         # same part order as batch.pack_host / views
         return [b, b, b, S, S, S, S, S * w, cap1, cap1, cap4, cap4, C, C, S, 2 + w, S + 1, A, S]
 
@@ -114,23 +129,32 @@ class GraphRunner:
             w *= 4
         return min(w, self.mblk)
 
-    def bucket_for(self, step: StepInputs, ncopies: int = 0) -> Optional[int]:
+    def seq_classes(self, b: int) -> List[int]:
+        out = sorted({min(c, b, self.max_seqs) for c in SEQ_CLASSES})
+        return out
+
+    def bucket_for(self, step: StepInputs, ncopies: int = 0) -> Optional[Tuple[int, int]]:
+        """(token bucket, sequence class) of the smallest static layout that
+        holds ``step``, or None."""
         T = step.num_tokens
         S = int(step.q_len.shape[0])
         A = int(step.allow_ids.shape[0]) if step.allow_ids is not None else 0
         if step.block_table.shape[1] > self.mblk:
             return None
         for b in self.buckets:
-            Sb, _, _, Acap = self._caps(b)
-            if T <= b and S < Sb and A <= Acap and ncopies <= self._ncopy(b):
-                return b
+            if T > b:
+                continue
+            for sb in self.seq_classes(b):
+                Sb, _, _, Acap = self._caps(b, sb)
+                if S < Sb and A <= Acap and ncopies <= self._ncopy(b, sb):
+                    return b, sb
         return None
 
     def pack_static(self, step: Optional[StepInputs], b: int, width: Optional[int] = None,
-                    copies: Sequence = ()) -> Optional[np.ndarray]:
-        S_b, cap1, cap4, A_cap = self._caps(b)
+                    copies: Sequence = (), sb: Optional[int] = None) -> Optional[np.ndarray]:
+        S_b, cap1, cap4, A_cap = self._caps(b, sb)
         w = self.mblk if width is None else width
-        C = self._ncopy(b)
+        C = self._ncopy(b, sb)
         T = step.num_tokens if step is not None else 0
         S = int(step.q_len.shape[0]) if step is not None else 0
         ids = np.zeros(b, np.int32)
@@ -198,12 +222,12 @@ class GraphRunner:
         if e is not None:
             return e
         t0 = time.perf_counter()
-        b, w, ns = key
-        sizes = self._sizes(b, w)
-        S_b = self._caps(b)[0]
+        b, sb, w, ns = key
+        sizes = self._sizes(b, w, sb)
+        S_b = self._caps(b, sb)[0]
         buf = torch.zeros(sum(sizes), dtype=torch.int32, device=self.device)
         e = _Bucket(key=key, sizes=sizes, S=S_b, buf=buf)
-        buf.copy_(torch.from_numpy(self.pack_static(None, b, w)))
+        buf.copy_(torch.from_numpy(self.pack_static(None, b, w, sb=sb)))
         # pre_tokens -1: cascade sizes live on the device (batch.views)
         e.dstep, e.csrc, e.cdst = views(buf, sizes + [S_b, -1, ns])
         self._body(e)                                   # eager warm-up (lazy allocations)
@@ -229,9 +253,10 @@ class GraphRunner:
         for b in self.buckets:
             if max_tokens is not None and b > max_tokens:
                 break
-            for w in widths:
-                for ns in kv_splits:
-                    self._get((b, w, int(ns)))
+            for sb in self.seq_classes(b):
+                for w in widths:
+                    for ns in kv_splits:
+                        self._get((b, sb, w, int(ns)))
         return self.captures - n0
 
     def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1) -> Optional[torch.Tensor]:
@@ -239,16 +264,17 @@ class GraphRunner:
         ``copies``); returns the device tensor of sampled tokens (first
         ``len(step.logit_rows)`` entries valid), or None when the step does
         not fit a bucket (the caller runs it eagerly)."""
-        b = self.bucket_for(step, len(copies))
-        if b is None:
+        bs = self.bucket_for(step, len(copies))
+        if bs is None:
             return None
+        b, sb = bs
         w = self.width_for(int(step.block_table.shape[1]))
         if w is None:
             return None
-        host = self.pack_static(step, b, w, copies)
+        host = self.pack_static(step, b, w, copies, sb)
         if host is None:
             return None
-        e = self._get((b, w, int(kv_splits)))
+        e = self._get((b, sb, w, int(kv_splits)))
         self.stager.to_device(host, out=e.buf)
         e.graph.replay()
         self.replays += 1

@@ -214,10 +214,10 @@ def test_graph_static_layout_matches_dynamic():
     h_dyn = model.forward(d, eng.kv)
     t_dyn = ops.sample_allowed(h_dyn, model.w.lm_head, d.allow_ptr, d.allow_ids, d.sample_ctr, 0.0, 0)
     eng.kv.data.copy_(kv0)
-    b = gr.bucket_for(step)
-    assert b == 16
-    host = gr.pack_static(step, b)
-    ds = views(torch.from_numpy(host), gr._sizes(b) + [gr._caps(b)[0], 0])[0]
+    b, sb = gr.bucket_for(step)
+    assert (b, sb) == (16, 8)
+    host = gr.pack_static(step, b, sb=sb)
+    ds = views(torch.from_numpy(host), gr._sizes(b, sb=sb) + [gr._caps(b, sb)[0], 0])[0]
     h_st = model.forward(ds, eng.kv)
     t_st = ops.sample_allowed(h_st, model.w.lm_head, ds.allow_ptr, ds.allow_ids, ds.sample_ctr, 0.0, 0)
     assert torch.allclose(h_st[:3].float(), h_dyn.float(), atol=1e-5)
@@ -228,9 +228,9 @@ def test_graph_static_layout_matches_dynamic():
     eng.kv.data.copy_(kv0)
     w = gr.width_for(int(step.block_table.shape[1]))
     assert w == 32
-    host = gr.pack_static(step, b, w, [(5, 6)])
-    ds, csrc, cdst = views(torch.from_numpy(host), gr._sizes(b, w) + [gr._caps(b)[0], 0])
-    assert csrc.numel() == gr._ncopy(b) and (csrc[1:] == -1).all()
+    host = gr.pack_static(step, b, w, [(5, 6)], sb)
+    ds, csrc, cdst = views(torch.from_numpy(host), gr._sizes(b, w, sb) + [gr._caps(b, sb)[0], 0])
+    assert csrc.numel() == gr._ncopy(b, sb) and (csrc[1:] == -1).all()
     ops.copy_blocks(eng.kv.data, csrc, cdst)
     assert torch.equal(eng.kv.data[:, :, 6], kv0[:, :, 5])
     assert torch.equal(eng.kv.data[:, :, 7:], kv0[:, :, 7:])
