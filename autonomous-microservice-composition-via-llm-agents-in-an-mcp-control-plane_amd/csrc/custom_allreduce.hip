@@ -21,6 +21,10 @@
 // Staging buffers are double-buffered by epoch parity, so no end-of-kernel
 // barrier is needed: a rank can only overwrite a buffer two calls later, after
 // every peer has passed the next call's start barrier (stream order).
+// The epoch lives on the DEVICE (a per-rank call counter: every block reads
+// it at entry, the last block to finish advances it), never in the launch
+// arguments, so a launch captured in a hipGraph is replayed with a fresh
+// epoch every time (tensor-parallel engine steps replay captured graphs).
 // Every wait has a wall-clock timeout (no hang if a peer dies): the kernel
 // records an error code and gives up instead of spinning.  The code lives in
 // coherent host memory, so ``car_error`` is a plain host read (no HIP call,
@@ -42,13 +46,43 @@ constexpr long long CAR_TIMEOUT_TICKS = 200000000ll;
 struct CarArgs {
   const bf16x8* inp;
   bf16x8* out;
-  bf16x8* bufs[CAR_MAX_RANKS];       // staging buffers of this epoch's parity
+  bf16x8* bufs[CAR_MAX_RANKS];       // staging buffers (parity 0; parity 1 at + par_vecs)
   unsigned* sigs[CAR_MAX_RANKS];     // signal arrays of every rank
   int* err;
+  unsigned* ctr;                     // device: [0] completed calls, [1] blocks done this call
   long long nvec;                    // message length in 16-byte vectors
+  long long par_vecs;                // staging buffer size per parity, 16-byte vectors
   int rank, world;
-  unsigned epoch;
+  unsigned epoch;                    // set in-kernel (car_begin)
 };
+
+// entry of every block: this call's epoch = completed calls + 1 (no block
+// advances the counter before every block has read it: car_end), and the
+// staging buffers of its parity
+DEV void car_begin(CarArgs& a) {
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0)
+    s_epoch = __hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  a.epoch = s_epoch;
+  if (a.epoch & 1u)
+    for (int p = 0; p < CAR_MAX_RANKS; ++p)
+      if (a.bufs[p]) a.bufs[p] += a.par_vecs;
+}
+
+// exit of every block: the last block to finish advances the call counter
+// (stream order makes it visible to the next call's blocks)
+DEV void car_end(const CarArgs& a) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned done = __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.ctr, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // flag slot of (phase, block, source rank) inside one rank's signal array
 DEV int sig_slot(int phase, int block, int src) {
@@ -123,15 +157,18 @@ DEV void block_range(long long n, long long& v0, long long& v1) {
 }
 
 __global__ __launch_bounds__(CAR_THREADS) void car_one_shot(CarArgs a) {
+  car_begin(a);
   long long v0, v1;
   block_range(a.nvec, v0, v1);
   bf16x8* mine = a.bufs[a.rank];
   for (long long v = v0 + threadIdx.x; v < v1; v += CAR_THREADS) mine[v] = a.inp[v];
   block_barrier(a, 0);
   sum_range_dyn(a, v0, v1, a.out);
+  car_end(a);
 }
 
 __global__ __launch_bounds__(CAR_THREADS) void car_two_shot(CarArgs a) {
+  car_begin(a);
   long long v0, v1;
   block_range(a.nvec, v0, v1);
   bf16x8* mine = a.bufs[a.rank];
@@ -149,6 +186,7 @@ __global__ __launch_bounds__(CAR_THREADS) void car_two_shot(CarArgs a) {
     const bf16x8* src = a.bufs[p];
     for (long long v = t0 + threadIdx.x; v < t1; v += CAR_THREADS) a.out[v] = src[v];
   }
+  car_end(a);
 }
 
 struct CarState {
@@ -157,9 +195,9 @@ struct CarState {
   char* data = nullptr;              // own staging: 2 x buf_bytes (epoch parity)
   unsigned* sig = nullptr;           // own signal array (uncached)
   int* err = nullptr;
+  unsigned* ctr = nullptr;           // device call counter (car_begin / car_end)
   char* peer_data[CAR_MAX_RANKS] = {};
   unsigned* peer_sig[CAR_MAX_RANKS] = {};
-  unsigned epoch = 0;
   bool opened = false;
 };
 
@@ -179,6 +217,8 @@ void* car_create(int rank, int world, size_t buf_bytes, void* handles_out) {
             hipExtMallocWithFlags((void**)&st->sig, SIG_BYTES, hipDeviceMallocUncached) ==
                 hipSuccess &&
             hipHostMalloc((void**)&st->err, sizeof(int), hipHostMallocCoherent) == hipSuccess &&
+            hipMalloc((void**)&st->ctr, 2 * sizeof(unsigned)) == hipSuccess &&
+            hipMemset(st->ctr, 0, 2 * sizeof(unsigned)) == hipSuccess &&
             hipMemset(st->sig, 0, SIG_BYTES) == hipSuccess &&
             hipDeviceSynchronize() == hipSuccess;
   if (ok) *st->err = 0;
@@ -189,6 +229,7 @@ void* car_create(int rank, int world, size_t buf_bytes, void* handles_out) {
     if (st->data) (void)hipFree(st->data);
     if (st->sig) (void)hipFree(st->sig);
     if (st->err) (void)hipHostFree(st->err);
+    if (st->ctr) (void)hipFree(st->ctr);
     delete st;
     return nullptr;
   }
@@ -225,20 +266,20 @@ int car_allreduce(void* state, const void* inp, void* out, long long n_elems, in
   CarState* st = (CarState*)state;
   if (!st->opened) return -1;
   if (n_elems % 8 || (size_t)n_elems * 2 > st->buf_bytes) return -2;
-  st->epoch += 1;
   CarArgs a;
   a.inp = (const bf16x8*)inp;
   a.out = (bf16x8*)out;
-  const size_t off = (st->epoch & 1) ? st->buf_bytes : 0;
   for (int p = 0; p < CAR_MAX_RANKS; ++p) {
-    a.bufs[p] = p < st->world ? (bf16x8*)(st->peer_data[p] + off) : nullptr;
+    a.bufs[p] = p < st->world ? (bf16x8*)st->peer_data[p] : nullptr;
     a.sigs[p] = p < st->world ? st->peer_sig[p] : nullptr;
   }
   a.err = st->err;
+  a.ctr = st->ctr;
   a.nvec = n_elems / 8;
+  a.par_vecs = (long long)(st->buf_bytes / 16);
   a.rank = st->rank;
   a.world = st->world;
-  a.epoch = st->epoch;
+  a.epoch = 0;
   long long want = (a.nvec + CAR_THREADS * 4 - 1) / (CAR_THREADS * 4);
   if (blocks <= 0) blocks = (int)min(want, (long long)CAR_MAX_BLOCKS);
   blocks = max(1, min(blocks, CAR_MAX_BLOCKS));
@@ -266,5 +307,6 @@ void car_destroy(void* state) {
   (void)hipFree(st->data);
   (void)hipFree(st->sig);
   (void)hipHostFree(st->err);
+  (void)hipFree(st->ctr);
   delete st;
 }

@@ -110,8 +110,18 @@ class LLMEngine:
         self._turn = 0
         self._next_cohort = 0
         self.stager = HostStager(self.device)
-        self._graphs_wanted = (self.device.type == "cuda" and bcast is None
-                               and getattr(model, "tp", 1) == 1) if graphs is None else graphs
+        if graphs is None:
+            graphs = self.device.type == "cuda" and os.environ.get("MCP_GRAPHS", "1") == "1"
+            if graphs and getattr(model, "tp", 1) > 1:
+                # TP: workers mirror the driver's graphs; every all-reduce of a
+                # bucket must be capturable (K12 / RCCL, not gloo on GPU tensors)
+                from .graphs import BUCKETS
+                ar = getattr(model, "_allreduce", None)
+                safe = getattr(ar, "graph_safe", None)
+                graphs = (bcast is not None and safe is not None
+                          and safe(max(BUCKETS) * model.cfg.hidden * 2)
+                          and not getattr(model, "seq_parallel", False))
+        self._graphs_wanted = graphs
         self.graphs = None          # engine.graphs.GraphRunner, created after the KV cache
         if num_blocks is not None:
             self.kv = KVCache(cfg.layers, model.hkv, cfg.head_dim, num_blocks, self.device)
@@ -131,7 +141,8 @@ class LLMEngine:
         self.steps = 0
         if self._graphs_wanted:
             from .graphs import GraphRunner
-            self.graphs = GraphRunner(model, self.kv, temperature, seed, max_seqs=max_batch)
+            self.graphs = GraphRunner(model, self.kv, temperature, seed, max_seqs=max_batch,
+                                      bcast=bcast)
         self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "graph_cow_steps": 0,
                       "graph_split_steps": 0, "kv_split_steps": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}

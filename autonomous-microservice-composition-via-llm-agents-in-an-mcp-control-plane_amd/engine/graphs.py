@@ -80,8 +80,10 @@ def _nw1_cutoff(t1: int) -> int:
 
 class GraphRunner:
     def __init__(self, model, kv, temperature: float, seed: int, buckets=BUCKETS,
-                 max_seqs: int = 256):
+                 max_seqs: int = 256, bcast=None, sample: bool = True):
         self.model, self.kv = model, kv
+        self.bcast = bcast          # TP driver: StepBroadcaster (workers mirror every graph)
+        self.sample = sample        # False on TP workers: forward only
         self.device = model.device
         self.group = model.cfg.group
         self.mblk = (model.cfg.max_pos + BLOCK_SIZE - 1) // BLOCK_SIZE
@@ -213,11 +215,22 @@ class GraphRunner:
     def _body(self, e: _Bucket):
         ops.copy_blocks(self.kv.data, e.csrc, e.cdst)
         hidden = self.model.forward(e.dstep, self.kv)
+        if not self.sample:
+            return None
         return ops.sample_allowed(hidden, self.model.w.lm_head, e.dstep.allow_ptr,
                                   e.dstep.allow_ids, e.dstep.sample_ctr, self.temperature,
                                   self.seed)
 
-    def _get(self, key: Tuple[int, int, int]) -> _Bucket:
+    def get(self, key) -> _Bucket:
+        """The captured graph of ``key`` (capturing it on first use)."""
+        return self._get(tuple(int(x) for x in key))
+
+    def replay(self, key) -> None:
+        """TP worker: replay ``key`` on the payload already in its buffer."""
+        self._b[tuple(int(x) for x in key)].graph.replay()
+        self.replays += 1
+
+    def _get(self, key: Tuple[int, int, int, int]) -> _Bucket:
         e = self._b.get(key)
         if e is not None:
             return e
@@ -256,7 +269,11 @@ class GraphRunner:
             for sb in self.seq_classes(b):
                 for w in widths:
                     for ns in kv_splits:
-                        self._get((b, sb, w, int(ns)))
+                        key = (b, sb, w, int(ns))
+                        if self.bcast is not None:      # workers capture in lockstep
+                            self._launch_tp(key, self.pack_static(None, b, w, sb=sb))
+                        else:
+                            self._get(key)
         return self.captures - n0
 
     def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1) -> Optional[torch.Tensor]:
@@ -274,8 +291,23 @@ class GraphRunner:
         host = self.pack_static(step, b, w, copies, sb)
         if host is None:
             return None
-        e = self._get((b, sb, w, int(kv_splits)))
-        self.stager.to_device(host, out=e.buf)
-        e.graph.replay()
+        key = (b, sb, w, int(kv_splits))
+        if self.bcast is not None:
+            e = self._launch_tp(key, host)
+        else:
+            e = self._get(key)
+            self.stager.to_device(host, out=e.buf)
+            e.graph.replay()
         self.replays += 1
         return e.tokens
+
+    def _launch_tp(self, key, host: np.ndarray) -> _Bucket:
+        """TP driver: key to the workers (they capture it too if new, running
+        the same eager warm-up collectives), then the payload into every
+        rank's bucket buffer, then every rank replays."""
+        self.bcast.send_graph(key, int(host.size))
+        e = self._get(key)
+        d = self.stager.to_device(host, out=e.buf)
+        self.bcast.send_payload(d)
+        e.graph.replay()
+        return e

@@ -7,6 +7,8 @@ row-parallel projections all-reduce over RCCL/xGMI (models.llama).  Workers
 hold identical KV-cache layouts (same block count), so block ids in the
 descriptor are valid everywhere.  Only the driver samples: after the final
 all-reduce every rank has the full hidden state and the LM head is replicated.
+Steps that fit a captured bucket are replayed from hipGraphs on every rank
+(engine.graphs: the driver broadcasts the graph key, then the static payload).
 """
 from __future__ import annotations
 
@@ -37,13 +39,29 @@ def agree_num_blocks(kv_bytes_per_block: int, device, group, reserve_frac: float
 
 
 def worker_loop(model, kv, bcast: StepBroadcaster) -> int:
-    """Mirror the driver's forward passes until it broadcasts stop."""
+    """Mirror the driver's forward passes until it broadcasts stop.  Graph
+    steps replay this rank's copy of the driver's captured hipGraph (same key,
+    same static layout; forward only - sampling is the driver's)."""
+    graphs = None
+
+    def graph_buffer(key):
+        nonlocal graphs
+        if graphs is None:
+            from .graphs import GraphRunner
+            graphs = GraphRunner(model, kv, 0.0, 0, sample=False)
+        return graphs.get(key).buf
+
     n = 0
     while True:
-        msg = bcast.recv()
+        msg = bcast.recv(graph_buffer)
         if msg is None:
             return n
         payload, layout = msg
+        if isinstance(layout, tuple) and layout[0] == "graph":
+            graphs.replay(layout[1])
+            model.comm_check()
+            n += 1
+            continue
         dstep, csrc, cdst = views(payload, layout)
         if csrc.numel():
             ops.copy_blocks(kv.data, csrc, cdst)

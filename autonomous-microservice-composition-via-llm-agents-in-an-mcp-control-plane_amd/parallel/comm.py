@@ -132,6 +132,16 @@ class AllReduce:
         if self.custom is not None:
             self.custom.check()
 
+    def graph_safe(self, nbytes: int) -> bool:
+        """Whether an all-reduce of up to ``nbytes`` can be captured in a
+        hipGraph: K12 (device-side epochs) and RCCL on the capture stream are;
+        a gloo collective on a GPU tensor (CPU tests) is host code and is not."""
+        if self.device.type != "cuda":
+            return False
+        if self.custom is not None and nbytes <= self.custom.max_bytes:
+            return True
+        return self.native is not None or not _is_gloo(self.group)
+
 
 def make_allreduce(group, device) -> AllReduce:
     return AllReduce(group, device)
@@ -214,18 +224,42 @@ class StepBroadcaster:
         if payload.numel():
             self._bcast(payload if payload.device == self.device else payload.to(self.device))
 
+    GRAPH = -2          # hdr[1] marker: replay the captured graph hdr[2:6]
+
+    def send_graph(self, key, n: int) -> None:
+        """Graph step: header (the graph key) first, so every worker can
+        capture the same graph (its eager warm-up runs the same collectives)
+        before the static payload is broadcast into the graph's buffer."""
+        hdr = np.full(self.HDR, 0, np.int32)
+        hdr[0], hdr[1] = n, self.GRAPH
+        hdr[2:2 + len(key)] = key
+        self._bcast(torch.from_numpy(hdr).to(self.device))
+
+    def send_payload(self, payload: torch.Tensor) -> None:
+        if payload.numel():
+            self._bcast(payload)
+
     def stop(self) -> None:
         hdr = np.zeros(self.HDR, np.int32)
         hdr[0] = -1
         self._bcast(torch.from_numpy(hdr).to(self.device))
 
-    def recv(self):
+    def recv(self, graph_buffer=None):
+        """Next message: None (stop), ``(payload, layout)`` (eager step) or,
+        for a graph step, ``(buf, ("graph", key))`` after the payload landed in
+        ``graph_buffer(key)`` (the worker's captured bucket buffer)."""
         hdr = torch.zeros(self.HDR, dtype=torch.int32, device=self.device)
         self._bcast(hdr)
         h = hdr.cpu().numpy()
         n, nl = int(h[0]), int(h[1])
         if n < 0:
             return None
+        if nl == self.GRAPH:
+            key = tuple(int(x) for x in h[2:6])
+            buf = graph_buffer(key)[:n]
+            if n:
+                self._bcast(buf)
+            return buf, ("graph", key)
         layout = [int(x) for x in h[2:2 + nl]]
         payload = torch.empty(n, dtype=torch.int32, device=self.device)
         if n:

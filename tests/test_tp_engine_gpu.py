@@ -4,7 +4,9 @@ row-parallel all-reduce through K12 (the xGMI peer-read kernel; here the
 weights: greedy (temperature 0) plans must be identical.  The driver runs in
 this process (TPPlanner, as behind the API with MCP_TP=2), the worker rank is
 a spawned process; the group is gloo (RCCL refuses two ranks on one device),
-so MCP_COMM=torch and a K12 staging buffer large enough for every message."""
+so MCP_COMM=torch and a K12 staging buffer large enough for every message.
+Steps that fit a hipGraph bucket replay captured graphs on both ranks (the K12
+epoch lives on the device, so replays resynchronise correctly)."""
 import os
 
 import pytest
@@ -39,12 +41,14 @@ def test_tp2_two_processes_one_gpu_matches_tp1(monkeypatch):
     try:
         ar = tp.engine.model._allreduce
         assert ar.custom is not None and ar.native is None
+        assert tp.engine.graphs is not None          # K12 all-reduces are capturable
         dags_tp = tp.plan_many(intents)
         tp.engine.model.comm_check()
         steps_tp = tp.engine.stats["steps"]
+        graph_steps_tp = tp.engine.stats["graph_steps"]
     finally:
         tp.shutdown()
-    assert steps_tp > 0
+    assert steps_tp > 0 and graph_steps_tp > 0   # worker ranks replayed the driver's graphs
     for d in dags_tp:
         validate_dag(d, names)
 
