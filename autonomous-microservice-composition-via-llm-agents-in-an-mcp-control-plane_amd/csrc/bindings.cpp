@@ -208,7 +208,7 @@ void topk_fused(const at::Tensor& Q, const at::Tensor& E, int64_t k, at::Tensor&
   CHECK_BF16_TENSOR(Q); CHECK_BF16_TENSOR(E);
   TORCH_CHECK(Q.dim() == 2 && E.dim() == 2 && Q.size(1) == E.size(1), "Q [B, D], E [N, D]");
   const int B = Q.size(0), N = E.size(0), D = Q.size(1);
-  const int nseg = topk_fused_segments(N);
+  const int nseg = topk_fused_segments(N, B);
   TORCH_CHECK(cand_v.scalar_type() == at::kFloat && cand_v.is_contiguous() &&
               cand_v.numel() == (int64_t)B * nseg * k, "cand_v [B, nseg, k] f32");
   CHECK_I32_TENSOR(cand_i);
@@ -454,7 +454,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("l2norm_rows", &l2norm_rows);
   m.def("topk_fused", &topk_fused, py::arg("Q"), py::arg("E"), py::arg("k"), py::arg("cand_v"),
         py::arg("cand_i"));
-  m.def("topk_fused_segments", &topk_fused_segments);
+  m.def("topk_fused_segments", &topk_fused_segments, py::arg("N"), py::arg("B") = 1);
   m.def("segment_topk", &segment_topk, py::arg("vals"), py::arg("idx"), py::arg("seg_len"),
         py::arg("k"), py::arg("out_v"), py::arg("out_i"));
   m.def("paged_attention", &paged_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),

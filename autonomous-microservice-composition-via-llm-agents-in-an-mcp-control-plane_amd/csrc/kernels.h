@@ -82,8 +82,8 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
 
 // topk.hip
 void launch_l2norm_rows(void* x, int N, int D, hipStream_t s);
-// fused scoring + per-segment top-k: cand [B, topk_fused_segments(N), k]
-int topk_fused_segments(int N);
+// fused scoring + per-segment top-k: cand [B, topk_fused_segments(N, B), k]
+int topk_fused_segments(int N, int B = 1);
 int launch_topk_fused(const void* Q, const void* E, int B, int N, int D, int k, float* cand_v,
                       int* cand_i, hipStream_t s);
 int launch_segment_topk(const float* vals, const int* idx_in, int B, int L, int seg_len, int k,

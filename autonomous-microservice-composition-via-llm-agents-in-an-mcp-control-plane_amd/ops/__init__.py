@@ -268,8 +268,11 @@ def l2norm_rows(x):
     return x
 
 
+FUSED_TOPK_MIN_SCORES = 1 << 27
+
+
 def topk_cosine(queries, corpus, k: int, seg_len: int = 4096, n_valid: Optional[int] = None,
-                fused: bool = True):
+                fused: Optional[bool] = None):
     """Top-k cosine similarity of unit-norm ``queries`` [B, D] against unit-norm
     ``corpus`` [N, D] (both bf16).  Returns (scores [B, k] f32, index [B, k] int32),
     best first (ties: lower row first).
@@ -281,8 +284,19 @@ def topk_cosine(queries, corpus, k: int, seg_len: int = 4096, n_valid: Optional[
     ``N / 4096 x k`` candidates.  Other shapes: fp32-output scoring GEMM +
     segmented top-k (the scoring GEMM needs N % 4: such corpora are padded at
     index build, ``retrieval.store``; ``n_valid`` = the real rows, the rest
-    are never returned)."""
-    use_fused = fused and queries.shape[0] <= 64 and k <= 64 and queries.shape[1] in (512, 1024)
+    are never returned).
+
+    ``fused=None`` picks by size: the fused kernel once the [B, N] fp32 score
+    matrix would pass 2^27 entries (512 MB), the GEMM path below that - measured
+    on MI355X (profiles/config3_topk.md): 1M x 64 queries 1.56 vs 2.26 ms, 10k
+    rows 0.12 vs 0.45-2.1 ms, but 10M x 16 / x 64 4.2 / 5.3 ms fused vs 7.0 /
+    14.7 through the score matrix.  True / False force a path."""
+    eligible = queries.shape[0] <= 64 and k <= 64 and queries.shape[1] in (512, 1024)
+    n_rows = n_valid if n_valid is not None else corpus.shape[0]
+    if fused is None:
+        # (the GEMM path needs rows % 4: an unpadded corpus stays on the fused kernel)
+        fused = queries.shape[0] * n_rows >= FUSED_TOPK_MIN_SCORES or corpus.shape[0] % 4 != 0
+    use_fused = fused and eligible
     if n_valid is not None and n_valid < corpus.shape[0] and (not queries.is_cuda or use_fused):
         corpus = corpus[:n_valid]                  # a row prefix: contiguous, no copy
         n_valid = None
@@ -294,7 +308,7 @@ def topk_cosine(queries, corpus, k: int, seg_len: int = 4096, n_valid: Optional[
     L_ = lib()
     D = queries.shape[1]
     if use_fused:
-        nseg = L_.topk_fused_segments(N)
+        nseg = L_.topk_fused_segments(N, queries.shape[0])
         vals = torch.empty(B, nseg * k, device=queries.device, dtype=torch.float32)
         idx = torch.empty(B, nseg * k, device=queries.device, dtype=torch.int32)
         L_.topk_fused(queries.contiguous(), corpus, k, vals, idx)

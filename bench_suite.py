@@ -73,7 +73,7 @@ def plumbing(runs: int = 30):
                           "reference_ms": REF_EXEC_MS[n], "speedup": round(REF_EXEC_MS[n] / p50, 2)}))
 
 
-def topk(n: int, dim: int, k: int, batches=(1, 16, 64), iters: int = 50):
+def topk(n: int, dim: int, k: int, batches=(1, 16, 32, 64), iters: int = 50):
     import torch
     import mcp_amd.ops as ops
     dev = torch.device("cuda")
@@ -114,7 +114,8 @@ def topk(n: int, dim: int, k: int, batches=(1, 16, 64), iters: int = 50):
         print(json.dumps({"config": "topk_cosine", "corpus": n, "dim": dim, "k": k, "queries": b,
                           "latency_ms": round(ms, 4), "corpus_GBps": round(gbs, 1), "exact": ok,
                           "max_value_diff": vdiff, "max_gather_diff": gdiff,
-                          "path": "fused" if b <= 64 and k <= 64 and dim in (512, 1024) else "gemm+segment"}),
+                          "path": "fused" if (b <= 64 and k <= 64 and dim in (512, 1024)
+                                            and b * n >= ops.FUSED_TOPK_MIN_SCORES) else "gemm+segment"}),
               flush=True)
 
 

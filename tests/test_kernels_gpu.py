@@ -236,7 +236,8 @@ def test_copy_blocks():
                                      (64, 1_000_003, 1024, 32), (16, 300001, 512, 64),
                                      (5, 4095, 1024, 10), (64, 4097, 1024, 64), (17, 9000, 1024, 1),
                                      (33, 20000, 512, 64)])
-def test_topk_cosine(B, N, D, k):
+@pytest.mark.parametrize("fused", [True, None])
+def test_topk_cosine(B, N, D, k, fused):
     """Fused scoring + per-segment top-k (B <= 64, D in {512, 1024}) and the
     unfused GEMM path (other D; corpus padded to a multiple of 4 once, the pad
     rows never returned): values equal torch's top-k, indices point at rows
@@ -248,7 +249,7 @@ def test_topk_cosine(B, N, D, k):
     ops.l2norm_rows(corpus)
     q = torch.randn(B, D, device=DEV).bfloat16()
     ops.l2norm_rows(q)
-    vals, idx = ops.topk_cosine(q, corpus, k, n_valid=N)
+    vals, idx = ops.topk_cosine(q, corpus, k, n_valid=N, fused=fused)
     corpus = corpus[:N]
     assert int(idx.max()) < N and int(idx.min()) >= 0
     ref_s = q.float() @ corpus.float().t()
