@@ -97,13 +97,18 @@ class LLMEngine:
         self.bcast = bcast          # parallel.comm.StepBroadcaster on a TP driver, else None
         self.cascade = cascade and os.environ.get("MCP_CASCADE", "1") == "1"   # shared-prefix attention
         # optional two launch cohorts in flight: the host schedules / updates one
-        # cohort while the GPU runs the other's forward.  Off by default: every
-        # cohort step streams all the weights again, so a request waits two
-        # weight-bound steps per sampled token; measured on one MI355X at 40 / 80
-        # / 160 intents/s (config 5) p50 368 / 464 / 594 ms with cohorts against
-        # 194 / 242 / 572 ms without (profiles/config5_pipeline_ab.jsonl)
+        # cohort while the GPU runs the other's forward.  Every cohort step
+        # streams all the weights again, so a request waits two weight-bound
+        # steps per sampled token: measured on one MI355X (config 5, same run)
+        # p50 368 / 464 / 594 ms with cohorts vs 194 / 242 / 572 ms without at
+        # 40 / 80 / 160 intents/s (profiles/config5_pipeline_ab.jsonl).  Off by
+        # default; "auto" = cohorts only while >= PIPELINE_MIN_SEQS requests run
+        # (160 / 200 intents/s: 615 / 1170 ms, no better than off).
         if pipeline is None:
-            pipeline = os.environ.get("MCP_PIPELINE", "0") == "1"
+            env = os.environ.get("MCP_PIPELINE", "0")
+            pipeline = "auto" if env == "auto" else env == "1"
+        if pipeline == "auto" and self.device.type != "cuda":
+            pipeline = False
         self.pipeline = pipeline
         self.inflight: Dict[int, _Launch] = {}
         self.last_progress = time.perf_counter()   # watched by the planner's stall watchdog
@@ -303,7 +308,7 @@ class LLMEngine:
         Pipelined: cohort c's previous launch is retired (its sampled tokens
         fed to the grammar) while the GPU is still busy with cohort c^1's
         forward, then cohort c is scheduled and launched asynchronously."""
-        if not self.pipeline or self._big_step():
+        if not self._pipelined_now() or self._big_step():
             while self.inflight:                  # drain the cohorts before a full-batch step
                 c, L = self.inflight.popitem()
                 self._retire(L)
@@ -332,6 +337,12 @@ class LLMEngine:
         return done
 
     PIPELINE_MAX_TOKENS = 1024
+    PIPELINE_MIN_SEQS = 64
+
+    def _pipelined_now(self) -> bool:
+        if self.pipeline == "auto":
+            return len(self.running) + len(self.waiting) >= self.PIPELINE_MIN_SEQS
+        return bool(self.pipeline)
 
     def _big_step(self) -> bool:
         """Large batches run as ONE launch: halving the GEMM M per cohort costs
