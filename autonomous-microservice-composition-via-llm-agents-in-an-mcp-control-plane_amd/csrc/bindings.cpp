@@ -171,6 +171,12 @@ void gemm_plan_set_py(int64_t N, int64_t K, const std::vector<int64_t>& codes) {
   gemm_plan_set((int)N, (int)K, c.data(), (int)c.size());
 }
 
+void gemm_plan_set_splits_py(int64_t N, int64_t K, const std::vector<int64_t>& splits) {
+  std::vector<int> c(splits.begin(), splits.end());
+  for (int v : c) TORCH_CHECK(v >= 0 && v <= 16, "gemm plan split must be 0..16");
+  gemm_plan_set_splits((int)N, (int)K, c.data(), (int)c.size());
+}
+
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
   TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
@@ -441,6 +447,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("qkv_rope", &qkv_rope);
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
+  m.def("gemm_plan_set_splits", &gemm_plan_set_splits_py,
+        "measured split-K of the 128^2 path for one (N, K): a count per 64-row M bucket (0 = rule)");
+  m.def("gemm_plan_split", &gemm_plan_split);
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_plan_lookup", &gemm_plan_lookup);
   m.def("gemm_splitk_init", [](int64_t bytes) { return gemm_splitk_init((size_t)bytes); },

@@ -223,6 +223,7 @@ namespace {
 struct GemmPlan {
   int N, K;
   std::vector<signed char> code;
+  std::vector<signed char> split;    // measured split-K of the 128^2 path (0: the rule)
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -234,7 +235,26 @@ void gemm_plan_set(int N, int K, const int* codes, int n) {
       p.code = std::move(c);
       return;
     }
-  g_plans.push_back({N, K, std::move(c)});
+  g_plans.push_back({N, K, std::move(c), {}});
+}
+
+void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.split.assign(splits, splits + n);
+      return;
+    }
+  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n)});
+}
+
+// measured split count for the 128^2 path at this M bucket (0 = none recorded)
+int gemm_plan_split(int M, int N, int K) {
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.split.size() ? p.split[b] : 0;
+    }
+  return 0;
 }
 
 void gemm_plan_clear() { g_plans.clear(); }
@@ -342,8 +362,14 @@ int gemm128_splits(int M, int N, int K) {
     const int S = enabled, nkt = K / BK;
     return (nkt % S == 0 && (size_t)S * M * N * sizeof(float) <= g_splitk_ws_bytes) ? S : 1;
   }
-  if (tiles > G) return 1;
   const int nkt = K / BK;
+  // a measured split (tools/tune_gemm_plan.py) for this (N, K, M bucket) wins
+  // over the rule below where it is admissible
+  const int ps = gemm_plan_split(M, N, K);
+  if (ps == 1) return 1;
+  if (ps > 1 && nkt % ps == 0 && nkt / ps >= 4 && (size_t)ps * M * N * sizeof(float) <= g_splitk_ws_bytes)
+    return ps;
+  if (tiles > G) return 1;
   // fewest splits that give every CU a workgroup while each keeps <= 32
   // k-tiles: fewer fp32 partials to write and reduce.  Measured at M = 64-256
   // on the 8B shapes (profiles/gemm_small_m_splitk_sweep.jsonl): gate|up 2 vs

@@ -65,6 +65,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
     mod.gemm_plan_clear()
     for sh in plan["shapes"]:
         mod.gemm_plan_set(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["codes"]])
+        if "splits" in sh and hasattr(mod, "gemm_plan_set_splits"):
+            mod.gemm_plan_set_splits(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["splits"]])
     return len(plan["shapes"])
 
 
