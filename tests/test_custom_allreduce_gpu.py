@@ -43,6 +43,31 @@ def _worker(rank, world, port, q):
                     tol = 2e-2 * ref.abs().max().item() + 1e-2
                     if err > tol:
                         errs.append((mode, n, it, err, tol))
+        # captured in a hipGraph and replayed (TP engine steps): the epoch lives
+        # on the device, so every replay synchronises afresh; interleaved with
+        # eager calls so both paths advance the same call counter
+        for mode in (1, 2):
+            n = 8192 * 16
+            xs = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+            ys = torch.zeros_like(xs)
+            car(xs.clone(), mode=mode)                # warm-up outside the capture
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                car(xs, out=ys, mode=mode)
+            for it in range(4):
+                xs.copy_(_data(rank, n, 100 + it).cuda())
+                g.replay()
+                torch.cuda.synchronize()
+                ref = sum(_data(r, n, 100 + it).float() for r in range(world))
+                err = (ys.float().cpu() - ref).abs().max().item()
+                if err > 2e-2 * ref.abs().max().item() + 1e-2:
+                    errs.append(("graph", mode, it, err))
+                y = car(_data(rank, 4096, 200 + it).cuda(), mode=mode)   # an eager call between replays
+                torch.cuda.synchronize()
+                ref = sum(_data(r, 4096, 200 + it).float() for r in range(world))
+                if (y.float().cpu() - ref).abs().max().item() > 2e-2 * ref.abs().max().item() + 1e-2:
+                    errs.append(("eager-after-graph", mode, it))
         # timing of the decode-sized message (one-shot) and a 4 MiB one (two-shot)
         times = {}
         for n, mode in ((8192 * 8, 1), (8192 * 256, 2)):

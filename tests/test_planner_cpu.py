@@ -238,6 +238,46 @@ def test_graph_static_layout_matches_dynamic():
     assert torch.allclose(h_w[:3].float(), h_dyn.float(), atol=1e-5)
 
 
+def test_graph_static_layout_carries_cascade_sizes():
+    """hipGraph layouts carry the cascade prefix on the device: segment 15 =
+    [pre_tokens, pre_keys, prefix blocks...] (views() with pre_tokens -1 turns
+    it into AttnMeta.pre_dims / pre_bt), kv_begin per sequence, and a step
+    without cascade packs pre_tokens 0 (the prefix pass then exits at once)."""
+    from mcp_amd.engine.batch import StepInputs, views
+    from mcp_amd.engine.graphs import GraphRunner
+    model = LlamaModel.random("tiny", "cpu", seed=2)
+    eng = LLMEngine(model, num_blocks=64, max_batch=8, temperature=0.0, graphs=False)
+    gr = GraphRunner(model, eng.kv, 0.0, 0)
+    q_lens, ctx = [2, 3], [130, 140]
+    T = sum(q_lens)
+    step = StepInputs(token_ids=np.arange(T, dtype=np.int32),
+                      positions=np.asarray([128, 129, 137, 138, 139], np.int32),
+                      slots=np.asarray([3 * 64, 3 * 64 + 1, 4 * 64 + 9, 4 * 64 + 10, 4 * 64 + 11], np.int32),
+                      q_start=np.asarray([0, 2], np.int32), q_len=np.asarray(q_lens, np.int32),
+                      ctx_len=np.asarray(ctx, np.int32),
+                      block_table=np.asarray([[0, 1, 3], [0, 1, 4]], np.int32),
+                      logit_rows=np.asarray([1, 4], np.int32),
+                      allow_ptr=np.asarray([0, 2, 4], np.int32),
+                      allow_ids=np.asarray([5, 6, 7, 8], np.int32),
+                      sample_ctr=np.asarray([1, 2], np.int32))
+    step.kv_begin = np.asarray([128, 128], np.int32)
+    step.pre_bt = np.asarray([0, 1], np.int32)
+    step.pre_tokens = T
+    b, sb = gr.bucket_for(step)
+    w = gr.width_for(3)
+    host = gr.pack_static(step, b, w, sb=sb)
+    d = views(torch.from_numpy(host), gr._sizes(b, w, sb) + [gr._caps(b, sb)[0], -1, 1])[0]
+    m = d.attn
+    assert m.pre_dims.tolist() == [T, 128]
+    assert m.pre_bt[:2].tolist() == [0, 1] and m.pre_bt.numel() == w
+    assert m.kv_begin[:2].tolist() == [128, 128] and int(m.kv_begin[2:].abs().sum()) == 0
+    assert m.pre_tokens == b and m.pre_keys == w * 64          # grid capacities
+    step.pre_tokens, step.pre_bt, step.kv_begin = 0, None, None
+    d2 = views(torch.from_numpy(gr.pack_static(step, b, w, sb=sb)),
+               gr._sizes(b, w, sb) + [gr._caps(b, sb)[0], -1, 1])[0]
+    assert d2.attn.pre_dims.tolist() == [0, 0] and int(d2.attn.kv_begin.abs().sum()) == 0
+
+
 def test_engine_stall_watchdog_returns_503():
     """A step that stops making progress (hung GPU) fails pending requests with
     EngineStalled -> HTTP 503, and /healthz reports the replica unhealthy."""
