@@ -115,6 +115,11 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
     kt0 = 0;
     ntiles = pre_keys / KT;
     bt = a.pre_bt;
+    if constexpr (KSPLIT) {                               // this split's share of the prefix tiles
+      const int span = ntiles, z = blockIdx.z, nz = gridDim.z;
+      kt0 = span * z / nz;
+      ntiles = span * (z + 1) / nz;
+    }
   } else {
     s = a.work_seq[blockIdx.x];
     const int q0 = a.work_q0[blockIdx.x];
@@ -385,6 +390,39 @@ __global__ __launch_bounds__(256) void attn_split_combine(const AttnArgs a, int 
   }
 }
 
+// Merge of the key-split prefix pass: rows [0, pre_tokens) x Hq, one thread
+// per (row, 8 dims); writes the normalised bf16 prefix partial and its LSE
+// exactly as the unsplit pass does (the per-sequence pass merges it next).
+__global__ __launch_bounds__(256) void attn_prefix_combine(const AttnArgs a, int nsplit) {
+  const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long row = i / (D / 8);
+  const int d0 = (int)(i % (D / 8)) * 8;
+  if (row >= (long long)pre_tokens * a.Hq) return;
+  float m = -INFINITY;
+  for (int z = 0; z < nsplit; ++z) m = fmaxf(m, a.split_lse[(size_t)z * a.rows + row]);
+  const float mu = m == -INFINITY ? 0.f : m;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
+  for (int z = 0; z < nsplit; ++z) {
+    const float w = exp2f(a.split_lse[(size_t)z * a.rows + row] - mu);   // 0 for empty splits
+    den += w;
+    const f32x4* p = reinterpret_cast<const f32x4*>(a.split_o + ((size_t)z * a.rows + row) * D + d0);
+    const f32x4 v0 = p[0], v1 = p[1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc[r] += w * v0[r];
+      acc[4 + r] += w * v1[r];
+    }
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  bf16x8 o;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) o[r] = (bf16)(acc[r] * inv);
+  *reinterpret_cast<bf16x8*>(a.out + row * D + d0) = o;
+  if (d0 == 0) a.lse_out[row] = den > 0.f ? mu + __log2f(den) : -INFINITY;
+}
+
 template <int G>
 void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s, int nsplit = 1) {
   // split items double-buffer their K/V tiles (one tile in flight while the
@@ -422,7 +460,17 @@ int prefix_nw() {
 // Shared-prefix pass: 8 waves per block (32 tokens x G heads) -> half the K/V
 // tile staging per query of the 4-wave item and 4 waves per SIMD at 2 blocks/CU
 template <int G>
-void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s) {
+void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
+  if (nsplit > 1) {
+    // key-split prefix pass (few query tokens: the unsplit grid is a few
+    // dozen workgroups each walking every prefix tile), then the merge
+    constexpr int QT = 8 * (16 / G);
+    const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv, nsplit);
+    attn_kernel<8, G, 1, 0, true><<<grid, 512, 0, s>>>(a);
+    const long long n = (long long)a.pre_tokens * a.Hq * (D / 8);
+    attn_prefix_combine<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, nsplit);
+    return;
+  }
   if (prefix_nw() == 4) {
     constexpr int QT = 4 * (16 / G);
     const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
@@ -487,7 +535,7 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
 int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
                             float* lse_out, const int* pre_bt, int pre_keys, int pre_tokens,
                             int Hq, int Hkv, int head_dim, float scale, hipStream_t s,
-                            const int* pre_dims) {
+                            const int* pre_dims, int nsplit, float* split_o, float* split_lse) {
   // pre_dims != null: pre_tokens is the grid's token capacity, the actual
   // [pre_tokens, pre_keys] are read on the device (hipGraph replay)
   if (head_dim != D) return 1;
@@ -506,6 +554,10 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
   a.pre_keys = pre_keys;
   a.pre_tokens = pre_tokens;
   a.pre_dims = pre_dims;
-  ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s))
+  if (nsplit > 1 && (!split_o || !split_lse)) return 4;
+  a.split_o = split_o;
+  a.split_lse = split_lse;
+  a.rows = pre_tokens * Hq;
+  ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s, nsplit))
   return 0;
 }

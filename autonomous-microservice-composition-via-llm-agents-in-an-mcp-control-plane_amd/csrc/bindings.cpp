@@ -286,7 +286,9 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
 void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                       at::Tensor& out, at::Tensor& lse, const at::Tensor& pre_bt, int64_t pre_keys,
                       int64_t pre_tokens, double scale,
-                      const c10::optional<at::Tensor>& pre_dims) {
+                      const c10::optional<at::Tensor>& pre_dims, int64_t nsplit,
+                      const c10::optional<at::Tensor>& split_o,
+                      const c10::optional<at::Tensor>& split_lse) {
   CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
   CHECK_I32_TENSOR(pre_bt); CHECK_DEV(lse); CHECK_CONTIG(lse);
   TORCH_CHECK(lse.scalar_type() == at::kFloat, "lse f32");
@@ -301,10 +303,22 @@ void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::
     TORCH_CHECK(pre_dims->numel() == 2, "pre_dims [2]");
     dims = pre_dims->data_ptr<int>();
   }
+  float* so = nullptr;
+  float* sl = nullptr;
+  if (nsplit > 1) {
+    // fp32 partials [nsplit][pre_tokens][Hq][D] and LSE [nsplit][pre_tokens][Hq]
+    TORCH_CHECK(split_o.has_value() && split_lse.has_value(), "split prefix needs split_o / split_lse");
+    TORCH_CHECK(split_o->scalar_type() == at::kFloat && split_lse->scalar_type() == at::kFloat &&
+                    split_o->is_contiguous() && split_lse->is_contiguous(), "split buffers f32");
+    TORCH_CHECK(split_o->numel() >= nsplit * pre_tokens * Hq * D &&
+                    split_lse->numel() >= nsplit * pre_tokens * Hq, "split buffer sizes");
+    so = split_o->data_ptr<float>();
+    sl = split_lse->data_ptr<float>();
+  }
   const int rc = launch_prefix_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                          out.data_ptr(), lse.data_ptr<float>(),
                                          pre_bt.data_ptr<int>(), pre_keys, pre_tokens, Hq, Hkv, D,
-                                         (float)scale, stream(), dims);
+                                         (float)scale, stream(), dims, (int)nsplit, so, sl);
   TORCH_CHECK(rc == 0, "prefix_attention: unsupported config (code ", rc, ")");
   check_launch("prefix_attention");
 }
@@ -485,7 +499,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("split_lse") = py::none());
   m.def("prefix_attention", &prefix_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("out"), py::arg("lse"), py::arg("pre_bt"), py::arg("pre_keys"),
-        py::arg("pre_tokens"), py::arg("scale"), py::arg("pre_dims") = py::none());
+        py::arg("pre_tokens"), py::arg("scale"), py::arg("pre_dims") = py::none(),
+        py::arg("nsplit") = 1, py::arg("split_o") = py::none(), py::arg("split_lse") = py::none());
   m.def("attn_tokens_per_item", &attn_tokens_per_item);
   m.def("sample_allowed", &sample_allowed, py::arg("hidden"), py::arg("W"), py::arg("allow_ptr"),
         py::arg("allow_ids"), py::arg("ctr"), py::arg("temperature"), py::arg("seed"),

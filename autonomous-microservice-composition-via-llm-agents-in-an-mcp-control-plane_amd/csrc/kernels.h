@@ -106,7 +106,8 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
 int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
                             float* lse_out, const int* pre_bt, int pre_keys, int pre_tokens,
                             int Hq, int Hkv, int head_dim, float scale, hipStream_t s,
-                            const int* pre_dims = nullptr);
+                            const int* pre_dims = nullptr, int nsplit = 1,
+                            float* split_o = nullptr, float* split_lse = nullptr);
 
 // sampling.hip
 void launch_sample_allowed(const void* hidden, const void* W, const int* allow_ptr,

@@ -195,6 +195,26 @@ def rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D):
     return q_out
 
 
+def prefix_splits(pre_tokens: int, pre_keys: int, hkv: int, num_cus: int = 256) -> int:
+    """Key-split factor of the cascade prefix pass (csrc/attention.hip): a
+    step with few query tokens launches ceil(tokens / 32) x Hkv workgroups that
+    each walk every prefix tile; split the tiles so the grid reaches ~2
+    workgroups per CU, >= 2 tiles per split.  ``pre_tokens`` / ``pre_keys``
+    are the grid capacities under a hipGraph.  ``MCP_PREFIX_SPLIT``: 0 off
+    (default: measured no faster at 40-120 intents/s, config 5 p50 173.5 /
+    234 / 379 ms split vs 176 / 228 / 357 unsplit,
+    profiles/attention_tuning.md), -1 auto, N forces N."""
+    forced = int(os.environ.get("MCP_PREFIX_SPLIT", "0"))
+    if forced == 0:
+        return 1
+    tiles = pre_keys // 64
+    grid = -(-pre_tokens // 32) * hkv
+    if forced > 1:
+        return max(1, min(forced, tiles))
+    ns = min(-(-2 * num_cus // max(grid, 1)), tiles // 2, 8)
+    return ns if ns >= 2 else 1
+
+
 def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
     """``meta`` is an ``AttnMeta`` (engine.batch) holding the per-sequence and
     work-list int32 tensors."""
@@ -209,8 +229,16 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
             # with device pre_dims (hipGraph) the sizes are read on the device
             pre_o = torch.empty_like(q)
             pre_lse = torch.empty(q.shape[0], q.shape[1], device=q.device, dtype=torch.float32)
+            ps = prefix_splits(meta.pre_tokens, meta.pre_keys, k_cache.shape[1])
+            kw_split = {}
+            if ps > 1:
+                kw_split = {"nsplit": ps,
+                            "split_o": torch.empty(ps * meta.pre_tokens * q.shape[1] * q.shape[2],
+                                                   device=q.device, dtype=torch.float32),
+                            "split_lse": torch.empty(ps * meta.pre_tokens * q.shape[1],
+                                                     device=q.device, dtype=torch.float32)}
             L.prefix_attention(q, k_cache, v_cache, pre_o, pre_lse, meta.pre_bt, meta.pre_keys,
-                               meta.pre_tokens, scale, pre_dims=pre_dims)
+                               meta.pre_tokens, scale, pre_dims=pre_dims, **kw_split)
             kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         ns = int(getattr(meta, "kv_splits", 1))
         for nw, ws, wq in meta.work_lists():
