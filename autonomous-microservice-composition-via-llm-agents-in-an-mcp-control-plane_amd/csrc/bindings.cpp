@@ -177,12 +177,6 @@ void gemm_plan_set_splits_py(int64_t N, int64_t K, const std::vector<int64_t>& s
   gemm_plan_set_splits((int)N, (int)K, c.data(), (int)c.size());
 }
 
-void gemm_plan_set_pipes_py(int64_t N, int64_t K, const std::vector<int64_t>& pipes) {
-  std::vector<int> c(pipes.begin(), pipes.end());
-  for (int v : c) TORCH_CHECK(v == 0 || v == 1, "gemm plan pipe must be 0 or 1");
-  gemm_plan_set_pipes((int)N, (int)K, c.data(), (int)c.size());
-}
-
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
   TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
@@ -470,11 +464,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_set_splits", &gemm_plan_set_splits_py,
         "measured split-K of the 128^2 path for one (N, K): a count per 64-row M bucket (0 = rule)");
   m.def("gemm_plan_split", &gemm_plan_split);
-  m.def("gemm_plan_set_pipes", &gemm_plan_set_pipes_py,
-        "per 64-row M bucket: 1 = the deep-pipelined 128^2 kernel (gemm_tn_128p) for code 0");
-  m.def("gemm_plan_pipe", &gemm_plan_pipe);
-  m.def("gemm128_pipe_force", [](int64_t v) { gemm128_pipe_force((int)v); },
-        "-1: the plan decides, 0 / 1 forces the 2-stage / deep-pipelined 128^2 kernel");
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_plan_lookup", &gemm_plan_lookup);
   m.def("gemm_splitk_init", [](int64_t bytes) { return gemm_splitk_init((size_t)bytes); },

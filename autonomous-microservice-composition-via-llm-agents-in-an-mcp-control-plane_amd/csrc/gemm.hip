@@ -155,144 +155,6 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
   }
 }
 
-// Deep-pipelined form of gemm_tn_128 for the latency-bound middle range
-// (M = 128-1024 serving steps, usually split-K): the 2-stage loop above ends
-// every k-tile in a __syncthreads(), whose fence waits vmcnt(0) - the next
-// tile's LDS-DMA must land within ONE k-tile of MFMAs (~0.2 us), and at these
-// M a workgroup spent ~1.2 us per k-tile waiting (qkv M = 384: 39 us vs
-// hipBLASLt 30).  Here NST LDS stages with NST - 2 tiles in flight across a
-// raw s_barrier and a counted vmcnt (cdna_hip_programming.md §5 "Pipelining
-// across barriers"); ONE barrier per k-tile.  Every iteration issues one
-// tile's DMAs (past the end: the last tile again, into the slot just freed)
-// so the vmcnt counts are static.  One workgroup per CU (NST x 32 KiB LDS).
-template <int EPI, typename OutT, bool SPLIT, int NST>
-__global__ __launch_bounds__(256, 1) void gemm_tn_128p(const bf16* __restrict__ X,
-                                                       const bf16* __restrict__ W,
-                                                       OutT* __restrict__ Y,
-                                                       const bf16* __restrict__ R, int M, int N,
-                                                       int K) {
-  static_assert(NST >= 3 && NST <= 4, "stages");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NST * 2 * TILE_ELEMS];   // [stage][A|B][128][64]
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  const int nwg = nm * nn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * nn;
-  const int g = wg / per_group;
-  const int first_m = g * GROUP;
-  const int gsz = min(nm - first_m, GROUP);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int klen = SPLIT ? K / (int)gridDim.y : K;
-  const int kbeg = SPLIT ? (int)blockIdx.y * klen : 0;
-  if constexpr (SPLIT) Y += (size_t)blockIdx.y * M * N;
-
-  const int lrow = lane >> 3;
-  const int lchunk = (lane & 7) ^ lrow;
-  const bf16* srcA[4];
-  const bf16* srcB[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + lrow;
-    srcA[i] = X + (size_t)min(m0 + row, M - 1) * K + kbeg + lchunk * 8;
-    srcB[i] = W + (size_t)min(n0 + row, N - 1) * K + kbeg + lchunk * 8;
-  }
-  const int nk = klen / BK;
-  auto stage = [&](int kt, int slot) {                 // 8 DMA instructions per wave
-    const int koff = min(kt, nk - 1) * BK;
-    bf16* la = smem + (slot * 2 + 0) * TILE_ELEMS;
-    bf16* lb = smem + (slot * 2 + 1) * TILE_ELEMS;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      glds16(srcA[i] + koff, la + (wave * 4 + i) * 512);
-      glds16(srcB[i] + koff, lb + (wave * 4 + i) * 512);
-    }
-  };
-
-  const int wm = wave >> 1, wn = wave & 1;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t) stage(t, t);
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    // tiles kt .. kt + NST - 2 are in flight: wait for kt's 8 (own waves')
-    if constexpr (NST == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();                     // every wave's DMAs of kt landed, slot kt-1 free
-    asm volatile("" ::: "memory");
-    stage(kt + NST - 1, (kt + NST - 1) % NST);
-    const int cur = kt % NST;
-    const bf16* la = smem + (cur * 2 + 0) * TILE_ELEMS;
-    const bf16* lb = smem + (cur * 2 + 1) * TILE_ELEMS;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + fq;
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int ra = wm * 64 + t * 16 + fr;
-        const int rb = wn * 64 + t * 16 + fr;
-        af[t] = *reinterpret_cast<const bf16x8*>(la + ra * BK + ((c ^ (ra & 7)) << 3));
-        bfr[t] = *reinterpret_cast<const bf16x8*>(lb + rb * BK + ((c ^ (rb & 7)) << 3));
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(bfr[nt], af[mt], acc[mt][nt]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // fragments read before the slot is reused
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // the trailing re-loads land before exit
-
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int m = m0 + wm * 64 + mt * 16 + fr;
-    if (m >= M) continue;
-    if constexpr (EPI == 2) {
-      const int F = N >> 1;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int f = ((n0 + wn * 64) >> 1) + p * 16 + fq * 4;
-        if (f >= F) continue;
-        const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
-        *reinterpret_cast<bf16x4*>((bf16*)Y + (size_t)m * F + f) = o;
-      }
-      continue;
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int n = n0 + wn * 64 + nt * 16 + fq * 4;
-      if (n >= N) continue;
-      f32x4 v = acc[mt][nt];
-      if (EPI == 1) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
-      }
-      if constexpr (sizeof(OutT) == 4) {
-        *reinterpret_cast<f32x4*>(Y + (size_t)m * N + n) = v;
-      } else {
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-        *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
-      }
-    }
-  }
-}
-
 // Sum of the S fp32 split-K partials [S][M][N] + the epilogue; one thread per
 // 4 outputs (EPI 2: gate column 32 j + i pairs with up column 32 j + 16 + i,
 // the interleaved SwiGLU layout, output f = 16 j + i).
@@ -362,7 +224,6 @@ struct GemmPlan {
   int N, K;
   std::vector<signed char> code;
   std::vector<signed char> split;    // measured split-K of the 128^2 path (0: the rule)
-  std::vector<signed char> pipe;     // 1: the deep-pipelined 128^2 kernel measured faster
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -374,7 +235,7 @@ void gemm_plan_set(int N, int K, const int* codes, int n) {
       p.code = std::move(c);
       return;
     }
-  g_plans.push_back({N, K, std::move(c), {}, {}});
+  g_plans.push_back({N, K, std::move(c), {}});
 }
 
 void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
@@ -383,25 +244,7 @@ void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
       p.split.assign(splits, splits + n);
       return;
     }
-  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n), {}});
-}
-
-void gemm_plan_set_pipes(int N, int K, const int* pipes, int n) {
-  for (auto& p : g_plans)
-    if (p.N == N && p.K == K) {
-      p.pipe.assign(pipes, pipes + n);
-      return;
-    }
-  g_plans.push_back({N, K, {}, {}, std::vector<signed char>(pipes, pipes + n)});
-}
-
-int gemm_plan_pipe(int M, int N, int K) {
-  for (const auto& p : g_plans)
-    if (p.N == N && p.K == K) {
-      const size_t b = (size_t)((M + 63) / 64) - 1;
-      return b < p.pipe.size() ? p.pipe[b] : 0;
-    }
-  return 0;
+  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n)});
 }
 
 // measured split count for the 128^2 path at this M bucket (0 = none recorded)
@@ -550,34 +393,12 @@ int gemm128_splits(int M, int N, int K) {
   return best;
 }
 
-// 128^2 path: the 2-stage kernel or the deep-pipelined one (gemm_tn_128p)
-namespace {
-int g_pipe_force = -1;                 // gemm128_pipe_force (tuning, tests)
-}  // namespace
-
-void gemm128_pipe_force(int v) { g_pipe_force = v; }
-
-int gemm128_pipe(int M, int N, int K) {
-  static int env = -2;
-  if (env == -2) {
-    const char* e = getenv("MCP_GEMM128_PIPE");
-    env = e ? atoi(e) : -1;                          // -1: the plan decides
-  }
-  if (g_pipe_force >= 0) return g_pipe_force;
-  if (env >= 0) return env;
-  return gemm_plan_pipe(M, N, K);
-}
-
 // EPI 0/1/2 through S split-K partials + the reduce; false if not split
 static bool launch_gemm_128_split(const void* X, const void* W, void* Y, const void* R, int M,
                                   int N, int K, int epi, hipStream_t s) {
   const int S = gemm128_splits(M, N, K);
   if (S <= 1) return false;
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-  if (gemm128_pipe(M, N, K) && (K / S) / BK >= 3)
-    gemm_tn_128p<0, float, true, 4><<<dim3(nm * nn, S), 256, 0, s>>>(
-        (const bf16*)X, (const bf16*)W, g_splitk_ws, nullptr, M, N, K);
-  else
   gemm_tn_128<0, float, true><<<dim3(nm * nn, S), 256, 0, s>>>(
       (const bf16*)X, (const bf16*)W, g_splitk_ws, nullptr, M, N, K);
   const size_t n4 = (size_t)M * (epi == 2 ? N / 2 : N) / 4;
@@ -595,16 +416,9 @@ static void launch_gemm_tn_128(const void* X, const void* W, void* Y, const void
   if (launch_gemm_128_split(X, W, Y, R, M, N, K, R ? 1 : 0, s)) return;
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   const dim3 grid(nm * nn);
-  const bool pipe = gemm128_pipe(M, N, K) && K / BK >= 3;
-  if (R && pipe)
-    gemm_tn_128p<1, bf16, false, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                         (const bf16*)R, M, N, K);
-  else if (R)
+  if (R)
     gemm_tn_128<1><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
                                         (const bf16*)R, M, N, K);
-  else if (pipe)
-    gemm_tn_128p<0, bf16, false, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                         nullptr, M, N, K);
   else
     gemm_tn_128<0><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N,
                                         K);
@@ -658,10 +472,6 @@ int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K,
     launch_gemm_tn_256_silu(X, W, Y, M, N, K, s);
   } else if (!launch_gemm_128_split(X, W, Y, nullptr, M, N, K, 2, s)) {
     const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
-    if (gemm128_pipe(M, N, K) && K / BK >= 3)
-      gemm_tn_128p<2, bf16, false, 4><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W,
-                                                                   (bf16*)Y, nullptr, M, N, K);
-    else
     gemm_tn_128<2><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
                                                  nullptr, M, N, K);
   }

@@ -71,9 +71,6 @@ void gemm_splitk_force(int S);   // -1 auto, 0/1 off, S > 1 forced where admissi
 void gemm_plan_set(int N, int K, const int* codes, int n);
 void gemm_plan_set_splits(int N, int K, const int* splits, int n);
 int gemm_plan_split(int M, int N, int K);
-void gemm_plan_set_pipes(int N, int K, const int* pipes, int n);
-int gemm_plan_pipe(int M, int N, int K);
-void gemm128_pipe_force(int v);
 void gemm_plan_clear();
 int gemm256d_ok(int M, int N, int K);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]

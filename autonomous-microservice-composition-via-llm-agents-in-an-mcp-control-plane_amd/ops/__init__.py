@@ -67,8 +67,6 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
         mod.gemm_plan_set(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["codes"]])
         if "splits" in sh and hasattr(mod, "gemm_plan_set_splits"):
             mod.gemm_plan_set_splits(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["splits"]])
-        if "pipes" in sh and hasattr(mod, "gemm_plan_set_pipes"):
-            mod.gemm_plan_set_pipes(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["pipes"]])
     return len(plan["shapes"])
 
 

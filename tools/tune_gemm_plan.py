@@ -8,8 +8,7 @@ are timed interleaved (3 rounds x 10 launches, min): code 0 = 128^2 kernel,
 fastest wins unless it beats the runner-up with the smaller code by < 1 %
 (hysteresis keeps the plan stable against timing noise).  Code 0 is timed at
 split-K 1 / 2 / 4 / 8 (2 / 4 / 8 below 129 rows, where "no split" means the
-skinny kernel), each with the 2-stage and the deep-pipelined 128^2 kernel,
-and the best (split, kernel) is recorded per bucket ("splits", "pipes"; the
+skinny kernel) and its best split is recorded per bucket ("splits"; the
 serving steps' M = 64-768 range, where the split rule alone was up to 20 %
 off, profiles/gemm_tuning.md).
 
@@ -40,13 +39,11 @@ dev = "cuda"
 s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
-def run(code, X, W, Y, split=-1, pipe=0):
+def run(code, X, W, Y, split=-1):
     if code == 0:
         L.gemm_splitk_force(split)
-        L.gemm128_pipe_force(pipe)
         L.gemm(X, W, Y, None, 0)
         L.gemm_splitk_force(-1)
-        L.gemm128_pipe_force(-1)
     else:
         L.gemm_variant(X, W, Y, 49 if code == 1 else 51)
 
@@ -64,32 +61,30 @@ def time_ms(fn, reps=10):
 result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
           "mstep": MSTEP, "codes": "0=128x128, 1=AGPR 256-row tiles, 2=AGPR 192-row tiles",
           "splits": "measured split-K of code 0 per bucket (0 = the rule)",
-          "pipes": "1 = code 0 runs the deep-pipelined 128^2 kernel (gemm_tn_128p)",
           "generated": time.strftime("%Y-%m-%d"), "shapes": []}
 t0 = time.time()
 for (N, K) in SHAPES:
     Xf = torch.randn(m_max, K, device=dev).bfloat16()
     W = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
     Yf = torch.empty(m_max, N, device=dev, dtype=torch.bfloat16)
-    codes, tf, splits, pipes = [], [], [], []
+    codes, tf, splits = [], [], []
     for b in range(m_max // MSTEP):
         M = (b + 1) * MSTEP
         X, Y = Xf[:M], Yf[:M]
         # code-0 candidates: (0, split)
         svals = ([2, 4, 8] if M <= 128 else [1, 2, 4, 8]) if M <= M_SPLIT_MAX else [-1]
-        cands = [(0, sv, pp) for sv in svals for pp in (0, 1)]
+        cands = [(0, sv) for sv in svals]
         if M >= M_MIN and K % 128 == 0 and N % 256 == 0:
-            cands += [(1, -1, 0), (2, -1, 0)]
+            cands += [(1, -1), (2, -1)]
         best = {c: float("inf") for c in cands}
         for _ in range(3):
             for c in cands:
-                best[c] = min(best[c], time_ms(lambda c=c: run(c[0], X, W, Y, c[1], c[2])))
+                best[c] = min(best[c], time_ms(lambda c=c: run(c[0], X, W, Y, c[1])))
         c0 = min((c for c in cands if c[0] == 0), key=lambda c: best[c])
         splits.append(max(c0[1], 0))
-        pipes.append(c0[2])
         if M < M_MIN:
             codes.append(-1)
-            tf.append({f"0s{c[1]}p{c[2]}": round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
+            tf.append({f"0s{c[1]}": round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
             continue
         best = {0: best[c0], **{c[0]: best[c] for c in cands if c[0] != 0}}
         cands = sorted(best)
@@ -100,8 +95,7 @@ for (N, K) in SHAPES:
                 win = c
         codes.append(win)
         tf.append({str(c): round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
-    result["shapes"].append({"N": N, "K": K, "codes": codes, "splits": splits, "pipes": pipes,
-                             "tflops": tf})
+    result["shapes"].append({"N": N, "K": K, "codes": codes, "splits": splits, "tflops": tf})
     print(json.dumps({"N": N, "K": K, "codes": codes, "s": round(time.time() - t0, 1)}), flush=True)
     del Xf, W, Yf
 with open(out_path, "w") as f:
