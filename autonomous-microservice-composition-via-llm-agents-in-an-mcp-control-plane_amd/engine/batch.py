@@ -75,11 +75,13 @@ def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
     if forced > 1:
         return forced
     work = items * hkv
-    if work >= num_cus or tiles < 16:
+    if work >= num_cus or tiles < 8:
         return 1
     # ~2 workgroups per CU (measured best at batch 1 / 4 and 8k-128k contexts,
-    # profiles/attention_splitkv.jsonl)
-    ns = min(tiles // 4, -(-2 * num_cus // work), 128)
+    # profiles/attention_splitkv.jsonl); >= 4 key tiles per split there, >= 2
+    # for the ~700-1000-key contexts of a single intent (config 2: 4-8 splits
+    # of 11-16 tiles measured 113 ms p50 vs 119 unsplit)
+    ns = min(tiles // 4 if tiles >= 32 else tiles // 2, -(-2 * num_cus // work), 128)
     sum_tokens = max(sum(q_lens), 1)
     while ns > 1 and ns * sum_tokens * hq * 128 * 4 > max_bytes:
         ns //= 2

@@ -337,6 +337,7 @@ class LLMEngine:
         return done
 
     PIPELINE_MAX_TOKENS = 1024
+    CASCADE_MIN_SHARERS = 4
     PIPELINE_MIN_SEQS = 64
 
     def _pipelined_now(self) -> bool:
@@ -384,8 +385,11 @@ class LLMEngine:
                 casc = next(q.prefix for q in pool if q.prefix is not None and id(q.prefix) == best)
                 # the prefix pass has ~(sharing tokens / 32) x Hkv workgroups: for a
                 # long prefix shared by few sequences that underfills the chip,
-                # while per-sequence attention can split the key range (split-KV)
-                if casc.length >= 16 * BLOCK_SIZE and n_share < 16:
+                # while per-sequence attention can split the key range (split-KV);
+                # with a handful of sharers the per-sequence split-KV path is
+                # faster at any prefix length (config 2, one intent: p50 121 ->
+                # 113 ms, profiles/config2_attention_ab.jsonl)
+                if (casc.length >= 16 * BLOCK_SIZE and n_share < 16) or n_share < self.CASCADE_MIN_SHARERS:
                     casc = None
         order = pool
         if casc is not None:

@@ -345,12 +345,14 @@ def test_engine_stall_recovers_after_the_step_returns():
 
 
 def test_kv_split_rule():
-    """Split-KV only for decode-sized items that underfill the chip with long
-    own key ranges; >= 4 tiles per split; forced / disabled by MCP_KV_SPLIT."""
+    """Split-KV only for decode-sized items that underfill the chip with own
+    key ranges of >= 8 tiles; >= 4 tiles per split from 32 tiles, >= 2 below
+    (a single intent's ~700-key context); forced / disabled by MCP_KV_SPLIT."""
     from mcp_amd.engine.batch import choose_kv_splits
     assert choose_kv_splits([1], [32768], 4, 8) == 64          # batch-1 decode, 32k keys
     assert choose_kv_splits([1] * 4, [32768] * 4, 4, 8) == 16
-    assert choose_kv_splits([1], [700], 4, 8) == 1               # short context
+    assert choose_kv_splits([1], [700], 4, 8) == 5               # single intent: 11 tiles / 2
+    assert choose_kv_splits([1], [400], 4, 8) == 1               # < 8 tiles: unsplit
     assert choose_kv_splits([1] * 64, [8192] * 64, 4, 8) == 1    # 512 items already fill it
     assert choose_kv_splits([300], [32768], 4, 8) == 1           # prefill chunk: 4-wave items
     assert choose_kv_splits([1], [2048], 4, 8) == 8              # 32 tiles -> 8 splits of 4
