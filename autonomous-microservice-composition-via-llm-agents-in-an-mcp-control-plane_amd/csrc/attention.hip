@@ -325,15 +325,19 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
 // ...; lane = (row l & 15, 32-wide d slice).  Each wave keeps its own running
 // max / weighted sum (loads of 4 splits in flight), then the 4 waves' partial
 // results are merged through LDS.
-template <int G>
+template <int G, int NWI = 1>
 __global__ __launch_bounds__(256) void attn_split_combine(const AttnArgs a, int nsplit) {
+  // NWI = waves of the split items: a 4-wave item's 4 row groups of 16 are
+  // merged by 4 consecutive workgroups
   constexpr int CW = 4;
+  constexpr int TPW = 16 / G;
   __shared__ float red_m[CW][64], red_d[CW][64];
   __shared__ float red_o[CW][32][65];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, dq = lane >> 4;
-  const int s = a.work_seq[blockIdx.x];
-  const int tok = a.work_q0[blockIdx.x] + fr / G;
+  const int item = blockIdx.x / NWI, sub = blockIdx.x % NWI;
+  const int s = a.work_seq[item];
+  const int tok = a.work_q0[item] + sub * TPW + fr / G;
   const bool valid = tok < a.q_len[s];
   const int head = blockIdx.y * G + fr % G;
   const size_t row = (size_t)(a.q_start[s] + (valid ? tok : 0)) * a.Hq + head;
@@ -437,6 +441,12 @@ void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s, int nspl
     attn_split_combine<G><<<dim3(nwork, a.Hkv), 256, 0, s>>>(a, nsplit);
     return;
   }
+  if (nw == 4 && nsplit > 1) {
+    // 4-wave items (jump-forward spans) of a few long-context sequences
+    attn_kernel<4, G, 0, 2, true><<<dim3(nwork, a.Hkv, nsplit), 256, 0, s>>>(a);
+    attn_split_combine<G, 4><<<dim3(nwork * 4, a.Hkv), 256, 0, s>>>(a, nsplit);
+    return;
+  }
   const dim3 grid(nwork, a.Hkv);
   static const int nw1_bufs = getenv("MCP_ATTN_NW1_BUFS") ? atoi(getenv("MCP_ATTN_NW1_BUFS")) : 1;
   if (nw == 1 && nw1_bufs == 2)
@@ -506,7 +516,7 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
   if (head_dim != D) return 1;
   if (nw != 1 && nw != 4) return 2;
   if (nwork <= 0) return 0;
-  if (nsplit > 1 && (nw != 1 || !split_o || !split_lse)) return 4;
+  if (nsplit > 1 && (!split_o || !split_lse)) return 4;
   AttnArgs a{};
   a.q = (const bf16*)q;
   a.kc = (const bf16*)k_cache;

@@ -245,7 +245,7 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   TORCH_CHECK(block_table.dim() == 2, "block_table [S, max_blocks]");
   TORCH_CHECK(work_seq.numel() == work_q0.numel(), "work list");
   if (nsplit > 1) {
-    TORCH_CHECK(nw == 1, "split-KV serves the 1-wave (decode) items");
+    TORCH_CHECK(nw == 1 || nw == 4, "split-KV serves 1- and 4-wave items");
     TORCH_CHECK(split_o.has_value() && split_lse.has_value(), "split-KV needs split_o / split_lse");
     TORCH_CHECK(split_o->scalar_type() == at::kFloat && split_o->is_contiguous() &&
                 split_o->numel() >= nsplit * q.numel(), "split_o [nsplit, T, Hq, D] f32");

@@ -52,24 +52,28 @@ N_SIZES = 19            # packed segments of pack_host (the layout's leading ent
 
 def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
                      max_bytes: int = 64 << 20, hq: int = 32) -> int:
-    """Split-KV factor for the 1-wave (decode-sized) attention items of a step
-    (csrc/attention.hip KSPLIT).  A step of few sequences with long contexts has
-    few work items (one per sequence and kv head) on 256 CUs - batch-1 decode
-    on 8B is 8 workgroups walking the whole context.  Split each item's own key
-    range (``kv_lens`` = keys it attends itself, after any cascade prefix) so
-    the grid reaches ~2 workgroups per CU, keeping >= 4 key tiles per split.
+    """Split-KV factor for the attention items of a step (csrc/attention.hip
+    KSPLIT, 1-wave and 4-wave items).  A step of few sequences with long
+    contexts has few work items (one per sequence and kv head) on 256 CUs -
+    batch-1 decode on 8B is 8 workgroups walking the whole context.  Split each
+    item's own key range (``kv_lens`` = keys it attends itself, after any
+    cascade prefix) so the grid reaches ~2 workgroups per CU (prefill chunks
+    make enough items and are never split).
     ``MCP_KV_SPLIT``: 0 disables, N > 1 forces N."""
     forced = int(os.environ.get("MCP_KV_SPLIT", "-1"))
     if forced == 0:
         return 1
     t1 = tokens_per_item(1, group)
+    t4 = tokens_per_item(4, group)
     cutoff = int(os.environ.get("MCP_ATTN_NW1_CUTOFF", str(t1 * 2)))
     items, tiles, rows = 0, 0, 0
     for ql, kl in zip(q_lens, kv_lens):
-        if 0 < ql <= cutoff:
-            items += -(-ql // t1)
-            tiles = max(tiles, -(-kl // 64))
-            rows += ql
+        if ql <= 0:
+            continue
+        # 1-wave items (decode) and 4-wave items (jump-forward spans) both split
+        items += -(-ql // t1) if ql <= cutoff else -(-ql // t4)
+        tiles = max(tiles, -(-kl // 64))
+        rows += ql
     if items == 0:
         return 1
     if forced > 1:

@@ -240,8 +240,8 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
             kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         ns = int(getattr(meta, "kv_splits", 1))
         for nw, ws, wq in meta.work_lists():
-            if nw == 1 and ns > 1:
-                # split-KV decode (K6): fp32 partials + LSE per split, merged in-kernel
+            if ns > 1:
+                # split-KV (K6): fp32 partials + LSE per split, merged by a second kernel
                 so = torch.empty(ns, *q.shape, device=q.device, dtype=torch.float32)
                 sl = torch.empty(ns, q.shape[0], q.shape[1], device=q.device, dtype=torch.float32)
                 L.paged_attention(q, k_cache, v_cache, out, meta.q_start, meta.q_len,

@@ -159,9 +159,12 @@ def test_paged_attention_split_kv_long_context(ctx, batch):
 
 def test_paged_attention_split_kv_uneven():
     """Split counts that do not divide the tiles, splits with no tiles (short
-    contexts), mixed with 4-wave items of the same step."""
+    contexts), 4-wave items (jump-forward spans, 70 tokens) split too."""
     for ns in (3, 7, 32):
         out, exp = _attn_case([1, 1, 1, 70, 2], [5000, 65, 900, 700, 64], 32, 8, seed=7, kv_splits=ns)
+        assert rel_err(out, exp) < 2e-2
+    for ns in (2, 5):                     # only 4-wave items, one sequence, 1k-4k keys
+        out, exp = _attn_case([12, 30], [1000, 4100], 32, 8, seed=8, kv_splits=ns)
         assert rel_err(out, exp) < 2e-2
 
 

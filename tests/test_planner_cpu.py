@@ -354,7 +354,8 @@ def test_kv_split_rule():
     assert choose_kv_splits([1], [700], 4, 8) == 5               # single intent: 11 tiles / 2
     assert choose_kv_splits([1], [400], 4, 8) == 1               # < 8 tiles: unsplit
     assert choose_kv_splits([1] * 64, [8192] * 64, 4, 8) == 1    # 512 items already fill it
-    assert choose_kv_splits([300], [32768], 4, 8) == 1           # prefill chunk: 4-wave items
+    assert choose_kv_splits([300], [32768], 4, 8) == 4           # 19 4-wave items: underfilled
+    assert choose_kv_splits([3000], [32768], 4, 8) == 1          # a big prefill fills the chip
     assert choose_kv_splits([1], [2048], 4, 8) == 8              # 32 tiles -> 8 splits of 4
     import os
     os.environ["MCP_KV_SPLIT"] = "0"
