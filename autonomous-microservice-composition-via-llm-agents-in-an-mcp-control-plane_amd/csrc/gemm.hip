@@ -436,18 +436,19 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
 // the HBM roof with COLD weights (the serving case, tools/bench_cold_small_m.py:
 // gate|up 38.8-44.5 us at M = 1-8 = 6 TB/s, vs 54 us through split-K 128^2 or
 // the stream kernel; o / down / qkv 2-4 % faster at M <= 4)
-static bool skinny_first(int M, int N) {
+static bool skinny_first(int M, int N, int K) {
   static int on = -1;
   if (on < 0) {
     const char* e = getenv("MCP_GEMM_SKINNY_FIRST");
     on = e ? atoi(e) : 1;
   }
-  return on && (M <= 4 || (N >= 16384 && M <= 12));
+  // o-proj sized (N, K <= 4096): skinny up to 16 rows (8.0-10.0 vs 7.8-10.5 us)
+  return on && (M <= 4 || (N >= 16384 && M <= 8) || (N <= 4096 && K <= 4096 && M <= 16));
 }
 
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     hipStream_t s) {
-  if (skinny_first(M, N) && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;
+  if (skinny_first(M, N, K) && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;
   if (gemm_stream_enabled() && gemm_stream_pick(M, N, K, R ? 1 : 0) &&
       launch_gemm_stream(X, W, Y, R, M, N, K, R ? 1 : 0, RopeArgs{}, s) == 0)
     return;
@@ -476,7 +477,7 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
                              hipStream_t s);
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (N % 64) return 1;
-  if (skinny_first(M, N) && launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0) return 0;
+  if (skinny_first(M, N, K) && launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0) return 0;
   if (gemm_stream_enabled() && gemm_stream_pick(M, N, K, 2) &&
       launch_gemm_stream(X, W, Y, nullptr, M, N, K, 2, RopeArgs{}, s) == 0)
     return 0;

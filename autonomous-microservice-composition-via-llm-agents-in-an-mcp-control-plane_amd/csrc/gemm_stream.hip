@@ -326,6 +326,9 @@ int gemm_stream_splits(int M, int N, int K, int epi) {
   const int tiles = N / 64;
   const int nsteps = K / SW_STEP;
   if (g_stream_force_s > 0) return g_stream_force_s;
+  // wide projections (gate|up, 448 tiles): measured with cold weights
+  // (tools/bench_cold_stream.py) S = 3 at M <= 16, no split above
+  if (tiles >= 256) return M <= 16 ? 3 : 1;
   const int target = 2 * gemm256_num_cus();
   int S = 1;
   while (S < 8 && tiles * S * 2 <= target + tiles && nsteps / (2 * S) >= 4 * SW_WAVES) S *= 2;
@@ -341,7 +344,11 @@ bool gemm_stream_pick(int M, int N, int K, int epi) {
   // 4096^2) up to M = 64; QKV + RoPE (epi 3) also saves the rope_kv launch up
   // to M = 64.  gate|up (N = 28672) keeps the 128^2 path (448 workgroups at
   // S = 2 already stream at ~6 TB/s).
-  if (M > 64 || N >= 16384) return false;
+  if (M > 64) return false;
+  // gate|up (N >= 16384): cold-weight sweep (tools/bench_cold_stream.py), the
+  // stream kernel beats split-K 128^2 at M = 9-32 (48.9-55.3 vs 51.3-59.7 us);
+  // M <= 8 / 12 go to the skinny kernel first (gemm.hip skinny_first)
+  if (N >= 16384) return M > 8 && M <= 32;
   if (M <= 32 || epi == 3) return true;
   return (long long)N * K <= 4096LL * 4096LL;
 }
