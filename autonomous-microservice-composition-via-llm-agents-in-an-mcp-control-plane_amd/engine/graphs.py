@@ -8,8 +8,8 @@ Python the launches, not the GPU, set the step time.  Steps with at most
 ``max(BUCKETS)`` tokens are therefore replayed from a captured hipGraph
 (``torch.cuda.CUDAGraph`` is the HIP graph API on ROCm).  A graph is keyed by
 (token bucket, sequence-capacity class, block-table width class, split-KV
-factor), captured at start-up (``warm``) or lazily on first use, after one
-eager warm-up of the same static step.  Every step of
+factor, cascade on / off), captured at start-up (``warm``) or lazily on first
+use, after one eager warm-up of the same static step.  Every step of
 a key uses ONE fixed int32 layout (``pack_static``):
 
 * tokens padded to the bucket size (padding writes no KV: slot -1), sequence
@@ -62,7 +62,7 @@ MIN_WIDTH = 32                 # block-table width classes: 32, 128, 512, ... bl
 
 @dataclasses.dataclass
 class _Bucket:
-    key: Tuple[int, int, int, int]
+    key: Tuple[int, int, int, int, int]
     sizes: List[int]
     S: int
     buf: torch.Tensor
@@ -90,7 +90,7 @@ class GraphRunner:
         self.temperature, self.seed = float(temperature), int(seed)
         self.buckets = tuple(sorted(buckets))
         self.max_seqs = int(max_seqs)
-        self._b: Dict[Tuple[int, int, int, int], _Bucket] = {}
+        self._b: Dict[Tuple[int, int, int, int, int], _Bucket] = {}
         self._pool = None
         self.stager = HostStager(self.device)
         self.replays = 0
@@ -230,19 +230,20 @@ class GraphRunner:
         self._b[tuple(int(x) for x in key)].graph.replay()
         self.replays += 1
 
-    def _get(self, key: Tuple[int, int, int, int]) -> _Bucket:
+    def _get(self, key: Tuple[int, int, int, int, int]) -> _Bucket:
         e = self._b.get(key)
         if e is not None:
             return e
         t0 = time.perf_counter()
-        b, sb, w, ns = key
+        b, sb, w, ns, casc = key
         sizes = self._sizes(b, w, sb)
         S_b = self._caps(b, sb)[0]
         buf = torch.zeros(sum(sizes), dtype=torch.int32, device=self.device)
         e = _Bucket(key=key, sizes=sizes, S=S_b, buf=buf)
         buf.copy_(torch.from_numpy(self.pack_static(None, b, w, sb=sb)))
-        # pre_tokens -1: cascade sizes live on the device (batch.views)
-        e.dstep, e.csrc, e.cdst = views(buf, sizes + [S_b, -1, ns])
+        # pre_tokens -1: cascade sizes live on the device (batch.views); the
+        # graphs of non-cascade steps launch no prefix pass at all
+        e.dstep, e.csrc, e.cdst = views(buf, sizes + [S_b, -1 if casc else 0, ns])
         self._body(e)                                   # eager warm-up (lazy allocations)
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
@@ -269,11 +270,12 @@ class GraphRunner:
             for sb in self.seq_classes(b):
                 for w in widths:
                     for ns in kv_splits:
-                        key = (b, sb, w, int(ns))
-                        if self.bcast is not None:      # workers capture in lockstep
-                            self._launch_tp(key, self.pack_static(None, b, w, sb=sb))
-                        else:
-                            self._get(key)
+                        for casc in (0, 1):
+                            key = (b, sb, w, int(ns), casc)
+                            if self.bcast is not None:      # workers capture in lockstep
+                                self._launch_tp(key, self.pack_static(None, b, w, sb=sb))
+                            else:
+                                self._get(key)
         return self.captures - n0
 
     def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1) -> Optional[torch.Tensor]:
@@ -291,7 +293,8 @@ class GraphRunner:
         host = self.pack_static(step, b, w, copies, sb)
         if host is None:
             return None
-        key = (b, sb, w, int(kv_splits))
+        casc = int(step.pre_tokens > 0 and step.pre_bt is not None and len(step.pre_bt) > 0)
+        key = (b, sb, w, int(kv_splits), casc)
         if self.bcast is not None:
             e = self._launch_tp(key, host)
         else:

@@ -233,6 +233,7 @@ class StepBroadcaster:
         hdr = np.full(self.HDR, 0, np.int32)
         hdr[0], hdr[1] = n, self.GRAPH
         hdr[2:2 + len(key)] = key
+        hdr[self.HDR - 1] = len(key)
         self._bcast(torch.from_numpy(hdr).to(self.device))
 
     def send_payload(self, payload: torch.Tensor) -> None:
@@ -255,7 +256,7 @@ class StepBroadcaster:
         if n < 0:
             return None
         if nl == self.GRAPH:
-            key = tuple(int(x) for x in h[2:6])
+            key = tuple(int(x) for x in h[2:2 + int(h[self.HDR - 1])])
             buf = graph_buffer(key)[:n]
             if n:
                 self._bcast(buf)
