@@ -74,6 +74,11 @@ struct AttnArgs {
   // the kernel (the grid covers the bucket's token capacity; items past
   // pre_tokens exit, pre_tokens = 0 = no cascade this step)
   const int* pre_dims;
+  // MODE 0, concurrent cascade: rows whose sequence starts past the prefix
+  // (kv_begin > 0) write their own normalised O and its LSE here instead of
+  // merging the prefix partial (which is computed at the same time on a side
+  // stream); attn_cascade_merge combines the two afterwards
+  float* own_lse;
 };
 
 // MODE 0: per (sequence, q-tile) work item, causal over keys
@@ -264,7 +269,7 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
     float lse = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
     float wa = 0.f, wb = 1.f;
     const bf16* pp = nullptr;
-    if (blockIdx.z == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
+    if (blockIdx.z == 0 && a.pre_o != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
       const float lse_a = a.pre_lse[row];
       const float mx = fmaxf(lse_a, lse);
       const float ea = exp2f(lse_a - mx), eb = lse == -INFINITY ? 0.f : exp2f(lse - mx);
@@ -291,7 +296,9 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   }
   float wa = 0.f, wb = 1.f;
   const bf16* po = nullptr;
-  if (MODE == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
+  if (MODE == 0 && a.own_lse != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
+    if (fq == 0) a.own_lse[row] = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
+  } else if (MODE == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
     // merge with the shared-prefix partial: weights from the two log2-sum-exps
     const float lse_b = m_run + __log2f(l_tot);
     const float lse_a = a.pre_lse[row];
@@ -379,6 +386,8 @@ __global__ __launch_bounds__(256) void attn_split_combine(const AttnArgs a, int 
     dt += sc[w] * red_d[w][lane];
   }
   const float inv = dt > 0.f ? 1.f / dt : 0.f;
+  if (a.own_lse != nullptr && dq == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0)
+    a.own_lse[row] = dt > 0.f ? mtu + __log2f(dt) : -INFINITY;
   bf16* op = a.out + row * D + 32 * dq;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -425,6 +434,31 @@ __global__ __launch_bounds__(256) void attn_prefix_combine(const AttnArgs a, int
   for (int r = 0; r < 8; ++r) o[r] = (bf16)(acc[r] * inv);
   *reinterpret_cast<bf16x8*>(a.out + row * D + d0) = o;
   if (d0 == 0) a.lse_out[row] = den > 0.f ? mu + __log2f(den) : -INFINITY;
+}
+
+// Concurrent cascade: out[row] (the sequence's own-key partial, normalised,
+// LSE own_lse) merged with the shared-prefix partial (pre_o, pre_lse) for the
+// rows [0, pre_tokens) x Hq; one thread per (row, 8 dims).
+__global__ __launch_bounds__(256) void attn_cascade_merge(const AttnArgs a) {
+  const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long row = i / (D / 8);
+  const int d0 = (int)(i % (D / 8)) * 8;
+  if (row >= (long long)pre_tokens * a.Hq) return;
+  const float la = a.pre_lse[row], lb = a.own_lse[row];
+  const float mx = fmaxf(la, lb);
+  const float mu = mx == -INFINITY ? 0.f : mx;
+  float wa = la == -INFINITY ? 0.f : exp2f(la - mu), wb = lb == -INFINITY ? 0.f : exp2f(lb - mu);
+  const float den = wa + wb;
+  wa = den > 0.f ? wa / den : 0.f;
+  wb = den > 0.f ? wb / den : 0.f;
+  const bf16x8 pa = *reinterpret_cast<const bf16x8*>(a.pre_o + row * D + d0);
+  bf16x8* op = reinterpret_cast<bf16x8*>(a.out + row * D + d0);
+  const bf16x8 pb = *op;
+  bf16x8 o;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)pa[r] * wa + (float)pb[r] * wb);
+  *op = o;
 }
 
 template <int G>
@@ -512,7 +546,7 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
                            float scale, const int* kv_begin, const void* pre_o,
                            const float* pre_lse, hipStream_t s, int nsplit, float* split_o,
-                           float* split_lse, int rows) {
+                           float* split_lse, int rows, float* own_lse) {
   if (head_dim != D) return 1;
   if (nw != 1 && nw != 4) return 2;
   if (nwork <= 0) return 0;
@@ -538,6 +572,7 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
   a.split_o = split_o;
   a.split_lse = split_lse;
   a.rows = rows;
+  a.own_lse = own_lse;
   ATTN_SWITCH_G(Hq / Hkv, attn_dispatch<GG>(nw, a, nwork, s, nsplit))
   return 0;
 }
@@ -569,5 +604,23 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
   a.split_lse = split_lse;
   a.rows = pre_tokens * Hq;
   ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s, nsplit))
+  return 0;
+}
+
+// concurrent cascade: merge the own-key partial in out with the prefix partial
+int launch_cascade_merge(void* out, const float* own_lse, const void* pre_o, const float* pre_lse,
+                         int pre_tokens, const int* pre_dims, int Hq, int head_dim, hipStream_t s) {
+  if (head_dim != D) return 1;
+  if (pre_tokens <= 0) return 0;
+  AttnArgs a{};
+  a.out = (bf16*)out;
+  a.own_lse = (float*)own_lse;
+  a.pre_o = (const bf16*)pre_o;
+  a.pre_lse = pre_lse;
+  a.pre_tokens = pre_tokens;
+  a.pre_dims = pre_dims;
+  a.Hq = Hq;
+  const long long n = (long long)pre_tokens * Hq * (D / 8);
+  attn_cascade_merge<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
   return 0;
 }

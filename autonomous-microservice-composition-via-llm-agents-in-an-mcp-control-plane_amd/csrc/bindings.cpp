@@ -233,7 +233,8 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
                      const c10::optional<at::Tensor>& pre_o,
                      const c10::optional<at::Tensor>& pre_lse, int64_t nsplit,
                      const c10::optional<at::Tensor>& split_o,
-                     const c10::optional<at::Tensor>& split_lse) {
+                     const c10::optional<at::Tensor>& split_lse,
+                     const c10::optional<at::Tensor>& own_lse) {
   CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
   CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
   CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq); CHECK_I32_TENSOR(work_q0);
@@ -255,16 +256,24 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   const int* kb = nullptr;
   const void* po = nullptr;
   const float* pl = nullptr;
+  float* ol = nullptr;
   if (kv_begin.has_value()) {
     CHECK_I32_TENSOR((*kv_begin));
     TORCH_CHECK(kv_begin->numel() == q_len.numel(), "kv_begin [S]");
-    TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "kv_begin needs pre_o / pre_lse");
-    CHECK_BF16_TENSOR((*pre_o));
-    TORCH_CHECK(pre_o->sizes() == q.sizes(), "pre_o shape");
-    TORCH_CHECK(pre_lse->scalar_type() == at::kFloat && pre_lse->numel() == q.size(0) * Hq, "pre_lse [T, Hq]");
     kb = kv_begin->data_ptr<int>();
-    po = pre_o->data_ptr();
-    pl = pre_lse->data_ptr<float>();
+    if (own_lse.has_value()) {
+      // concurrent cascade: own-key partial + its LSE, merged later (cascade_merge)
+      TORCH_CHECK(own_lse->scalar_type() == at::kFloat && own_lse->is_contiguous() &&
+                      own_lse->numel() == q.size(0) * Hq, "own_lse [T, Hq] f32");
+      ol = own_lse->data_ptr<float>();
+    } else {
+      TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "kv_begin needs pre_o / pre_lse or own_lse");
+      CHECK_BF16_TENSOR((*pre_o));
+      TORCH_CHECK(pre_o->sizes() == q.sizes(), "pre_o shape");
+      TORCH_CHECK(pre_lse->scalar_type() == at::kFloat && pre_lse->numel() == q.size(0) * Hq, "pre_lse [T, Hq]");
+      po = pre_o->data_ptr();
+      pl = pre_lse->data_ptr<float>();
+    }
   }
   const int rc = launch_paged_attention(
       q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
@@ -272,9 +281,31 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
       block_table.size(1), work_seq.data_ptr<int>(), work_q0.data_ptr<int>(), work_seq.numel(), nw,
       Hq, Hkv, D, (float)scale, kb, po, pl, stream(), (int)nsplit,
       nsplit > 1 ? split_o->data_ptr<float>() : nullptr,
-      nsplit > 1 ? split_lse->data_ptr<float>() : nullptr, (int)(q.size(0) * Hq));
+      nsplit > 1 ? split_lse->data_ptr<float>() : nullptr, (int)(q.size(0) * Hq), ol);
   TORCH_CHECK(rc == 0, "paged_attention: unsupported config (code ", rc, ")");
   check_launch("paged_attention");
+}
+
+void cascade_merge(at::Tensor& out, const at::Tensor& own_lse, const at::Tensor& pre_o,
+                   const at::Tensor& pre_lse, int64_t pre_tokens,
+                   const c10::optional<at::Tensor>& pre_dims) {
+  CHECK_BF16_TENSOR(out); CHECK_BF16_TENSOR(pre_o);
+  TORCH_CHECK(out.dim() == 3 && pre_o.sizes() == out.sizes(), "out / pre_o [T, Hq, D]");
+  const int Hq = out.size(1), D = out.size(2);
+  TORCH_CHECK(own_lse.scalar_type() == at::kFloat && pre_lse.scalar_type() == at::kFloat &&
+                  own_lse.numel() == out.size(0) * Hq && pre_lse.numel() == out.size(0) * Hq,
+              "own_lse / pre_lse [T, Hq] f32");
+  TORCH_CHECK(pre_tokens <= out.size(0), "pre_tokens");
+  const int* dims = nullptr;
+  if (pre_dims.has_value()) {
+    CHECK_I32_TENSOR((*pre_dims));
+    dims = pre_dims->data_ptr<int>();
+  }
+  const int rc = launch_cascade_merge(out.data_ptr(), own_lse.data_ptr<float>(), pre_o.data_ptr(),
+                                      pre_lse.data_ptr<float>(), (int)pre_tokens, dims, Hq, D,
+                                      stream());
+  TORCH_CHECK(rc == 0, "cascade_merge: unsupported config (code ", rc, ")");
+  check_launch("cascade_merge");
 }
 
 void prefix_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
@@ -485,7 +516,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("block_table"), py::arg("work_seq"), py::arg("work_q0"), py::arg("nw"),
         py::arg("scale"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
         py::arg("pre_lse") = py::none(), py::arg("nsplit") = 1, py::arg("split_o") = py::none(),
-        py::arg("split_lse") = py::none());
+        py::arg("split_lse") = py::none(), py::arg("own_lse") = py::none());
+  m.def("cascade_merge", &cascade_merge, py::arg("out"), py::arg("own_lse"), py::arg("pre_o"),
+        py::arg("pre_lse"), py::arg("pre_tokens"), py::arg("pre_dims") = py::none());
   m.def("prefix_attention", &prefix_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("out"), py::arg("lse"), py::arg("pre_bt"), py::arg("pre_keys"),
         py::arg("pre_tokens"), py::arg("scale"), py::arg("pre_dims") = py::none(),

@@ -99,7 +99,10 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            const int* work_q0, int nwork, int nw, int Hq, int Hkv, int head_dim,
                            float scale, const int* kv_begin, const void* pre_o,
                            const float* pre_lse, hipStream_t s, int nsplit = 1,
-                           float* split_o = nullptr, float* split_lse = nullptr, int rows = 0);
+                           float* split_o = nullptr, float* split_lse = nullptr, int rows = 0,
+                           float* own_lse = nullptr);
+int launch_cascade_merge(void* out, const float* own_lse, const void* pre_o, const float* pre_lse,
+                         int pre_tokens, const int* pre_dims, int Hq, int head_dim, hipStream_t s);
 int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,
                             float* lse_out, const int* pre_bt, int pre_keys, int pre_tokens,
                             int Hq, int Hkv, int head_dim, float scale, hipStream_t s,

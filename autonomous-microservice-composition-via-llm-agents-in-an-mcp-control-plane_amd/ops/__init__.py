@@ -193,6 +193,19 @@ def rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D):
     return q_out
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    """One persistent side stream per device (concurrent cascade attention)."""
+    key = torch.device(device).index
+    st = _SIDE.get(key)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _SIDE[key] = st
+    return st
+
+
 def prefix_splits(pre_tokens: int, pre_keys: int, hkv: int, num_cus: int = 256) -> int:
     """Key-split factor of the cascade prefix pass (csrc/attention.hip): a
     step with few query tokens launches ceil(tokens / 32) x Hkv workgroups that
@@ -221,6 +234,14 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
         L = lib()
         kw = {}
         pre_dims = getattr(meta, "pre_dims", None)
+        concurrent = meta.pre_tokens > 0 and os.environ.get("MCP_ATTN_CONCURRENT", "1") == "1"
+        main = torch.cuda.current_stream(q.device)
+        if concurrent:
+            # the prefix pass and the own-key pass are independent: run the
+            # prefix pass on a side stream (fork / join events, hipGraph-safe),
+            # then merge the two partials (attn_cascade_merge)
+            side = _side_stream(q.device)
+            side.wait_stream(main)
         if meta.pre_tokens > 0:
             # cascade: all requests' query tokens vs the shared prefix K/V in full
             # MFMA tiles, then each request's own keys + LSE merge (csrc/attention.hip);
@@ -235,9 +256,17 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
                                                    device=q.device, dtype=torch.float32),
                             "split_lse": torch.empty(ps * meta.pre_tokens * q.shape[1],
                                                      device=q.device, dtype=torch.float32)}
-            L.prefix_attention(q, k_cache, v_cache, pre_o, pre_lse, meta.pre_bt, meta.pre_keys,
-                               meta.pre_tokens, scale, pre_dims=pre_dims, **kw_split)
-            kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
+            if concurrent:
+                with torch.cuda.stream(side):
+                    L.prefix_attention(q, k_cache, v_cache, pre_o, pre_lse, meta.pre_bt,
+                                       meta.pre_keys, meta.pre_tokens, scale, pre_dims=pre_dims,
+                                       **kw_split)
+                own_lse = torch.empty(q.shape[0], q.shape[1], device=q.device, dtype=torch.float32)
+                kw = {"kv_begin": meta.kv_begin, "own_lse": own_lse}
+            else:
+                L.prefix_attention(q, k_cache, v_cache, pre_o, pre_lse, meta.pre_bt, meta.pre_keys,
+                                   meta.pre_tokens, scale, pre_dims=pre_dims, **kw_split)
+                kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         ns = int(getattr(meta, "kv_splits", 1))
         for nw, ws, wq in meta.work_lists():
             if ns > 1:
@@ -250,6 +279,9 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
                 continue
             L.paged_attention(q, k_cache, v_cache, out, meta.q_start, meta.q_len, meta.ctx_len,
                               meta.block_table, ws, wq, nw, scale, **kw)
+        if concurrent:
+            main.wait_stream(side)
+            L.cascade_merge(out, kw["own_lse"], pre_o, pre_lse, meta.pre_tokens, pre_dims=pre_dims)
         return out
     r = ref.paged_attention(q, k_cache, v_cache, meta.q_start, meta.q_len, meta.ctx_len,
                             meta.block_table, scale)

@@ -267,11 +267,15 @@ def test_topk_cosine(B, N, D, k, fused):
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
 @pytest.mark.parametrize("kv_splits", [1, 4])
 @pytest.mark.parametrize("prefix_split", ["0", "-1", "3"])
-def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, monkeypatch):
+@pytest.mark.parametrize("concurrent", ["0", "1"])
+def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, concurrent, monkeypatch):
     """Shared-prefix pass + per-sequence pass with LSE merge == full attention
-    (also with split-KV: split 0 folds the prefix partial in; and with the
-    prefix pass itself split over its key tiles + merged: off / auto / 3)."""
+    (also with split-KV: split 0 folds the prefix partial in; with the prefix
+    pass itself split over its key tiles + merged: off / auto / 3; and with
+    the prefix pass on a side stream concurrent with the own-key pass, the
+    two partials merged afterwards)."""
     monkeypatch.setenv("MCP_PREFIX_SPLIT", prefix_split)
+    monkeypatch.setenv("MCP_ATTN_CONCURRENT", concurrent)
     torch.manual_seed(5)
     D, BS = 128, 64
     P_full = 640                                   # 10 shared blocks
