@@ -234,7 +234,7 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
         L = lib()
         kw = {}
         pre_dims = getattr(meta, "pre_dims", None)
-        concurrent = meta.pre_tokens > 0 and os.environ.get("MCP_ATTN_CONCURRENT", "1") == "1"
+        concurrent = meta.pre_tokens > 0 and os.environ.get("MCP_ATTN_CONCURRENT", "0") == "1"
         main = torch.cuda.current_stream(q.device)
         if concurrent:
             # the prefix pass and the own-key pass are independent: run the
