@@ -211,17 +211,22 @@ def prefix_splits(pre_tokens: int, pre_keys: int, hkv: int, num_cus: int = 256) 
     step with few query tokens launches ceil(tokens / 32) x Hkv workgroups that
     each walk every prefix tile; split the tiles so the grid reaches ~2
     workgroups per CU, >= 2 tiles per split.  ``pre_tokens`` / ``pre_keys``
-    are the grid capacities under a hipGraph.  ``MCP_PREFIX_SPLIT``: 0 off
-    (default: measured no faster at 40-120 intents/s, config 5 p50 173.5 /
-    234 / 379 ms split vs 176 / 228 / 357 unsplit,
-    profiles/attention_tuning.md), -1 auto, N forces N."""
-    forced = int(os.environ.get("MCP_PREFIX_SPLIT", "0"))
+    are the grid capacities under a hipGraph.  Only for small grids (<= a
+    quarter of the CUs): the unsplit pass walks the ~11 prefix tiles with one
+    tile of DMA lookahead, ~25 us even for 16 query tokens; split, 4-16
+    requests take 25-37 us instead of 34-45 for the whole attention, while at
+    256 requests the merge costs more than it saves
+    (tools/bench_attention.py, profiles/attention_tuning.md).
+    ``MCP_PREFIX_SPLIT``: -1 auto (default), 0 off, N forces N."""
+    forced = int(os.environ.get("MCP_PREFIX_SPLIT", "-1"))
     if forced == 0:
         return 1
     tiles = pre_keys // 64
     grid = -(-pre_tokens // 32) * hkv
     if forced > 1:
         return max(1, min(forced, tiles))
+    if grid > num_cus // 4:
+        return 1
     ns = min(-(-2 * num_cus // max(grid, 1)), tiles // 2, 8)
     return ns if ns >= 2 else 1
 

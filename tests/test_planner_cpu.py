@@ -363,3 +363,19 @@ def test_kv_split_rule():
         assert choose_kv_splits([1], [32768], 4, 8) == 1
     finally:
         del os.environ["MCP_KV_SPLIT"]
+
+
+def test_prefix_split_rule(monkeypatch):
+    """Cascade prefix key split: only small grids (<= a quarter of the CUs)
+    split; 0 disables; N forces N (bounded by the tile count)."""
+    from mcp_amd import ops
+    monkeypatch.delenv("MCP_PREFIX_SPLIT", raising=False)
+    assert ops.prefix_splits(16, 704, 8) == 5          # 8 workgroups, 11 tiles
+    assert ops.prefix_splits(192, 704, 8) == 5         # 48 workgroups
+    assert ops.prefix_splits(256, 704, 8) == 5         # 64 = 256 / 4
+    assert ops.prefix_splits(288, 704, 8) == 1         # 72 > 64: no split
+    assert ops.prefix_splits(16, 128, 8) == 1          # 2 tiles: nothing to split
+    monkeypatch.setenv("MCP_PREFIX_SPLIT", "0")
+    assert ops.prefix_splits(16, 704, 8) == 1
+    monkeypatch.setenv("MCP_PREFIX_SPLIT", "3")
+    assert ops.prefix_splits(4096, 704, 8) == 3

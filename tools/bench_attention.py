@@ -19,10 +19,11 @@ Hq, Hkv, D = 32, 8, 128
 # argv[1]: new tokens per request (16: 4-wave items; <= 8: 1-wave decode items)
 # "a:b" alternates requests of a and b new tokens (mixed decode / jump-forward steps)
 qls = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "16").split(":")]
-S, prefix = 256, 704
+import os
+S, prefix = int(os.environ.get("ATTN_S", "256")), 704      # ATTN_S: requests in the step
 ql_s = np.array([qls[s % len(qls)] for s in range(S)], np.int32)
 ql = int(ql_s.max())
-own = 200
+own = int(os.environ.get("ATTN_OWN", "200"))
 nb_pre = prefix // 64
 rng = np.random.default_rng(0)
 blocks_per_seq = (prefix + own + ql + 63) // 64
@@ -91,6 +92,6 @@ for nw, ws, wq in d.attn.work_lists():
 t_prefix()
 t_own()
 err = ((out.float() - ref.float()).norm() / ref.norm()).item()
-print(json.dumps({"ql": sys.argv[1] if len(sys.argv) > 1 else "16", "full_us": round(tf, 1), "prefix_us": round(tp, 1), "prefix_tflops": round(fl_pre / tp / 1e6, 1),
+print(json.dumps({"S": S, "own": own, "ql": sys.argv[1] if len(sys.argv) > 1 else "16", "full_us": round(tf, 1), "prefix_us": round(tp, 1), "prefix_tflops": round(fl_pre / tp / 1e6, 1),
                   "own_us": round(to, 1), "own_tflops": round(fl_own / to / 1e6, 1),
                   "cascade_vs_plain_rel_err": err}))
