@@ -79,6 +79,10 @@ struct AttnArgs {
   // merging the prefix partial (which is computed at the same time on a side
   // stream); attn_cascade_merge combines the two afterwards
   float* own_lse;
+  // MODE 1: grid (Hkv, token blocks) instead of (token blocks, Hkv), so that
+  // block id % 8 (the XCD) is the kv head when Hkv = 8: each XCD's L2 then
+  // holds one head's prefix K/V (352 KiB) instead of all eight
+  int head_major;
 };
 
 // MODE 0: per (sequence, q-tile) work item, causal over keys
@@ -99,7 +103,9 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * 2 * TILE];   // [buf][K|V][64][128]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kvh = blockIdx.y;
+  const bool hm = MODE == 1 && a.head_major;
+  const int kvh = hm ? blockIdx.x : blockIdx.y;
+  const int qblk = hm ? blockIdx.y : blockIdx.x;
   const int fr = lane & 15, fq = lane >> 4;
   const int head = kvh * G + fr % G;
   const int Hq = a.Hq, Hkv = a.Hkv;
@@ -110,8 +116,8 @@ __global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
   if (MODE == 1) {
     const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
     const int pre_keys = a.pre_dims ? a.pre_dims[1] : a.pre_keys;
-    if ((int)blockIdx.x * QT >= pre_tokens) return;      // whole block idle (before any barrier)
-    tok = blockIdx.x * QT + wave * TPW + fr / G;          // flat token index
+    if (qblk * QT >= pre_tokens) return;                 // whole block idle (before any barrier)
+    tok = qblk * QT + wave * TPW + fr / G;                // flat token index
     qvalid = tok < pre_tokens;
     qs = 0;
     ql = pre_tokens;
@@ -509,7 +515,8 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
     // key-split prefix pass (few query tokens: the unsplit grid is a few
     // dozen workgroups each walking every prefix tile), then the merge
     constexpr int QT = 8 * (16 / G);
-    const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv, nsplit);
+    const int nblk = (a.pre_tokens + QT - 1) / QT;
+    const dim3 grid = a.head_major ? dim3(a.Hkv, nblk, nsplit) : dim3(nblk, a.Hkv, nsplit);
     attn_kernel<8, G, 1, 0, true><<<grid, 512, 0, s>>>(a);
     const long long n = (long long)a.pre_tokens * a.Hq * (D / 8);
     attn_prefix_combine<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, nsplit);
@@ -517,11 +524,13 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
   }
   if (prefix_nw() == 4) {
     constexpr int QT = 4 * (16 / G);
-    const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
+    const int nblk = (a.pre_tokens + QT - 1) / QT;
+    const dim3 grid = a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
     attn_kernel<4, G, 1><<<grid, 256, 0, s>>>(a);
   } else {
     constexpr int QT = 8 * (16 / G);
-    const dim3 grid((a.pre_tokens + QT - 1) / QT, a.Hkv);
+    const int nblk = (a.pre_tokens + QT - 1) / QT;
+    const dim3 grid = a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
     attn_kernel<8, G, 1><<<grid, 512, 0, s>>>(a);
   }
 }
@@ -603,6 +612,9 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
   a.split_o = split_o;
   a.split_lse = split_lse;
   a.rows = pre_tokens * Hq;
+  // MCP_ATTN_PREFIX_HEAD_MAJOR=0: token-major grid (A/B)
+  static const int head_major = getenv("MCP_ATTN_PREFIX_HEAD_MAJOR") ? atoi(getenv("MCP_ATTN_PREFIX_HEAD_MAJOR")) : 1;
+  a.head_major = head_major;
   ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s, nsplit))
   return 0;
 }

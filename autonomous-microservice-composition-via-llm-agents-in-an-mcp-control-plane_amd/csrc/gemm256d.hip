@@ -431,6 +431,14 @@ static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R
   if (const int rc = gemm256d_ok(M, N, K)) return rc;
   if (bm == 0) bm = gemm256d_height(M, N, K);
   const int nm = (M + bm - 1) / bm, nn = (N + BN - 1) / BN;
+  // at most half the CUs' worth of 256-row tiles: the whole product runs
+  // stream-K (every tile over >= 2 workgroups, last arriver sums the slabs)
+  // instead of leaving half the chip idle (MCP_GEMM_SK_SMALL=0 disables)
+  static const int sk_small = getenv("MCP_GEMM_SK_SMALL") ? atoi(getenv("MCP_GEMM_SK_SMALL")) : 1;
+  if (sk_small && bm == 256 && epi >= 0 && epi <= 2) {
+    if (!g_cus) gemm256d_waves_bm(M, N, K, 256);
+    if (2 * nm * nn <= g_cus) return launch_gemm_tn_256sk_tail(X, W, Y, R, M, N, K, epi, 0, s);
+  }
   const int tile0 = hybrid_tile0(M, N, bm, epi);
   const dim3 grid(tile0 > 0 ? tile0 : nm * nn);
   if (tile0 > 0) {

@@ -315,6 +315,8 @@ def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, concurrent, 
     assert rel_err(out, exp) < 2e-2
 
 
+
+
 @pytest.mark.parametrize("M,F,K", [(7, 512, 256), (300, 1792, 4096), (3000, 14336, 4096), (520, 3584, 1024)])
 def test_gemm_silu_fused(M, F, K):
     torch.manual_seed(3)
