@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import zlib
 import os
 import statistics
 import sys
@@ -117,7 +118,7 @@ def main():
     def handler(request: httpx.Request):
         host = request.url.host
         attempts[host] = attempts.get(host, 0) + 1
-        h = hash(host) % 7
+        h = zlib.crc32(host.encode()) % 7                    # stable across runs (str hash is salted)
         if h == 0 and not host.endswith("fallback"):          # dead primary
             return httpx.Response(503)
         if h == 1 and attempts[host] % 2 == 1:                # flaky: fails every other call
