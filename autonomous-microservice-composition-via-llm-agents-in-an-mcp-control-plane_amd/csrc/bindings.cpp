@@ -177,6 +177,13 @@ void gemm_plan_set_splits_py(int64_t N, int64_t K, const std::vector<int64_t>& s
   gemm_plan_set_splits((int)N, (int)K, c.data(), (int)c.size());
 }
 
+void gemm_plan_set_flex_py(int64_t N, int64_t K, const std::vector<int64_t>& flex) {
+  std::vector<int> c(flex.begin(), flex.end());
+  for (int v : c)
+    TORCH_CHECK(v == -1 || (v & 31) < gemm_flex_count(), "gemm plan flex must be -1 or a candidate");
+  gemm_plan_set_flex((int)N, (int)K, c.data(), (int)c.size());
+}
+
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
   TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
@@ -495,7 +502,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_set_splits", &gemm_plan_set_splits_py,
         "measured split-K of the 128^2 path for one (N, K): a count per 64-row M bucket (0 = rule)");
   m.def("gemm_plan_split", &gemm_plan_split);
+  m.def("gemm_plan_set_flex", &gemm_plan_set_flex_py,
+        "measured flex tile per 64-row M bucket for one (N, K) (-1 = none; +32 = 4-stage form)");
+  m.def("gemm_plan_flex", &gemm_plan_flex);
   m.def("gemm_plan_clear", &gemm_plan_clear);
+  m.def("gemm_flex_count", &gemm_flex_count, "flex tile candidates (gemm(..., algo=16 + i))");
+  m.def("gemm_flex_tiles", &gemm_flex_tiles, py::arg("cand"), py::arg("M"), py::arg("N"));
   m.def("gemm_plan_lookup", &gemm_plan_lookup);
   m.def("gemm_splitk_init", [](int64_t bytes) { return gemm_splitk_init((size_t)bytes); },
         "allocate the split-K fp32 workspace (call outside graph capture)");

@@ -224,6 +224,7 @@ struct GemmPlan {
   int N, K;
   std::vector<signed char> code;
   std::vector<signed char> split;    // measured split-K of the 128^2 path (0: the rule)
+  std::vector<signed char> flex;     // measured flex tile (gemm_flex.hip) or -1
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -235,7 +236,7 @@ void gemm_plan_set(int N, int K, const int* codes, int n) {
       p.code = std::move(c);
       return;
     }
-  g_plans.push_back({N, K, std::move(c), {}});
+  g_plans.push_back({N, K, std::move(c), {}, {}});
 }
 
 void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
@@ -244,7 +245,28 @@ void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
       p.split.assign(splits, splits + n);
       return;
     }
-  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n)});
+  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n), {}});
+}
+
+void gemm_plan_set_flex(int N, int K, const int* flex, int n) {
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.flex.assign(flex, flex + n);
+      return;
+    }
+  g_plans.push_back({N, K, {}, {}, std::vector<signed char>(flex, flex + n)});
+}
+
+// measured flex tile candidate for this M bucket (-1 = none: the code path)
+int gemm_plan_flex(int M, int N, int K) {
+  static const int on = getenv("MCP_GEMM_FLEX") ? atoi(getenv("MCP_GEMM_FLEX")) : 1;
+  if (!on) return -1;
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.flex.size() ? p.flex[b] : -1;
+    }
+  return -1;
 }
 
 // measured split count for the 128^2 path at this M bucket (0 = none recorded)
@@ -457,6 +479,10 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
   if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
       launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0)
     return;
+  // serving-size M: a tile shape that fills one wave of workgroups, measured
+  // faster than the 128^2 split-K / AGPR paths for this bucket (plan "flex")
+  const int fx = gemm_plan_flex(M, N, K);
+  if (fx >= 0 && launch_gemm_flex(X, W, Y, R, M, N, K, fx, s) == 0) return;
   if (gemm_select(M, N, K) == 1)
     launch_gemm_tn_256(X, W, Y, R, M, N, K, s);
   else
@@ -465,6 +491,7 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
 
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                          int algo, hipStream_t s) {
+  if (algo >= 16 && launch_gemm_flex(X, W, Y, R, M, N, K, algo - 16, s) == 0) return;   // tuning
   if (algo < 0) launch_gemm_tn(X, W, Y, R, M, N, K, s);
   else if (algo == 3 && launch_gemm_stream(X, W, Y, R, M, N, K, R ? 1 : 0, RopeArgs{}, s) == 0) return;
   else if (algo == 2 && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;

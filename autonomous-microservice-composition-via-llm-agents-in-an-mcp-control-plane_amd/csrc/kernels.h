@@ -18,6 +18,13 @@ void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const voi
 void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
 
 // QKV projection + RoPE + paged K/V write fused in the GEMM epilogue (K1+K4+K10)
+// serving-size M: tile shape per (M, N) filling one wave of workgroups (gemm_flex.hip)
+int launch_gemm_flex(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                     int cand, hipStream_t s);
+int gemm_flex_count();
+void gemm_plan_set_flex(int N, int K, const int* flex, int n);
+int gemm_plan_flex(int M, int N, int K);
+int gemm_flex_tiles(int cand, int M, int N);
 struct RopeArgs {
   const int* pos;          // [T] positions
   const int* slots;        // [T] KV-cache slots (-1: no write)

@@ -67,6 +67,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
         mod.gemm_plan_set(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["codes"]])
         if "splits" in sh and hasattr(mod, "gemm_plan_set_splits"):
             mod.gemm_plan_set_splits(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["splits"]])
+        if "flex" in sh and hasattr(mod, "gemm_plan_set_flex"):
+            mod.gemm_plan_set_flex(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["flex"]])
     return len(plan["shapes"])
 
 

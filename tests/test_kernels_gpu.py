@@ -65,6 +65,42 @@ def test_gemm(M, N, K):
     assert rel_err(Y2, ref.gemm(X, W, R)) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 384, 256), (77, 1028, 512), (300, 6144, 4096), (1000, 4096, 1024),
+                                   (513, 640, 14336)])
+def test_gemm_flex_tiles(M, N, K):
+    """Every flex tile (gemm_flex.hip), 2- and 4-stage forms, plain and
+    + residual, against fp32 - ragged M / N edges included."""
+    torch.manual_seed(11)
+    L = ops.lib()
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    exp = ref.gemm(X, W)
+    exp_r = ref.gemm(X, W, R)
+    for c in list(range(L.gemm_flex_count())) + [32 + c for c in range(L.gemm_flex_count())]:
+        Y = torch.full((M, N), float("nan"), device=DEV).bfloat16()
+        L.gemm(X, W, Y, None, 16 + c)
+        assert rel_err(Y, exp) < 1e-2, c
+        L.gemm(X, W, Y, R, 16 + c)
+        assert rel_err(Y, exp_r) < 1e-2, c
+
+
+def test_gemm_plan_flex_dispatch():
+    """A plan that names a flex tile for a bucket routes ops.gemm there."""
+    L = ops.lib()
+    M, N, K = 320, 640, 512
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    try:
+        L.gemm_plan_set(N, K, [0] * 8)
+        L.gemm_plan_set_flex(N, K, [-1] * 4 + [32 + 4] * 4)
+        assert L.gemm_plan_flex(M, N, K) == 36 and L.gemm_plan_flex(200, N, K) == -1
+        assert rel_err(ops.gemm(X, W), ref.gemm(X, W)) < 1e-2
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)
+
+
 def test_gemm_orientation_exact():
     # A = I, asymmetric B: catches a transposed C-write (cdna_hip_programming.md §3)
     K = 128

@@ -10,7 +10,12 @@ fastest wins unless it beats the runner-up with the smaller code by < 1 %
 split-K 1 / 2 / 4 / 8 (2 / 4 / 8 below 129 rows, where "no split" means the
 skinny kernel) and its best split is recorded per bucket ("splits"; the
 serving steps' M = 64-768 range, where the split rule alone was up to 20 %
-off, profiles/gemm_tuning.md).
+off, profiles/gemm_tuning.md).  For M = 128-2048 on the non-SwiGLU shapes
+every flex tile (gemm_flex.hip, 2- and 4-stage forms) is timed too and the
+fastest is recorded per bucket ("flex", -1 = none) when it beats the code
+path by > 1 %.  Buckets up to 2048 rows are timed with COLD weights (each
+launch reads the next of several weight copies, > 1.5 GB: a serving step
+streams the whole model, nothing stays in the 256 MB Infinity Cache).
 
     python tools/tune_gemm_plan.py [out.json] [m_max]
 """
@@ -34,13 +39,17 @@ SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
+FLEX_MIN, FLEX_MAX = 128, 2048             # flex tiles measured here (cold weights up to FLEX_MAX)
+NFLEX = L.gemm_flex_count()
 
 dev = "cuda"
 s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
 def run(code, X, W, Y, split=-1):
-    if code == 0:
+    if code == 3:                          # flex tile, split = candidate
+        L.gemm(X, W, Y, None, 16 + split)
+    elif code == 0:
         L.gemm_splitk_force(split)
         L.gemm(X, W, Y, None, 0)
         L.gemm_splitk_force(-1)
@@ -48,11 +57,11 @@ def run(code, X, W, Y, split=-1):
         L.gemm_variant(X, W, Y, 49 if code == 1 else 51)
 
 
-def time_ms(fn, reps=10):
-    fn()
+def time_ms(fn, Ws, reps=10):
+    fn(Ws[0])
     s_ev.record()
-    for _ in range(reps):
-        fn()
+    for i in range(reps):
+        fn(Ws[i % len(Ws)])
     e_ev.record()
     torch.cuda.synchronize()
     return s_ev.elapsed_time(e_ev) / reps
@@ -61,27 +70,37 @@ def time_ms(fn, reps=10):
 result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
           "mstep": MSTEP, "codes": "0=128x128, 1=AGPR 256-row tiles, 2=AGPR 192-row tiles",
           "splits": "measured split-K of code 0 per bucket (0 = the rule)",
+          "flex": "measured flex tile per bucket (gemm_flex.hip candidate, +32 = 4-stage; -1 = none)",
           "generated": time.strftime("%Y-%m-%d"), "shapes": []}
 t0 = time.time()
 for (N, K) in SHAPES:
     Xf = torch.randn(m_max, K, device=dev).bfloat16()
     W = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+    Wcold = [W] + [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+                   for _ in range(int(1.5e9 // (N * K * 2)))]
     Yf = torch.empty(m_max, N, device=dev, dtype=torch.bfloat16)
-    codes, tf, splits = [], [], []
+    codes, tf, splits, flex = [], [], [], []
     for b in range(m_max // MSTEP):
         M = (b + 1) * MSTEP
         X, Y = Xf[:M], Yf[:M]
+        Ws = Wcold if M <= FLEX_MAX else [W]
         # code-0 candidates: (0, split)
         svals = ([2, 4, 8] if M <= 128 else [1, 2, 4, 8]) if M <= M_SPLIT_MAX else [-1]
         cands = [(0, sv) for sv in svals]
         if M >= M_MIN and K % 128 == 0 and N % 256 == 0:
             cands += [(1, -1), (2, -1)]
-        best = {c: float("inf") for c in cands}
+        fl = []
+        if FLEX_MIN <= M <= FLEX_MAX and N != 28672:          # gate|up runs the SwiGLU epilogue
+            fl = [(3, f) for f in list(range(NFLEX)) + [32 + f for f in range(NFLEX)]]
+        best = {c: float("inf") for c in cands + fl}
         for _ in range(3):
-            for c in cands:
-                best[c] = min(best[c], time_ms(lambda c=c: run(c[0], X, W, Y, c[1])))
+            for c in cands + fl:
+                best[c] = min(best[c], time_ms(lambda w, c=c: run(c[0], X, w, Y, c[1]), Ws))
         c0 = min((c for c in cands if c[0] == 0), key=lambda c: best[c])
         splits.append(max(c0[1], 0))
+        ref_ms = min(best[c] for c in cands)
+        fbest = min(fl, key=lambda c: best[c]) if fl else None
+        flex.append(fbest[1] if fbest and best[fbest] * 1.01 < ref_ms else -1)
         if M < M_MIN:
             codes.append(-1)
             tf.append({f"0s{c[1]}": round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
@@ -95,9 +114,11 @@ for (N, K) in SHAPES:
                 win = c
         codes.append(win)
         tf.append({str(c): round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
-    result["shapes"].append({"N": N, "K": K, "codes": codes, "splits": splits, "tflops": tf})
-    print(json.dumps({"N": N, "K": K, "codes": codes, "s": round(time.time() - t0, 1)}), flush=True)
-    del Xf, W, Yf
+    result["shapes"].append({"N": N, "K": K, "codes": codes, "splits": splits, "flex": flex,
+                             "tflops": tf})
+    print(json.dumps({"N": N, "K": K, "codes": codes, "flex": flex, "s": round(time.time() - t0, 1)}),
+          flush=True)
+    del Xf, W, Yf, Wcold
 with open(out_path, "w") as f:
     json.dump(result, f, indent=None, separators=(",", ":"))
     f.write("\n")
