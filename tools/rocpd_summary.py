@@ -13,6 +13,7 @@ from collections import defaultdict
 
 CATS = [("gemm (MFMA 256x256, AGPR 1 wave/SIMD)", r"gemm_tn_256d"),
         ("gemm (MFMA 256x256)", r"gemm_tn_256"), ("gemm (MFMA 128x128)", r"gemm_tn_128"),
+        ("gemm (flex tiles)", r"gemm_tn_flex"),
         ("gemm (skinny K2)", r"gemm_skinny"), ("gemm (K2 weight-streaming)", r"gemm_stream|stream_"),
         ("split-K reduce", r"splitk_reduce"), ("attention", r"attn_"),
         ("sampling", r"sample_"), ("rmsnorm", r"rmsnorm"), ("rope+kv write", r"rope"),
@@ -51,6 +52,26 @@ def main(db, last_ms=None):
     print("\n| kernel | calls | total ms | mean us | % |\n|---|---|---|---|---|")
     for name, n, tot, avg in rows[:25]:
         print(f"| `{short(name)}` | {n} | {tot / 1e6:.2f} | {avg / 1e3:.1f} | {100 * tot / total:.1f} |")
+    other = [r for r in rows if not any(re.search(p, r[0]) for _, p in CATS[:-1])]
+    if other:
+        print("\n| uncategorised kernel | calls | total ms | mean us |\n|---|---|---|---|")
+        for name, n, tot, avg in other[:12]:
+            print(f"| `{name[:110]}` | {n} | {tot / 1e6:.2f} | {avg / 1e3:.1f} |")
+    # idle time between kernels (union of kernel intervals on the device):
+    # host-side gaps (scheduling, grammar, H2D, first launch) show up as the
+    # long ones; launch-to-launch bubbles as the short ones
+    iv = sorted(c.execute("select start, end from kernels where start >= ?", (t0,)))
+    gaps, cur = [], None
+    for s, e in iv:
+        if cur is not None and s > cur:
+            gaps.append(s - cur)
+        cur = e if cur is None else max(cur, e)
+    edges = [(0, 10e3), (10e3, 100e3), (100e3, 1e6), (1e6, 1e12)]
+    labels = ["< 10 us", "10-100 us", "0.1-1 ms", "> 1 ms"]
+    print("\n| idle gap | count | total ms | % of window |\n|---|---|---|---|")
+    for (lo, hi), lab in zip(edges, labels):
+        g = [x for x in gaps if lo <= x < hi]
+        print(f"| {lab} | {len(g)} | {sum(g) / 1e6:.1f} | {100 * sum(g) / span:.1f} |")
 
 
 if __name__ == "__main__":
