@@ -29,6 +29,33 @@ def test_plan_file_shape():
         # buckets below 256 rows are left to the skinny / 128 kernels
         assert all(c == -1 for c in s["codes"][:3])
         assert all(c >= 0 for c in s["codes"][3:])
+        if "lib" in s:            # hipBLASLt buckets (tools/tune_gemm_lib.py): o, down, qkv only
+            assert (s["N"], s["K"]) in {(4096, 4096), (4096, 14336), (6144, 4096)}
+            assert len(s["lib"]) == len(s["codes"]) and set(s["lib"]) <= {0, 1}
+
+
+def test_lib_pick_follows_plan(tmp_path, monkeypatch):
+    """ops._lib_pick reads the plan's per-bucket "lib" flags; a reload replaces
+    them and MCP_GEMM_LIB=0 (module switch) turns them off."""
+    L = _lib()
+    p = tmp_path / "plan.json"
+    p.write_text(json.dumps({"arch": "gfx950", "mstep": 64, "shapes": [
+        {"N": 4096, "K": 4096, "codes": [-1, -1, -1, 1, 1], "lib": [0, 0, 0, 1, 0]}]}))
+    try:
+        ops._load_gemm_plan(L, str(p))
+        assert ops._lib_pick(256, 4096, 4096) and not ops._lib_pick(257, 4096, 4096)
+        assert not ops._lib_pick(192, 4096, 4096) and not ops._lib_pick(10_000, 4096, 4096)
+        assert not ops._lib_pick(256, 4096, 14336)                 # other shape
+        monkeypatch.setattr(ops, "_LIB_ON", False)
+        assert not ops._lib_pick(256, 4096, 4096)
+        monkeypatch.setattr(ops, "_LIB_ON", True)
+        p.write_text(json.dumps({"arch": "gfx950", "mstep": 64,
+                                 "shapes": [{"N": 4096, "K": 4096, "codes": [-1, -1, -1, 1]}]}))
+        ops._load_gemm_plan(L, str(p))
+        assert not ops._lib_pick(256, 4096, 4096)                  # flags do not leak across loads
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)
 
 
 def test_plan_lookup_buckets():

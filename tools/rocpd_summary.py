@@ -13,7 +13,7 @@ from collections import defaultdict
 
 CATS = [("gemm (MFMA 256x256, AGPR 1 wave/SIMD)", r"gemm_tn_256d"),
         ("gemm (MFMA 256x256)", r"gemm_tn_256"), ("gemm (MFMA 128x128)", r"gemm_tn_128"),
-        ("gemm (flex tiles)", r"gemm_tn_flex"),
+        ("gemm (flex tiles)", r"gemm_tn_flex"), ("gemm (hipBLASLt, plan 'lib' buckets)", r"Cijk_"),
         ("gemm (skinny K2)", r"gemm_skinny"), ("gemm (K2 weight-streaming)", r"gemm_stream|stream_"),
         ("split-K reduce", r"splitk_reduce"), ("attention", r"attn_"),
         ("sampling", r"sample_"), ("rmsnorm", r"rmsnorm"), ("rope+kv write", r"rope"),
