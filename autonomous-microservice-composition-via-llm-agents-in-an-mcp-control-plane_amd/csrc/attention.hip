@@ -91,8 +91,9 @@ struct AttnArgs {
 //         sequence that shares one registry prefix, 16-token tiles that mix
 //         sequences (they attend to the same K/V), no mask (every query sits
 //         after the prefix).  Writes normalised O and its LSE.
-template <int NW, int G, int MODE, int NBUF_ = 0, bool KSPLIT = false>
-__global__ __launch_bounds__(NW * 64) void attn_kernel(const AttnArgs a) {
+template <int NW, int G, int MODE, int NBUF_ = 0, bool KSPLIT = false, int WPE = 1>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void attn_kernel(const AttnArgs a) {
   constexpr int TPW = 16 / G;                 // tokens per wave
   constexpr int QT = NW * TPW;                // tokens per work item
   constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
@@ -489,10 +490,17 @@ void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s, int nspl
   }
   const dim3 grid(nwork, a.Hkv);
   static const int nw1_bufs = getenv("MCP_ATTN_NW1_BUFS") ? atoi(getenv("MCP_ATTN_NW1_BUFS")) : 1;
+  // 4-wave items single-buffered at <= 168 VGPRs (150 + 0 AGPRs, 3 waves per
+  // SIMD): 3 blocks per CU (96 KiB LDS) instead of 2 double-buffered ones
+  // (178 registers): per-request pass 3-6 % faster at 10-32 tokens per request,
+  // equal at 6-8 (profiles/attention_tuning.md); MCP_ATTN_NW4_FORM=0 = old form
+  static const int nw4_form = getenv("MCP_ATTN_NW4_FORM") ? atoi(getenv("MCP_ATTN_NW4_FORM")) : 1;
   if (nw == 1 && nw1_bufs == 2)
     attn_kernel<1, G, 0, 2><<<grid, 64, 0, s>>>(a);
   else if (nw == 1)
     attn_kernel<1, G, 0><<<grid, 64, 0, s>>>(a);
+  else if (nw4_form == 1)
+    attn_kernel<4, G, 0, 1, false, 3><<<grid, 256, 0, s>>>(a);
   else
     attn_kernel<4, G, 0><<<grid, 256, 0, s>>>(a);
 }
