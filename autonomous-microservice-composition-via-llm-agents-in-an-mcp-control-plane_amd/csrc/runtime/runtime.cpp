@@ -277,6 +277,8 @@ std::vector<std::vector<int>> topo_generations(int n, const std::vector<std::pai
 
 }  // namespace
 
+void register_grammar(py::module_& m);     // grammar.cpp
+
 PYBIND11_MODULE(MODULE_NAME, m) {
   m.doc() = "native CPU runtime of the MI355X planner engine";
   py::register_exception<OutOfBlocks>(m, "OutOfBlocks", PyExc_RuntimeError);
@@ -293,4 +295,5 @@ PYBIND11_MODULE(MODULE_NAME, m) {
         py::arg("copies") = py::none(), py::arg("pre_bt") = py::none(), py::arg("pre_tokens") = 0,
         py::arg("allowed") = py::none(), py::arg("ctr") = py::none());
   m.def("topo_generations", &topo_generations);
+  register_grammar(m);
 }

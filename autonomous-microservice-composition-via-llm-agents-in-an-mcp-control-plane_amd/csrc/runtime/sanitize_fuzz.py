@@ -145,4 +145,56 @@ for _ in range(ITERS):
     expect(IndexError, rt.topo_generations, max(n, 1), [(0, max(n, 1))])
     expect(IndexError, rt.topo_generations, max(n, 1), [(-1, 0)])
 
+# ---- native grammar decoder (grammar.cpp) in lock-step with planner/grammar.py,
+# char-level token ids (JSON-quoted alternatives stay prefix-free)
+import json  # noqa: E402
+import os  # noqa: E402
+
+gspec = importlib.util.spec_from_file_location(
+    "mcp_grammar_ref", os.path.join(os.path.dirname(sys.argv[1]), "..", "planner", "grammar.py"))
+grammar = importlib.util.module_from_spec(gspec)
+gspec.loader.exec_module(grammar)
+
+
+class CharTok:
+    @staticmethod
+    def encode(text):
+        return [ord(c) for c in text]
+
+
+for it in range(max(1, ITERS // 4)):
+    S = rng.randint(1, 12)
+    keys_pool = [f"k{i}" for i in range(6)] + ["svc0", "svc1"]
+    services = []
+    for i in range(S):
+        ks = rng.sample(keys_pool, rng.randint(0, 4))
+        services.append({"name": f"svc{i}", "endpoint": f"http://svc{i}/api",
+                         "input_schema": {"type": "object", "properties": {k: {"type": "string"} for k in ks}},
+                         "fallback": f"http://fb{i}/api" if rng.random() < 0.5 else None})
+    mx = rng.randint(1, 6)
+    spec = grammar.GrammarSpec(services, CharTok(), max_nodes=mx, min_nodes=rng.randint(1, mx),
+                               allow_retries=rng.random() < 0.7)
+    nspec = rt.grammar_spec(spec.native_payload())
+    for _ in range(4):
+        a, b = grammar.DagDecoder(spec), rt.DagDecoder(nspec)
+        assert a.advance() == b.advance()
+        while not a.done:
+            al = a.allowed()
+            assert al == b.allowed()
+            if rng.random() < 0.1:
+                expect(ValueError, b.feed, max(al) + 1000)
+            t = rng.choice(al)
+            a.feed(t)
+            b.feed(t)
+            assert a.advance() == b.advance()
+        assert b.done and b.text == a.text
+        json.loads(b.text)
+        expect(ValueError, b.feed, 34)
+bad = spec.native_payload()
+bad["name_trie"] = (["a", "ab"], [[1], [1, 2]])                 # not prefix-free
+expect(ValueError, rt.grammar_spec, bad)
+bad = spec.native_payload()
+bad["services"][0]["keys"] = [10 ** 6]                           # key id out of range
+expect(ValueError, rt.grammar_spec, bad)
+
 print(f"sanitize_fuzz OK ({ITERS} iterations)")

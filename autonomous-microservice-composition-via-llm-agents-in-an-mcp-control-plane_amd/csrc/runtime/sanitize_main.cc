@@ -6,12 +6,14 @@
 // runtime.cpp in with -fsanitize=address,undefined, registers the module as a
 // built-in (_runtime_san) and embeds the interpreter to run a fuzz script
 // (sanitize_fuzz.py) against it.  Any heap overflow, use-after-free or UB in
-// the allocator, the step packer or the topological sort aborts the run.
+// the allocator, the step packer, the topological sort or the grammar decoder
+// aborts the run.
 //
 // Build + run: tests/test_runtime_sanitize_cpu.py (host only; GPU sanitizers
 // are not available on the MI355X pool).
 #define MODULE_NAME _runtime_san
 #include "runtime.cpp"
+#include "grammar.cpp"
 
 #include <pybind11/embed.h>
 

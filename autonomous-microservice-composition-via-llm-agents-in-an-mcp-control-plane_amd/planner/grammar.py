@@ -26,6 +26,7 @@ through the model (their KV is needed) but in a single batched forward.
 from __future__ import annotations
 
 import json
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 RETRY_CHOICES = ["0", "1", "2", "3"]
@@ -153,6 +154,73 @@ class GrammarSpec:
             t = build_trie([self.tok.encode(a) for a in alts])
             self._trie_cache[alts] = t
         return t
+
+    # ------------------------------------------------------------ native
+    _native = None          # engine._runtime GrammarSpec, False when unavailable
+
+    def decoder(self):
+        """A fresh per-request decoder: the C++ state machine
+        (csrc/runtime/grammar.cpp, same tokens / allowed sets / text) when the
+        native runtime is built, else ``DagDecoder``.  MCP_NATIVE_GRAMMAR=0
+        forces the Python one."""
+        if self._native is None:
+            self._native = False
+            if os.environ.get("MCP_NATIVE_GRAMMAR", "1") != "0":
+                from ..engine import native
+                if native.available() and hasattr(native._RT, "grammar_spec") \
+                        and len(self.names) < 256:
+                    self._native = native._RT.grammar_spec(self.native_payload())
+        if self._native is not False:
+            from ..engine import native
+            return native._RT.DagDecoder(self._native)
+        return DagDecoder(self)
+
+    def native_payload(self) -> dict:
+        """Every forced chunk and choice of the program, tokenised here (the
+        Python tokenizer stays the single source of token ids)."""
+        def chunk(text):
+            return (text, self.encode(text))
+
+        def alts(a):
+            return (list(a), [list(self.tok.encode(x)) for x in a])
+
+        names = self.names
+        name_idx = {}
+        for i, n in enumerate(names):
+            name_idx.setdefault(n, i)
+        key_ids: Dict[str, int] = {}
+        keys = []
+        for ks in self.keys:
+            for k in ks:
+                if k not in key_ids:
+                    key_ids[k] = len(keys)
+                    srcs, a_s, _, pos = self.sources(k)
+                    keys.append({
+                        "first": chunk(json.dumps(k) + ":"),
+                        "rest": chunk("," + json.dumps(k) + ":"),
+                        "alt0": chunk(a_s[0]),
+                        "trie": alts(a_s),
+                        "pos": [-1 if n == k else pos[n] for n in names],
+                        "alt_name": [name_idx.get(x, -1) for x in srcs],
+                    })
+        services = []
+        for svc, ks in zip(self.services, self.keys):
+            fb = svc.get("fallback")
+            services.append({
+                "endpoint": chunk(',"endpoint":' + json.dumps(svc["endpoint"]) + ',"inputs":{'),
+                "keys": [key_ids[k] for k in ks],
+                "fallback": alts((',"fallback":' + json.dumps(fb) + "}", "}")) if fb else None,
+            })
+        return {
+            "S": len(names), "max_nodes": self.max_nodes, "min_nodes": self.min_nodes,
+            "allow_retries": bool(self.allow_retries), "jnames": list(self.jnames),
+            "name_trie": alts(self.jnames), "retry_trie": alts(tuple(RETRY_CHOICES)),
+            "cont_trie": alts((',{"name":', '],"edges":[')),
+            "chunks": {"start": chunk('{"nodes":[{"name":'), "retries": chunk('},"retries":'),
+                       "close1": chunk("}"), "close2": chunk("}}"), "next": chunk(',{"name":'),
+                       "edges": chunk('],"edges":['), "close_edge": chunk("}"), "end": chunk("]}")},
+            "services": services, "keys": keys, "encode": self.encode,
+        }
 
 
 class DagDecoder:

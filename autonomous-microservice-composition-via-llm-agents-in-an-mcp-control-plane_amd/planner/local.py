@@ -129,7 +129,7 @@ class LocalPlanner(Planner):
             if len(self._prefix_cache) > 256:
                 self._prefix_cache.clear()
             self._prefix_cache[key] = ptoks
-        return (DagDecoder(spec), ptoks, t1) if timed else (DagDecoder(spec), ptoks)
+        return (spec.decoder(), ptoks, t1) if timed else (spec.decoder(), ptoks)
 
     @staticmethod
     def suffix_text(intent: str) -> str:

@@ -1,0 +1,94 @@
+"""The native grammar decoder (csrc/runtime/grammar.cpp) against the Python
+DagDecoder (planner/grammar.py): both are driven in lock-step with the same
+random choices and must produce identical forced-token spans, allowed sets (in
+the same order: the sampling kernel keys its draw by list position), done
+flags and final text."""
+import json
+import random
+
+import pytest
+
+from mcp_amd.engine import native
+from mcp_amd.orchestrator import validate_dag
+from mcp_amd.planner.grammar import DagDecoder, GrammarSpec
+from mcp_amd.planner.tokenizer import get_tokenizer
+from mcp_amd.registry import make_service, synthetic_registry
+
+pytestmark = pytest.mark.skipif(not native.available() or not hasattr(native._RT, "grammar_spec"),
+                                reason="native runtime not built")
+
+
+def lockstep(spec, rng):
+    py_dec, c_dec = DagDecoder(spec), native._RT.DagDecoder(spec._native_for_test)
+    a, b = py_dec.advance(), c_dec.advance()
+    assert a == b
+    n = 0
+    while not py_dec.done:
+        assert not c_dec.done
+        al_py, al_c = py_dec.allowed(), c_dec.allowed()
+        assert al_py == al_c and len(al_py) >= 2
+        t = rng.choice(al_py)
+        py_dec.feed(t)
+        c_dec.feed(t)
+        a, b = py_dec.advance(), c_dec.advance()
+        assert a == b
+        n += 1
+    assert c_dec.done and c_dec.allowed() == []
+    assert c_dec.text == py_dec.text
+    assert c_dec.result() == py_dec.result()
+    return py_dec.result(), n
+
+
+def _spec(reg, **kw):
+    spec = GrammarSpec(reg, get_tokenizer(), **kw)
+    spec._native_for_test = native._RT.grammar_spec(spec.native_payload())
+    return spec
+
+
+@pytest.mark.parametrize("nsvc,max_nodes,min_nodes,retries",
+                         [(1, 3, 1, True), (3, 6, 1, True), (10, 5, 5, True), (10, 6, 2, False),
+                          (50, 8, 1, True), (200, 4, 4, True)])
+def test_native_matches_python(nsvc, max_nodes, min_nodes, retries):
+    reg = synthetic_registry(nsvc, seed=nsvc)
+    spec = _spec(reg, max_nodes=max_nodes, min_nodes=min_nodes, allow_retries=retries)
+    rng = random.Random(nsvc)
+    names = [s["name"] for s in reg]
+    for _ in range(30):
+        dag, _ = lockstep(spec, rng)
+        validate_dag(dag, names)
+
+
+def test_native_payload_key_named_like_a_service():
+    """An input key equal to a service name: the payload source of that key is
+    also a node name (an edge when that service was chosen earlier), exactly as
+    the Python program's string comparison has it."""
+    reg = [make_service("alpha", {"q": "string"}, {"alpha_out": "string"}, fallback=""),
+           make_service("beta", {"alpha": "string", "q": "string"}, {"r": "string"},
+                        fallback="http://beta-b/api"),
+           make_service("gamma", {"beta": "string", "alpha": "string"}, {"s": "string"}, fallback="")]
+    spec = _spec(reg, max_nodes=3, min_nodes=3)
+    rng = random.Random(3)
+    for _ in range(50):
+        lockstep(spec, rng)
+
+
+def test_native_rejects_disallowed_token():
+    spec = _spec(synthetic_registry(5, seed=2), max_nodes=3)
+    dec = native._RT.DagDecoder(spec._native_for_test)
+    dec.advance()
+    bad = max(dec.allowed()) + 1
+    while bad in dec.allowed():
+        bad += 1
+    with pytest.raises(ValueError):
+        dec.feed(bad)
+
+
+def test_spec_decoder_factory(monkeypatch):
+    reg = synthetic_registry(4, seed=1)
+    spec = GrammarSpec(reg, get_tokenizer(), max_nodes=2)
+    d = spec.decoder()
+    assert type(d).__name__ == "DagDecoder" and not isinstance(d, DagDecoder)   # native
+    monkeypatch.setenv("MCP_NATIVE_GRAMMAR", "0")
+    spec2 = GrammarSpec(reg, get_tokenizer(), max_nodes=2)
+    assert isinstance(spec2.decoder(), DagDecoder)
+    json.dumps(spec.native_payload()["chunks"])        # the payload is plain data (+ encode)
