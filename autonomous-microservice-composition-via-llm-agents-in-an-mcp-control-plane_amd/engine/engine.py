@@ -424,7 +424,8 @@ class LLMEngine:
             return None
         allowed = ctr = None
         if sample_seqs:            # grammar masks go in the same single H2D copy
-            allowed = [q.decoder.allowed() for q in sample_seqs]
+            with span("sched.allowed"):
+                allowed = [q.decoder.allowed() for q in sample_seqs]
             ctr = [(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF for q in sample_seqs]
         # a step that fits a captured bucket replays its hipGraph (prefix
         # copy-on-write, cascade and split-KV attention included)
@@ -478,6 +479,13 @@ class LLMEngine:
         if self.bcast is not None:          # TP: a collective that timed out fails the step
             self.model.comm_check()
         batch_seqs, sample_seqs = L.batch_seqs, L.sample_seqs
+        with span("retire.update"):
+            self._update(batch_seqs, sample_seqs, new_tokens)
+        self.stats["update_s"] += time.perf_counter() - t2
+        METRICS.set("batch_occupancy", len(self.running))
+        METRICS.set("kv_block_utilization", self.alloc.utilization())
+
+    def _update(self, batch_seqs, sample_seqs, new_tokens):
         # ---- bookkeeping
         for seq, take in batch_seqs:
             seq.num_cached += take
@@ -494,9 +502,6 @@ class LLMEngine:
             if not seq.is_prefix_job and seq.decoder.done and not seq.done:
                 self._finish(seq)
         self.running = [s for s in self.running if not s.done]
-        self.stats["update_s"] += time.perf_counter() - t2
-        METRICS.set("batch_occupancy", len(self.running))
-        METRICS.set("kv_block_utilization", self.alloc.utilization())
 
     def _launch(self, host, layout):
         """(packed step) -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
