@@ -22,15 +22,17 @@ def test_plan_file_shape():
         plan = json.load(f)
     assert plan["arch"] == "gfx950" and plan["mstep"] == 64
     shapes = {(s["N"], s["K"]) for s in plan["shapes"]}
-    # the four Llama-3-8B TP=1 projections: qkv, o, gate|up, down
+    # the four Llama-3-8B TP=1 projections: qkv, o, gate|up, down (+ the 70B ones, config 4)
     assert {(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)} <= shapes
+    assert {(10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672)} <= shapes
     for s in plan["shapes"]:
         assert all(c in (-1, 0, 1, 2) for c in s["codes"])
         # buckets below 256 rows are left to the skinny / 128 kernels
         assert all(c == -1 for c in s["codes"][:3])
         assert all(c >= 0 for c in s["codes"][3:])
         if "lib" in s:            # hipBLASLt buckets (tools/tune_gemm_lib.py): o, down, qkv only
-            assert (s["N"], s["K"]) in {(4096, 4096), (4096, 14336), (6144, 4096)}
+            assert (s["N"], s["K"]) in {(4096, 4096), (4096, 14336), (6144, 4096),      # 8B
+                                        (8192, 8192), (8192, 28672), (10240, 8192)}     # 70B
             assert len(s["lib"]) == len(s["codes"]) and set(s["lib"]) <= {0, 1}
 
 
@@ -101,5 +103,5 @@ def test_plan_loader_env(tmp_path, monkeypatch):
     finally:
         monkeypatch.delenv("MCP_GEMM_PLAN", raising=False)
         L.gemm_plan_clear()
-        assert ops._load_gemm_plan(L) == 4
+        assert ops._load_gemm_plan(L) == len(json.load(open(ops.GEMM_PLAN_FILE))["shapes"])
     assert os.path.exists(ops.GEMM_PLAN_FILE)

@@ -25,6 +25,7 @@ from mcp_amd.ops import reference as ref  # noqa: E402
 ops._LIB_ON = False                       # time our kernels, not an old "lib" plan
 path = sys.argv[1] if len(sys.argv) > 1 else ops.GEMM_PLAN_FILE
 m_max = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+only = {tuple(int(v) for v in x.split("x")) for x in sys.argv[3].split(",")} if len(sys.argv) > 3 else None
 plan = json.load(open(path))
 ops.lib()
 dev = "cuda"
@@ -47,15 +48,20 @@ def time_us(fn, n, reps=6):
 t0 = time.time()
 for sh in plan["shapes"]:
     N, K = sh["N"], sh["K"]
-    if (N, K) not in ((4096, 4096), (4096, 14336), (6144, 4096)):
+    if (N, K) not in ((4096, 4096), (4096, 14336), (6144, 4096),
+                      (8192, 8192), (8192, 28672), (10240, 8192)):
         continue
+    if only is not None and (N, K) not in only:
+        continue
+    qkv_shape = (N, K) in ((6144, 4096), (10240, 8192))
+    Hq = N // 128 - 16                     # 8 kv heads of d = 128 (Llama-3 8B / 70B)
     X = torch.randn(m_max, K, device=dev).bfloat16()
     Y = torch.randn(m_max, N, device=dev).bfloat16()
     Ws = [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
           for _ in range(max(2, int(1.2e9 // (N * K * 2))))]
-    if N == 6144:                          # Llama-3-8B heads: 32 q / 8 kv, d = 128, 64-token blocks
+    if qkv_shape:                          # Hq q / 8 kv heads, d = 128, 64-token blocks
         nb = m_max // 64 + 1
-        rope = (torch.empty(m_max, 32, 128, device=dev, dtype=torch.bfloat16),
+        rope = (torch.empty(m_max, Hq, 128, device=dev, dtype=torch.bfloat16),
                 torch.zeros(nb, 8, 64, 128, device=dev, dtype=torch.bfloat16),
                 torch.zeros(nb, 8, 64, 128, device=dev, dtype=torch.bfloat16),
                 torch.arange(m_max, device=dev, dtype=torch.int32) % 8000,
@@ -66,12 +72,12 @@ for sh in plan["shapes"]:
     for b in range(m_max // 64):
         M = (b + 1) * 64
         x, y = X[:M], Y[:M]
-        if N == 6144:
+        if qkv_shape:
             q, kc, vc, pos, slots, qkv = rope[0][:M], rope[1], rope[2], rope[3][:M], rope[4][:M], Q[:M]
-            ours = time_us(lambda i: ops.qkv_rope(x, Ws[i], pos, slots, cs, q, kc, vc, 32, 8, 128,
+            ours = time_us(lambda i: ops.qkv_rope(x, Ws[i], pos, slots, cs, q, kc, vc, Hq, 8, 128,
                                                   qkv=qkv), len(Ws))
             blas = time_us(lambda i: (torch.matmul(x, Ws[i].t(), out=qkv),
-                                      ops.rope_kv(qkv, pos, slots, cs, q, kc, vc, 32, 8, 128)), len(Ws))
+                                      ops.rope_kv(qkv, pos, slots, cs, q, kc, vc, Hq, 8, 128)), len(Ws))
         else:
             ours = time_us(lambda i: ops.gemm(x, Ws[i], R=y, out=y), len(Ws))
             blas = time_us(lambda i: y.addmm_(x, Ws[i].t()), len(Ws))

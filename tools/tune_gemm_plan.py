@@ -17,7 +17,10 @@ path by > 1 %.  Buckets up to 2048 rows are timed with COLD weights (each
 launch reads the next of several weight copies, > 1.5 GB: a serving step
 streams the whole model, nothing stays in the 256 MB Infinity Cache).
 
-    python tools/tune_gemm_plan.py [out.json] [m_max]
+    python tools/tune_gemm_plan.py [out.json] [m_max] [8b|70b]
+
+``70b``: the Llama-3-70B TP=1 projections (config 4) instead of the 8B ones;
+tools/merge_gemm_plan.py folds such a file into the shipped plan.
 """
 import json
 import os
@@ -34,8 +37,11 @@ L = ops.lib()
 L.gemm_plan_clear()
 out_path = sys.argv[1] if len(sys.argv) > 1 else ops.GEMM_PLAN_FILE
 m_max = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
-# Llama-3-8B (TP=1): qkv, o, gate|up (SwiGLU, interleaved), down
-SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
+# Llama-3-8B (TP=1): qkv, o, gate|up (SwiGLU, interleaved), down; 70B (TP=1) on request
+MODEL = sys.argv[3] if len(sys.argv) > 3 else "8b"
+SHAPES = {"8b": [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)],
+          "70b": [(10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672)]}[MODEL]
+SWIGLU_N = {28672, 57344}
 MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
@@ -90,7 +96,7 @@ for (N, K) in SHAPES:
         if M >= M_MIN and K % 128 == 0 and N % 256 == 0:
             cands += [(1, -1), (2, -1)]
         fl = []
-        if FLEX_MIN <= M <= FLEX_MAX and N != 28672:          # gate|up runs the SwiGLU epilogue
+        if FLEX_MIN <= M <= FLEX_MAX and N not in SWIGLU_N:   # gate|up runs the SwiGLU epilogue
             fl = [(3, f) for f in list(range(NFLEX)) + [32 + f for f in range(NFLEX)]]
         best = {c: float("inf") for c in cands + fl}
         for _ in range(3):
