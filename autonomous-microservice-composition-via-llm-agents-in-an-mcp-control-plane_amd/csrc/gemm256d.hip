@@ -412,7 +412,10 @@ int launch_gemm_tn_256sk_tail(const void* X, const void* W, void* Y, const void*
                               int K, int epi, int tile0, hipStream_t s);
 
 // hybrid data-parallel + stream-K tail: the full waves here, a tail wave at
-// most half full spread over every CU (MCP_GEMM_HYBRID=0 disables)
+// most a quarter full spread over every CU (MCP_GEMM_HYBRID=0 disables).
+// gate|up (N = 28672, 32 k-units) with cold weights: tails of 16 / 32 tiles
+// gain 2-6 %, 64 is even, 96 / 128 lose 2-6 % to the slab hand-offs
+// (M = 2368-2560: 473 vs 446 us plain; profiles/gemm_tuning.md)
 static int hybrid_tile0(int M, int N, int bm, int epi) {
   static int on = -1;
   if (on < 0) {
@@ -423,7 +426,7 @@ static int hybrid_tile0(int M, int N, int bm, int epi) {
   if (!g_cus) gemm256d_waves_bm(M, N, 128, 256);     // initialises g_cus
   const int T = ((M + 255) / 256) * ((N + BN - 1) / BN);
   const int full = (T / g_cus) * g_cus, tail = T - full;
-  return (full > 0 && tail > 0 && 2 * tail <= g_cus) ? full : 0;
+  return (full > 0 && tail > 0 && 4 * tail <= g_cus) ? full : 0;
 }
 
 static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R, int M, int N,
