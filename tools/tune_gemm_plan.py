@@ -46,6 +46,9 @@ MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
 FLEX_MIN, FLEX_MAX = 128, 2048             # flex tiles measured here (cold weights up to FLEX_MAX)
+# MCP_TUNE_COLD_ALL=1: cold weights at every M (a decode step streams the whole
+# model at any size; warm weights flatter the larger-N shapes above 2048 rows)
+COLD_ALL = os.environ.get("MCP_TUNE_COLD_ALL", "0") == "1"
 NFLEX = L.gemm_flex_count()
 
 dev = "cuda"
@@ -89,7 +92,7 @@ for (N, K) in SHAPES:
     for b in range(m_max // MSTEP):
         M = (b + 1) * MSTEP
         X, Y = Xf[:M], Yf[:M]
-        Ws = Wcold if M <= FLEX_MAX else [W]
+        Ws = Wcold if (M <= FLEX_MAX or COLD_ALL) else [W]
         # code-0 candidates: (0, split)
         svals = ([2, 4, 8] if M <= 128 else [1, 2, 4, 8]) if M <= M_SPLIT_MAX else [-1]
         cands = [(0, sv) for sv in svals]
