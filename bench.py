@@ -144,9 +144,15 @@ def main():
         engine.run()
         return seqs, time.perf_counter() - t, engine.stats["tokens"] - tok0
 
+    # server start-up (planner.local / bench_serve): capture the hipGraph
+    # buckets before any request, so no timed step pays for a lazy capture
+    t0 = time.time()
+    ncap = engine.warm_graphs(contexts=(2048,)) if cuda else 0
+    log(f"[rank {rank}] start-up graph capture: {ncap} graphs in {time.time() - t0:.1f}s")
     for w in range(args.warmup):
         _, dt, toks = one_step(-1 - w)
         log(f"[rank {rank}] warmup {w}: {dt * 1e3:.0f} ms, {toks} tokens")
+    cap0 = engine.stats.get("graph_captures", 0)
     seqs_all = []
     if world > 1:
         dist.barrier()
@@ -188,7 +194,8 @@ def main():
             seqs_all += b
             log(f"[rank {rank}] batch {k}: done {max(q.t_done for q in b) - t_sub[k]:.3f} s after submit")
     tokens = engine.stats["tokens"] - tok0
-    log(f"[rank {rank}] {engine.stats['steps'] - steps0} engine steps, {tokens} tokens")
+    log(f"[rank {rank}] {engine.stats['steps'] - steps0} engine steps, {tokens} tokens, "
+        f"{engine.stats.get('graph_captures', 0) - cap0} lazy graph captures in the timed steps")
     sync()
     if world > 1:
         dist.barrier()
