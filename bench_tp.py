@@ -96,6 +96,9 @@ def main():
     reg = MemoryRegistry(synthetic_registry(args.services, seed=4))
     planner = LocalPlanner(eng, reg, max_nodes=args.max_nodes, retrieval_threshold=10 ** 9)
     names = [s.name for s in reg.list_services()]
+    t0 = time.perf_counter()
+    ncap = eng.warm_graphs(contexts=(8192,))         # server start-up capture (planner.local)
+    log(f"[rank 0] start-up graph capture: {ncap} graphs in {time.perf_counter() - t0:.1f}s")
     for w in range(args.warmup):
         planner.plan_many([synthetic_intent(10_000 + i) for i in range(args.batch)])
     torch.cuda.synchronize()
