@@ -267,6 +267,23 @@ class LLMEngine:
         self.last_progress = time.perf_counter()
         return n
 
+    def launch_ahead(self) -> bool:
+        """Launch the next step now and retire it in the next ``step()``: a
+        caller that is about to prepare more requests (suffix tokenisation of a
+        batch) lets the GPU run the queued work - the batch's shared-prefix job
+        - meanwhile.  Only on an idle engine (nothing running or in flight) and
+        without the two-cohort pipeline; returns whether a step was launched.
+        Headline A/B (same box, interleaved): 217.3 / 215.6 plans/s with it,
+        215.4 / 219.1 without - within run-to-run noise (the overlap is the
+        ~10 ms suffix tokenisation of a 256-intent batch)."""
+        if self.pipeline or self.inflight or self.running or not self.waiting:
+            return False
+        L = self._schedule_launch(None)
+        if L is None:
+            return False
+        self.inflight[-1] = L
+        return True
+
     def has_work(self) -> bool:
         return bool(self.running or self.waiting or self.inflight)
 

@@ -136,12 +136,21 @@ class LocalPlanner(Planner):
         return f"\nUser intent: “{intent}”\n\nJSON DAG:"
 
     # ------------------------------------------------------- batch (sync)
-    def submit_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> list:
-        """Queue a batch of intents on the engine without running it (the
-        caller drives ``engine.step()``; ``plan_many`` = this + run)."""
+    def submit_many(self, intents: Sequence[str], fresh_prefix: bool = True,
+                    launch_ahead: bool = False) -> list:
+        """Queue a batch of intents on the engine (the caller drives
+        ``engine.step()``; ``plan_many`` = this + run).  ``launch_ahead``: the
+        batch's shared registry-prefix job is created and launched on the GPU
+        first, and the per-intent suffixes are tokenised while it runs (the
+        caller must be the engine's only driver)."""
         services = self.registry.list_services()
         seqs = []
         batch_enc = getattr(self.tok, "encode_batch", None)
+        if launch_ahead and intents and batch_enc and (self.retriever is None or
+                                                       len(services) <= self.retrieval_threshold):
+            _, ptoks0 = self._decoder_and_prefix(intents[0], services)
+            if self.engine.get_prefix(ptoks0) is not None:
+                self.engine.launch_ahead()
         sufs = batch_enc([self.suffix_text(it) for it in intents]) if batch_enc else None
         for i, it in enumerate(intents):
             if sufs is not None and (self.retriever is None or
@@ -160,7 +169,7 @@ class LocalPlanner(Planner):
     def plan_many(self, intents: Sequence[str], fresh_prefix: bool = True) -> List[dict]:
         """Plan a batch of intents to completion on the calling thread."""
         with self._lock:
-            seqs = self.submit_many(intents, fresh_prefix)
+            seqs = self.submit_many(intents, fresh_prefix, launch_ahead=True)
             self.engine.run()
         out = []
         for s in seqs:

@@ -140,7 +140,8 @@ def main():
         intents = [synthetic_intent(base + i) for i in range(args.batch)]
         tok0 = engine.stats["tokens"]
         t = time.perf_counter()
-        seqs = planner.submit_many(intents)
+        # the batch prefix job runs on the GPU while the suffixes tokenise (MCP_LAUNCH_AHEAD=0: off)
+        seqs = planner.submit_many(intents, launch_ahead=os.environ.get("MCP_LAUNCH_AHEAD", "1") == "1")
         engine.run()
         return seqs, time.perf_counter() - t, engine.stats["tokens"] - tok0
 
