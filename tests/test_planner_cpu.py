@@ -379,3 +379,26 @@ def test_prefix_split_rule(monkeypatch):
     assert ops.prefix_splits(16, 704, 8) == 1
     monkeypatch.setenv("MCP_PREFIX_SPLIT", "3")
     assert ops.prefix_splits(4096, 704, 8) == 3
+
+
+def test_launch_ahead_matches_plain_submit():
+    """submit_many(launch_ahead=True) launches the batch's prefix job before the
+    suffixes are tokenised and retires it in the next step: same greedy plans,
+    all blocks returned, nothing left in flight; a second launch_ahead while a
+    step is in flight does nothing."""
+    reg = MemoryRegistry(synthetic_registry(6, seed=4))
+    intents = [synthetic_intent(i) for i in range(5)]
+    out = []
+    for ahead in (False, True):
+        torch.manual_seed(0)
+        model = LlamaModel.random("tiny", "cpu", seed=1)
+        eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, graphs=False)
+        planner = LocalPlanner(eng, reg, max_nodes=3)
+        seqs = planner.submit_many(intents, launch_ahead=ahead)
+        assert bool(eng.inflight) == ahead
+        if ahead:
+            assert not eng.launch_ahead()              # a step is already in flight
+        eng.run()
+        assert eng.alloc.num_free == eng.kv.num_blocks and not eng.inflight
+        out.append([s.result for s in seqs])
+    assert out[0] == out[1]
