@@ -28,7 +28,7 @@ from typing import Dict, List, Optional, Sequence
 
 from ..utils.metrics import METRICS
 from .base import Planner
-from .grammar import DagDecoder, GrammarSpec
+from .grammar import GrammarSpec
 from .prompt import build_prompt_parts
 from .tokenizer import get_tokenizer
 
