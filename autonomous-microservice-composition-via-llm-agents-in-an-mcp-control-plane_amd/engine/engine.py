@@ -417,30 +417,45 @@ class LLMEngine:
                     casc = None
         order = pool
         if casc is not None:
-            order = [q for q in pool if q.prefix is casc and q.materialized] + \
-                    [q for q in pool if not (q.prefix is casc and q.materialized)]
+            first, rest = [], []
+            for q in pool:
+                (first if (q.prefix is casc and q.materialized) else rest).append(q)
+            order = first + rest
         pre_tokens = 0
         casc_keys = (casc.length // BLOCK_SIZE) * BLOCK_SIZE if casc is not None else 0
+        alloc = self.alloc.alloc
+        add_entry, add_batch, add_sample = entries.append, batch_seqs.append, sample_seqs.append
+        # the per-request loop of every step (host critical path): locals bound,
+        # _ensure_blocks / wants_sample inlined
         for seq in order:
             if not seq.materialized:           # waiting for its prefix job
                 continue
-            n = len(seq.pending)
+            pend = seq.pending
+            n = len(pend)
             if n == 0:
                 continue
-            take = min(n, budget - T)
+            take = budget - T
             if take <= 0:
                 break
+            if n < take:
+                take = n
             start = seq.num_cached
-            self._ensure_blocks(seq, start + take)
-            in_casc = casc is not None and seq.prefix is casc
+            blocks = seq.blocks
+            need = (start + take + BLOCK_SIZE - 1) // BLOCK_SIZE - len(blocks)
+            if need > 0:
+                blocks += alloc(need)
             T += take
-            if in_casc:
+            if casc is not None and seq.prefix is casc:
                 pre_tokens = T
-            sample = take == n and seq.wants_sample
-            entries.append((seq.pending, take, start, seq.blocks, casc_keys if in_casc else 0, sample))
-            batch_seqs.append((seq, take))
+                ck = casc_keys
+            else:
+                ck = 0
+            dec = seq.decoder
+            sample = take == n and dec is not None and not dec.done
+            add_entry((pend, take, start, blocks, ck, sample))
+            add_batch((seq, take))
             if sample:
-                sample_seqs.append(seq)
+                add_sample(seq)
         group = self.model.cfg.group
         if T == 0:
             if copies:     # copy-on-write blocks still have to land before later steps
