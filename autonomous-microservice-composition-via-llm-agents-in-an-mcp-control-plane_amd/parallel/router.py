@@ -37,6 +37,7 @@ import itertools
 import multiprocessing as mp
 import queue
 import threading
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -71,7 +72,11 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     from ..retrieval.store import SchemaIndex
     if device.startswith("cuda"):
         torch.cuda.set_device(torch.device(device))
-    m = LlamaModel.random(cfg.model, device, seed=cfg.seed)
+    if os.path.isdir(cfg.model):                       # an HF checkpoint directory
+        from ..models.weights import model_from_checkpoint
+        m = model_from_checkpoint(cfg.model, device)
+    else:
+        m = LlamaModel.random(cfg.model, device, seed=cfg.seed)
     kw = {"num_blocks": cfg.num_blocks} if cfg.num_blocks else {}
     eng = LLMEngine(m, max_batch=cfg.max_batch, max_step_tokens=cfg.max_step_tokens,
                     temperature=cfg.temperature, seed=cfg.seed + idx, **kw)
@@ -81,7 +86,9 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     else:
         registry = _VersionedMemoryRegistry(records, version)
     retriever = SchemaIndex(registry, dim=cfg.embed_dim, device=device)
-    planner = LocalPlanner(eng, registry, max_nodes=cfg.max_nodes, retriever=retriever,
+    from ..planner.tokenizer import tokenizer_for
+    planner = LocalPlanner(eng, registry, tokenizer=tokenizer_for(cfg.model),
+                           max_nodes=cfg.max_nodes, retriever=retriever,
                            retrieval_threshold=cfg.retrieval_threshold, topk=cfg.topk)
     outq.put(("ready", idx, None))
     pending = {}

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ..planner.local import LocalPlanner
+from ..planner.tokenizer import tokenizer_for
 
 
 def _default_devices(tp: int) -> List[str]:
@@ -55,12 +56,17 @@ def build_rank(model_name: str, rank: int, world: int, device: str, seed: int,
     from ..models.llama import (LlamaModel, LlamaWeights, get_config, random_weights,
                                 shard_layer)
     from .comm import StepBroadcaster
-    cfg = get_config(model_name)
     group = dist.group.WORLD
-    if full_weights_seed is None:
+    if os.path.isdir(model_name):            # an HF checkpoint: this rank's shards only
+        from ..models.weights import model_from_checkpoint
+        model = model_from_checkpoint(model_name, device, tp_rank=rank, tp=world, tp_group=group)
+        cfg = model.cfg
+    elif full_weights_seed is None:
+        cfg = get_config(model_name)
         model = LlamaModel.random(model_name, device, seed=seed, tp_rank=rank, tp=world,
                                   tp_group=group)
     else:
+        cfg = get_config(model_name)
         full = random_weights(cfg, device, seed=full_weights_seed)
         sh = LlamaWeights(embed=full.embed, final_norm=full.final_norm, lm_head=full.lm_head,
                           layers=[shard_layer(l, cfg, rank, world) for l in full.layers])
@@ -127,7 +133,8 @@ class TPPlanner(LocalPlanner):
                         temperature=settings.temperature if temperature is None else temperature,
                         seed=settings.seed, bcast=bc)
         retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)
-        planner = cls(eng, registry, max_nodes=settings.max_nodes, retriever=retr,
+        planner = cls(eng, registry, tokenizer=tokenizer_for(settings.model),
+                      max_nodes=settings.max_nodes, retriever=retr,
                       retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
         planner._workers = workers
         return planner

@@ -30,7 +30,7 @@ from ..utils.metrics import METRICS
 from .base import Planner
 from .grammar import GrammarSpec
 from .prompt import build_prompt_parts
-from .tokenizer import get_tokenizer
+from .tokenizer import get_tokenizer, tokenizer_for
 
 
 class EngineStalled(RuntimeError):
@@ -91,7 +91,11 @@ class LocalPlanner(Planner):
             # capture the hipGraph buckets at start-up, not under the first requests
             eng.warm_graphs(max_tokens=settings.max_step_tokens)
         retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)
-        return cls(eng, registry, max_nodes=settings.max_nodes, retriever=retr,
+        tok = tokenizer_for(settings.model)
+        if tok.vocab_size > model.cfg.vocab_size:
+            raise ValueError(f"tokenizer vocabulary {tok.vocab_size} exceeds the model's "
+                             f"{model.cfg.vocab_size}")
+        return cls(eng, registry, tokenizer=tok, max_nodes=settings.max_nodes, retriever=retr,
                    retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
 
     # ----------------------------------------------------------- prepare
@@ -125,7 +129,7 @@ class LocalPlanner(Planner):
         ptoks = self._prefix_cache.get(key)
         if ptoks is None:
             prefix, _ = build_prompt_parts(cands, intent)
-            ptoks = [self.tok.bos_id] + self.tok.encode(prefix)
+            ptoks = self.tok.prompt_ids(prefix)
             if len(self._prefix_cache) > 256:
                 self._prefix_cache.clear()
             self._prefix_cache[key] = ptoks
