@@ -167,7 +167,7 @@ void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64
 
 void gemm_plan_set_py(int64_t N, int64_t K, const std::vector<int64_t>& codes) {
   std::vector<int> c(codes.begin(), codes.end());
-  for (int v : c) TORCH_CHECK(v >= -1 && v <= 2, "gemm plan code must be -1..2");
+  for (int v : c) TORCH_CHECK(v >= -1 && v <= 5, "gemm plan code must be -1..5");
   gemm_plan_set((int)N, (int)K, c.data(), (int)c.size());
 }
 

@@ -217,7 +217,8 @@ int gemm256_num_cus();
 // loaded by ops.lib()): per (N, K) weight shape one code per 64-row M bucket
 // (bucket b = rows (64 b, 64 b + 64]; every tile height divides 64, so all M
 // of a bucket have the tile counts of its top row, the row that was timed):
-// 0 = 128^2 kernel, 1 = AGPR kernel with 256-row tiles, 2 = with 192-row tiles.
+// 0 = 128^2 kernel, 1..5 = AGPR kernel (gemm256d.hip) with 256-, 192-, 160-,
+// 224- or 128-row tiles (gemm256d_code_height).
 // Written once at load, before any launch; read-only afterwards.
 namespace {
 struct GemmPlan {
@@ -492,6 +493,10 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                          int algo, hipStream_t s) {
   if (algo >= 16 && launch_gemm_flex(X, W, Y, R, M, N, K, algo - 16, s) == 0) return;   // tuning
+  // 9..13: the AGPR kernel at the tile height of plan code algo - 8 (tuning)
+  if (algo >= 9 && algo <= 13 &&
+      launch_gemm_tn_256d_bm(X, W, Y, R, M, N, K, R ? 1 : 0, gemm256d_code_height(algo - 8), s) == 0)
+    return;
   if (algo < 0) launch_gemm_tn(X, W, Y, R, M, N, K, s);
   else if (algo == 3 && launch_gemm_stream(X, W, Y, R, M, N, K, R ? 1 : 0, RopeArgs{}, s) == 0) return;
   else if (algo == 2 && launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0) return;

@@ -383,6 +383,9 @@ int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int
     case 50: return launch_gemm_tn_256sk(X, W, Y, nullptr, M, N, K, 0, 1, s);
     case 51: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 192, s);
     case 52: return launch_gemm_tn_256d(X, W, Y, nullptr, M, N, K, 0, s);
+    case 53: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 160, s);
+    case 54: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 224, s);
+    case 55: return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 0, 128, s);
     default: return 1;
   }
 }

@@ -30,11 +30,15 @@
 // Rows past M re-read row M-1 (clamped per-lane offsets); their outputs are
 // never stored.
 //
-// Tile height BMT = 256 or 192 (96x128 per wave, 6x8 MFMA tiles): M = 2600
-// rows (a decode step of the headline bench) are 11 M-tiles of 256 - 176
-// tiles for N = 4096, 69 % of 256 CUs - but 14 M-tiles of 192 - 224 tiles,
-// 88 %.  gemm.hip picks the height by a wave-quantisation cost model (the
-// same choice as hipBLASLt's MT192x256 kernels for these shapes).
+// Tile height BMT = 128, 160, 192, 224 or 256 rows (BMT / 2 rows per wave =
+// BMT / 32 MFMA row tiles of 16).  One wave of workgroups is the unit of
+// time at one workgroup per CU, so the height that makes ceil(M / BMT) x
+// (N / 256) closest to a whole number of waves wins: for N = 4096 (16 column
+// tiles) every M in 1792..4096 has a height with 14-16 row tiles (>= 88 % of
+// the 256 CUs busy), e.g. M = 2560 = 16 x 160 - where 256-row tiles fill
+// 160 of 256 CUs.  The measured plan (ops/gemm_plan_gfx950.json, codes 1-5)
+// picks the height per 64-row M bucket; smaller heights read more LDS and
+// issue more DMA per MFMA (8 + MTW fragment reads per 8 MTW MFMAs).
 #include <type_traits>
 
 #include "common.h"
@@ -87,12 +91,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
                                                        int K, const RopeArgs ra) {
-  static_assert(BMT == 256 || BMT == 192, "tile height");
-  constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (8 or 6)
-  constexpr int WROWS = BMT / 2;                    // rows per wave (128 or 96)
+  static_assert(BMT % 32 == 0 && BMT >= 128 && BMT <= 256, "tile height");
+  constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (4..8)
+  constexpr int WROWS = BMT / 2;                    // rows per wave (64..128)
   constexpr int PIECE_A = BMT * ROWB;               // the X operand of a slot
   constexpr int SLOT_B = PIECE_A + PIECE_BB;
-  constexpr int QA = BMT / 32;                      // A DMA instructions per wave (8 or 6)
+  constexpr int QA = BMT / 32;                      // A DMA instructions per wave (4..8)
   constexpr int NDMA = QA + 8;                      // DMA instructions per wave and k-tile
   constexpr int NRD = 8 + MTW;                      // fragment reads per wave and k-half
   constexpr int NMF = MTW * 8;                      // MFMAs per wave and k-half
@@ -184,8 +188,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   for (int i = 0; i < NDMA; ++i) dma1(0, 0, i);
 #pragma unroll
   for (int i = 0; i < NDMA; ++i) dma1(1, 1, i);
+  // tile 0 landed (own DMAs): the NDMA of tile 1 may still be in flight
   if constexpr (NDMA == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (NDMA == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  else if constexpr (NDMA == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  else if constexpr (NDMA == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   raw_barrier();
 #pragma unroll
   for (int i = 0; i < NRD; ++i) fread1(0, 0, F[0], i);
@@ -261,6 +269,23 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     static_assert(4 * WROWS * RB <= 2 * SLOT_B, "epilogue staging fits the operand slots");
     __syncthreads();                                 // every wave is done with the slots
     char* stg = smem + wave * (WROWS * RB);
+    const int lr = lane / NCH, lc = lane % NCH;
+    constexpr int NST = WROWS / RPS;                 // store rows per lane
+    const int ldy = EPI == 2 ? N / 2 : N;
+    const int col0 = EPI == 2 ? (n0 + wn * 128) / 2 : n0 + wn * 128;
+    // EPI 1: this lane's residual rows, all loaded up front (clamped rows, no
+    // branch) so their latency hides behind the LDS staging below; loaded
+    // behind the per-row "m < M" store guard they serialised on one L2 / HBM
+    // round trip per row (cdna_hip_programming.md §5 "Projection GEMM at
+    // M = 256" item 4(c): ~10 us per o projection at M = 2560)
+    bf16x8 rres[EPI == 1 ? NST : 1];
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        const int m = min(m0 + wm * WROWS + i * RPS + lr, M - 1);
+        rres[i] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldy + col0 + lc * 8);
+      }
+    }
     auto put = [&](int row, int col, const bf16x4& v) {
       const int byte = col * 2;
       *reinterpret_cast<bf16x4*>(stg + row * RB + (((byte >> 4) ^ (row & (NCH - 1))) << 4) +
@@ -323,19 +348,16 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
         }
       }
     }
-    const int ldy = EPI == 2 ? N / 2 : N;
-    const int col0 = EPI == 2 ? (n0 + wn * 128) / 2 : n0 + wn * 128;
-    const int lr = lane / NCH, lc = lane % NCH;
     // EPI 3, K / V heads: this lane's rows' cache slots, loaded up front (a
     // load per row inside the loop would serialise on its latency)
-    int rslot[EPI == 3 ? WROWS / RPS : 1];
+    int rslot[EPI == 3 ? NST : 1];
     if (EPI == 3 && head >= ra.Hq) {
 #pragma unroll
-      for (int i = 0; i < WROWS / RPS; ++i)
+      for (int i = 0; i < NST; ++i)
         rslot[i] = ra.slots[min(m0 + wm * WROWS + i * RPS + lr, M - 1)];
     }
 #pragma unroll
-    for (int i = 0; i < WROWS / RPS; ++i) {
+    for (int i = 0; i < NST; ++i) {
       const int row = i * RPS + lr;
       const int m = m0 + wm * WROWS + row;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + row * RB + ((lc ^ (row & (NCH - 1))) << 4));
@@ -357,9 +379,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
       if (m < M) {
         const size_t off = (size_t)m * ldy + col0 + lc * 8;
         if constexpr (EPI == 1) {
-          const bf16x8 r = *reinterpret_cast<const bf16x8*>(R + off);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)r[j]);
+          for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rres[i][j]);
         }
         *reinterpret_cast<bf16x8*>(Y + off) = v;
       }
@@ -378,10 +399,22 @@ int gemm256d_ok(int M, int N, int K) {
   return 0;
 }
 
-// Tile height by waves of tiles on the CUs (one workgroup per CU either way):
-// time ~ ceil(tiles / G) x tile time, and a 192-row tile takes 3/4 of a
-// 256-row one; MCP_GEMM_BM=256 / 192 forces it.
+// Tile height by waves of tiles on the CUs (one workgroup per CU at every
+// height): time ~ ceil(tiles / G) x tile time, a tile of h rows costing h / 256
+// of a 256-row one divided by the height's relative MFMA efficiency (more LDS
+// reads and DMA per MFMA at smaller heights; profiles/gemm_tuning.md).
+// MCP_GEMM_BM=<height> forces one; the measured plan (codes 1-5) wins over
+// this model wherever it has the shape.
 static int g_cus = 0;
+static double height_eff(int bm) {
+  switch (bm) {
+    case 256: return 1.0;
+    case 224: return 0.98;
+    case 192: return 0.96;
+    case 160: return 0.92;
+    default: return 0.87;
+  }
+}
 double gemm256d_waves_bm(int M, int N, int K, int bm) {
   if (!g_cus) {
     int d = 0;
@@ -391,7 +424,19 @@ double gemm256d_waves_bm(int M, int N, int K, int bm) {
                 ? prop.multiProcessorCount : 256;
   }
   const double tiles = (double)((M + bm - 1) / bm) * ((N + BN - 1) / BN);
-  return ceil(tiles / g_cus) * bm / 256.0;           // in 256-row tile times
+  return ceil(tiles / g_cus) * bm / 256.0 / height_eff(bm);   // in 256-row tile times
+}
+
+// plan code -> tile height (gemm.hip's measured plan; 0 = the 128^2 kernel)
+int gemm256d_code_height(int code) {
+  switch (code) {
+    case 1: return 256;
+    case 2: return 192;
+    case 3: return 160;
+    case 4: return 224;
+    case 5: return 128;
+    default: return 0;
+  }
 }
 
 int gemm256d_height(int M, int N, int K) {
@@ -400,14 +445,22 @@ int gemm256d_height(int M, int N, int K) {
     const char* e = getenv("MCP_GEMM_BM");
     forced = e ? atoi(e) : 0;
   }
-  if (forced == 256 || forced == 192) return forced;
-  const int plan = gemm_plan_lookup(M, N, K);        // measured (gemm.hip)
-  if (plan == 1 || plan == 2) return plan == 2 ? 192 : 256;
-  // the 192 kernel runs ~4 % below the 256 one per FLOP: prefer 256 on ties
-  return gemm256d_waves_bm(M, N, K, 192) * 1.04 < gemm256d_waves_bm(M, N, K, 256) ? 192 : 256;
+  if (forced >= 128 && forced <= 256 && forced % 32 == 0) return forced;
+  const int plan_h = gemm256d_code_height(gemm_plan_lookup(M, N, K));   // measured (gemm.hip)
+  if (plan_h) return plan_h;
+  int best = 256;
+  double bc = gemm256d_waves_bm(M, N, K, 256);
+  for (int bm = 224; bm >= 128; bm -= 32) {
+    const double c = gemm256d_waves_bm(M, N, K, bm);
+    if (c < bc) {
+      bc = c;
+      best = bm;
+    }
+  }
+  return best;
 }
 
-// bm: tile height 256 or 192 (0: pick by gemm256d_height); ra: EPI 3 only
+// bm: tile height 128-256 (0: pick by gemm256d_height); ra: EPI 3 only
 int launch_gemm_tn_256sk_tail(const void* X, const void* W, void* Y, const void* R, int M, int N,
                               int K, int epi, int tile0, hipStream_t s);
 
@@ -429,6 +482,22 @@ static int hybrid_tile0(int M, int N, int bm, int epi) {
   return (full > 0 && tail > 0 && 4 * tail <= g_cus) ? full : 0;
 }
 
+template <int BMT>
+static int launch_height(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                         int K, int epi, dim3 grid, const RopeArgs& ra, hipStream_t s) {
+  auto x = (const bf16*)X;
+  auto w = (const bf16*)W;
+  auto y = (bf16*)Y;
+  auto r = (const bf16*)R;
+  switch (epi) {
+    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
+    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+    default: return 2;
+  }
+}
+
 static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R, int M, int N,
                             int K, int epi, int bm, const RopeArgs& ra, hipStream_t s) {
   if (const int rc = gemm256d_ok(M, N, K)) return rc;
@@ -446,34 +515,16 @@ static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R
   const dim3 grid(tile0 > 0 ? tile0 : nm * nn);
   if (tile0 > 0) {
     // full waves first (same stream: the tail starts when they are done)
-    int rc = 0;
-    switch (epi) {
-      case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N, K, ra); break;
-      case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, ra); break;
-      default: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N, K, ra); break;
-    }
-    rc = launch_gemm_tn_256sk_tail(X, W, Y, R, M, N, K, epi, tile0, s);
-    return rc;
+    if (const int rc = launch_height<256>(X, W, Y, R, M, N, K, epi, grid, ra, s)) return rc;
+    return launch_gemm_tn_256sk_tail(X, W, Y, R, M, N, K, epi, tile0, s);
   }
-  auto x = (const bf16*)X;
-  auto w = (const bf16*)W;
-  auto y = (bf16*)Y;
-  auto r = (const bf16*)R;
-  if (bm == 192) {
-    switch (epi) {
-      case 0: gemm_tn_256d<0, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-      case 1: gemm_tn_256d<1, 192><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
-      case 2: gemm_tn_256d<2, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-      case 3: gemm_tn_256d<3, 192><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-      default: return 2;
-    }
-  }
-  switch (epi) {
-    case 0: gemm_tn_256d<0, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-    case 1: gemm_tn_256d<1, 256><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
-    case 2: gemm_tn_256d<2, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-    case 3: gemm_tn_256d<3, 256><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-    default: return 2;
+  switch (bm) {
+    case 256: return launch_height<256>(X, W, Y, R, M, N, K, epi, grid, ra, s);
+    case 224: return launch_height<224>(X, W, Y, R, M, N, K, epi, grid, ra, s);
+    case 192: return launch_height<192>(X, W, Y, R, M, N, K, epi, grid, ra, s);
+    case 160: return launch_height<160>(X, W, Y, R, M, N, K, epi, grid, ra, s);
+    case 128: return launch_height<128>(X, W, Y, R, M, N, K, epi, grid, ra, s);
+    default: return 4;
   }
 }
 

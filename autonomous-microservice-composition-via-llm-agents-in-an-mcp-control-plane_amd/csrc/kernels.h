@@ -80,6 +80,9 @@ void gemm_plan_set_splits(int N, int K, const int* splits, int n);
 int gemm_plan_split(int M, int N, int K);
 void gemm_plan_clear();
 int gemm256d_ok(int M, int N, int K);
+int gemm256d_code_height(int code);     // plan code 1..5 -> AGPR tile height (0: none)
+int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                           int K, int epi, int bm, hipStream_t s);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,

@@ -58,7 +58,6 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
     import json
 
     path = path or os.environ.get("MCP_GEMM_PLAN", GEMM_PLAN_FILE)
-    _LIB_RES.clear()
     if path == "0" or not os.path.exists(path) or not hasattr(mod, "gemm_plan_set"):
         return 0
     with open(path) as f:
@@ -70,28 +69,7 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
             mod.gemm_plan_set_splits(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["splits"]])
         if "flex" in sh and hasattr(mod, "gemm_plan_set_flex"):
             mod.gemm_plan_set_flex(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["flex"]])
-        if "lib" in sh:
-            _LIB_RES[(int(sh["N"]), int(sh["K"]))] = [bool(c) for c in sh["lib"]]
     return len(plan["shapes"])
-
-
-# 64-row M buckets where the tuner measured hipBLASLt faster than every MFMA
-# path of ours (tools/tune_gemm_lib.py, cold weights): residual projections (o,
-# down) as its GEMM with its own beta = 1 epilogue (x += a W^T in place, one
-# fp32 rounding); the QKV projection as its GEMM + our rope_kv against our
-# qkv_rope (RoPE + paged K/V write fused in the AGPR epilogue).  Down projection (K = 14336) at M = 2176-3072: one wave of our
-# 256- / 192-row tiles leaves 1/8 - 1/3 of the CUs idle, 277-287 us vs 213-250
-# (profiles/gemm_tuning.md).  MCP_GEMM_LIB=0 keeps every call on our kernels.
-_LIB_RES = {}
-_LIB_ON = os.environ.get("MCP_GEMM_LIB", "1") == "1"
-
-
-def _lib_pick(M: int, N: int, K: int) -> bool:
-    b = _LIB_RES.get((N, K)) if _LIB_ON else None
-    if not b or M <= 0:
-        return False
-    i = (M - 1) >> 6
-    return i < len(b) and b[i]
 
 
 def library_path() -> Optional[str]:
@@ -171,16 +149,13 @@ def embedding(ids, table, out=None):
 
 
 def gemm(X, W, R=None, out=None, algo: int = -1):
-    """Y = X @ W^T (+ R).  X [M, K], W [N, K].  algo: -1 auto, 0 = 128^2, 1 = 256^2."""
+    """Y = X @ W^T (+ R).  X [M, K], W [N, K].  algo: -1 auto (the measured
+    plan), 0 = 128^2, 1 = 256^2 path, 9..13 = AGPR kernel at plan code algo - 8."""
     if X.is_cuda:
         if _TRACE is not None:
             _trace(X, W, "gemm" if R is None else "gemm+res")
-        L = lib()
-        if R is not None and out is R and algo < 0 and X.dim() == 2 and \
-                _lib_pick(X.shape[0], W.shape[0], W.shape[1]):
-            return out.addmm_(X, W.t())             # hipBLASLt, beta = 1 (measured faster)
         out = X.new_empty(*X.shape[:-1], W.shape[0]) if out is None else out
-        L.gemm(X, W, out, R, algo)
+        lib().gemm(X, W, out, R, algo)
         return out
     r = ref.gemm(X, W, R)
     return r if out is None else out.copy_(r)
@@ -206,10 +181,6 @@ def qkv_rope(h, wqkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, 
     if h.is_cuda:
         T = h.numel() // h.shape[-1]
         qkv = h.new_empty(T, wqkv.shape[0]) if qkv is None else qkv
-        if h.dim() == 2 and _lib_pick(T, wqkv.shape[0], wqkv.shape[1]):
-            torch.matmul(h, wqkv.t(), out=qkv)      # hipBLASLt (measured faster) + rope_kv
-            lib().rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
-            return q_out
         lib().qkv_rope(h, wqkv, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
         return q_out
     qkv = ref.gemm(h, wqkv)

@@ -26,38 +26,19 @@ def test_plan_file_shape():
     assert {(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)} <= shapes
     assert {(10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672)} <= shapes
     for s in plan["shapes"]:
-        assert all(c in (-1, 0, 1, 2) for c in s["codes"])
+        assert all(c in (-1, 0, 1, 2, 3, 4, 5) for c in s["codes"])
         # buckets below 256 rows are left to the skinny / 128 kernels
         assert all(c == -1 for c in s["codes"][:3])
         assert all(c >= 0 for c in s["codes"][3:])
-        if "lib" in s:            # hipBLASLt buckets (tools/tune_gemm_lib.py): o, down, qkv only
-            assert (s["N"], s["K"]) in {(4096, 4096), (4096, 14336), (6144, 4096),      # 8B
-                                        (8192, 8192), (8192, 28672), (10240, 8192)}     # 70B
-            assert len(s["lib"]) == len(s["codes"]) and set(s["lib"]) <= {0, 1}
 
 
-def test_lib_pick_follows_plan(tmp_path, monkeypatch):
-    """ops._lib_pick reads the plan's per-bucket "lib" flags; a reload replaces
-    them and MCP_GEMM_LIB=0 (module switch) turns them off."""
-    L = _lib()
-    p = tmp_path / "plan.json"
-    p.write_text(json.dumps({"arch": "gfx950", "mstep": 64, "shapes": [
-        {"N": 4096, "K": 4096, "codes": [-1, -1, -1, 1, 1], "lib": [0, 0, 0, 1, 0]}]}))
-    try:
-        ops._load_gemm_plan(L, str(p))
-        assert ops._lib_pick(256, 4096, 4096) and not ops._lib_pick(257, 4096, 4096)
-        assert not ops._lib_pick(192, 4096, 4096) and not ops._lib_pick(10_000, 4096, 4096)
-        assert not ops._lib_pick(256, 4096, 14336)                 # other shape
-        monkeypatch.setattr(ops, "_LIB_ON", False)
-        assert not ops._lib_pick(256, 4096, 4096)
-        monkeypatch.setattr(ops, "_LIB_ON", True)
-        p.write_text(json.dumps({"arch": "gfx950", "mstep": 64,
-                                 "shapes": [{"N": 4096, "K": 4096, "codes": [-1, -1, -1, 1]}]}))
-        ops._load_gemm_plan(L, str(p))
-        assert not ops._lib_pick(256, 4096, 4096)                  # flags do not leak across loads
-    finally:
-        L.gemm_plan_clear()
-        ops._load_gemm_plan(L)
+def test_no_library_route():
+    """Every GEMM bucket runs on our own kernels: the plan carries no hipBLASLt
+    ("lib") buckets and ops has no library dispatch."""
+    with open(ops.GEMM_PLAN_FILE) as f:
+        plan = json.load(f)
+    assert all("lib" not in s for s in plan["shapes"])
+    assert not hasattr(ops, "_lib_pick") and not hasattr(ops, "_LIB_RES")
 
 
 def test_plan_lookup_buckets():
@@ -83,7 +64,7 @@ def test_plan_lookup_buckets():
         L.gemm_plan_set(4096, 4096, [-1] * 8)                  # replace, not append
         assert L.gemm_plan_lookup(300, 4096, 4096) == -1
         with pytest.raises(Exception):
-            L.gemm_plan_set(4096, 4096, [3])
+            L.gemm_plan_set(4096, 4096, [6])
     finally:
         L.gemm_plan_clear()
         ops._load_gemm_plan(L)

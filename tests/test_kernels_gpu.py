@@ -426,7 +426,9 @@ def test_gemm_256d_agpr(M, N, K):
     X = torch.randn(M, K, device=DEV).bfloat16()
     W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    for v in (49, 50, 51):             # data-parallel, stream-K (last-arriver slab sums), 192-row tiles
+    # data-parallel 256-row tiles, stream-K (last-arriver slab sums), 192-,
+    # 160-, 224- and 128-row tiles
+    for v in (49, 50, 51, 53, 54, 55):
         Y.zero_()
         L.gemm_variant(X, W, Y, v)
         assert rel_err(Y, ref.gemm(X, W)) < 1e-2, v
@@ -441,10 +443,10 @@ def test_gemm_256d_agpr(M, N, K):
     assert rel_err(y, e) < 2e-2
 
 
-@pytest.mark.parametrize("code", [0, 1, 2])
+@pytest.mark.parametrize("code", [0, 1, 2, 3, 4, 5])
 def test_gemm_plan_codes(code):
-    """Every kernel a measured tile plan can name (0 = 128^2, 1 = AGPR 256-row,
-    2 = AGPR 192-row tiles) through the production entry points: plain, residual
+    """Every kernel a measured tile plan can name (0 = 128^2, 1..5 = AGPR
+    256-, 192-, 160-, 224-, 128-row tiles) through the production entry points: plain, residual
     in place, SwiGLU; M not a multiple of any tile height."""
     torch.manual_seed(7)
     L = ops.lib()
@@ -623,35 +625,32 @@ def test_gemm_hybrid_streamk_tail(M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(2600, 4096, 14336), (2560, 4096, 4096), (700, 4096, 4096)])
-def test_residual_gemm_library_buckets(M, N, K):
-    """Residual projections in the plan's hipBLASLt buckets (x += a W^T through
-    addmm_, beta = 1) and the same call on our MFMA residual epilogue
-    (MCP_GEMM_LIB off) both match the fp32 reference."""
+def test_residual_gemm_every_height(M, N, K):
+    """Residual projections (x += a W^T in place, the o / down projections) on
+    the AGPR kernel at every tile height (algo 9..13 = plan codes 1..5) and
+    through the production selector match the fp32 reference."""
     torch.manual_seed(11)
     X = torch.randn(M, K, device=DEV).bfloat16()
     W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     R = torch.randn(M, N, device=DEV).bfloat16()
     exp = X.float() @ W.float().t() + R.float()
-    for on in (True, False):
-        old = ops._LIB_ON
-        ops._LIB_ON = on
-        try:
-            y = R.clone()
-            out = ops.gemm(X, W, R=y, out=y)
-        finally:
-            ops._LIB_ON = old
+    for algo in (-1, 9, 10, 11, 12, 13):
+        y = R.clone()
+        out = ops.gemm(X, W, R=y, out=y, algo=algo)
         assert out.data_ptr() == y.data_ptr()
-        assert rel_err(out, exp) < 1e-2
+        assert rel_err(out, exp) < 1e-2, algo
 
 
 @pytest.mark.parametrize("M", [1024, 2600])
-def test_qkv_rope_library_buckets(M):
-    """QKV through the library route (hipBLASLt GEMM + rope_kv) and through our
-    fused path give the same q / K / V rows as the fp32 reference."""
+def test_qkv_rope_fused_every_height(M):
+    """QKV + RoPE + paged K/V write fused in the AGPR epilogue (EPI 3) at every
+    tile height the plan can pick gives the fp32 reference's q / K / V rows."""
     torch.manual_seed(12)
+    L = ops.lib()
     Hq, Hkv, D, H, BS = 32, 8, 128, 4096, 64
+    N = (Hq + 2 * Hkv) * D
     X = torch.randn(M, H, device=DEV).bfloat16()
-    W = (torch.randn((Hq + 2 * Hkv) * D, H, device=DEV) / math.sqrt(H)).bfloat16()
+    W = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
     nb = (M + BS - 1) // BS + 1
     pos = torch.randint(0, 8000, (M,), device=DEV, dtype=torch.int32)
     slots = torch.randperm(nb * BS, device=DEV)[:M].to(torch.int32)
@@ -659,15 +658,15 @@ def test_qkv_rope_library_buckets(M):
     qkv = ref.gemm(X, W).cpu()
     qr, kr, vr = (torch.zeros(M, Hq, D), torch.zeros(nb, Hkv, BS, D), torch.zeros(nb, Hkv, BS, D))
     ref.rope_kv(qkv, pos.cpu(), slots.cpu(), cs.cpu(), qr, kr, vr, Hq, Hkv, D)
-    for on in (True, False):
-        q = torch.empty(M, Hq, D, device=DEV, dtype=torch.bfloat16)
-        kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
-        vc = torch.zeros_like(kc)
-        old = ops._LIB_ON
-        ops._LIB_ON = on
-        try:
+    try:
+        for code in (1, 2, 3, 4, 5):
+            L.gemm_plan_set(N, H, [code] * 64)
+            q = torch.empty(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+            kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+            vc = torch.zeros_like(kc)
             ops.qkv_rope(X, W, pos, slots, cs, q, kc, vc, Hq, Hkv, D)
-        finally:
-            ops._LIB_ON = old
-        assert rel_err(q.cpu(), qr) < 1e-2
-        assert rel_err(kc.cpu(), kr) < 1e-2 and rel_err(vc.cpu(), vr) < 1e-2
+            assert rel_err(q.cpu(), qr) < 1e-2, code
+            assert rel_err(kc.cpu(), kr) < 1e-2 and rel_err(vc.cpu(), vr) < 1e-2, code
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)

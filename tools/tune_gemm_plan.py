@@ -2,9 +2,11 @@
 it where ops.lib() loads it (ops/gemm_plan_gfx950.json).
 
 For every (N, K) weight shape and every 64-row M bucket (timed at the bucket's
-top row, which has the tile counts of the whole bucket) the three MFMA kernels
-are timed interleaved (3 rounds x 10 launches, min): code 0 = 128^2 kernel,
-1 = AGPR kernel with 256-row tiles, 2 = AGPR kernel with 192-row tiles.  The
+top row, which has the tile counts of the whole bucket) our MFMA kernels are
+timed interleaved (3 rounds x 10 launches, min): code 0 = 128^2 kernel, codes
+1-5 = the AGPR kernel (gemm256d.hip) with 256-, 192-, 160-, 224- and 128-row
+tiles.  The residual projections (o, down: N = H) are timed with the
+production residual epilogue (y = x W^T + y), the others as plain GEMMs.  The
 fastest wins unless it beats the runner-up with the smaller code by < 1 %
 (hysteresis keeps the plan stable against timing noise).  Code 0 is timed at
 split-K 1 / 2 / 4 / 8 (2 / 4 / 8 below 129 rows, where "no split" means the
@@ -16,6 +18,9 @@ fastest is recorded per bucket ("flex", -1 = none) when it beats the code
 path by > 1 %.  Buckets up to 2048 rows are timed with COLD weights (each
 launch reads the next of several weight copies, > 1.5 GB: a serving step
 streams the whole model, nothing stays in the 256 MB Infinity Cache).
+
+hipBLASLt (``torch.matmul`` / ``addmm_``) is timed beside them as a yardstick
+only ("ref_us": [ours, hipBLASLt] per bucket); nothing dispatches to it.
 
     python tools/tune_gemm_plan.py [out.json] [m_max] [8b|70b]
 
@@ -55,15 +60,23 @@ dev = "cuda"
 s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
-def run(code, X, W, Y, split=-1):
-    if code == 3:                          # flex tile, split = candidate
-        L.gemm(X, W, Y, None, 16 + split)
+RESIDUAL = set()                           # (N, K) timed with the residual epilogue
+
+
+def run(code, X, W, Y, split=-1, R=None):
+    if code == "flex":                     # flex tile, split = candidate
+        L.gemm(X, W, Y, R, 16 + split)
+    elif code == "lib":                    # hipBLASLt yardstick (never dispatched)
+        if R is not None:
+            Y.addmm_(X, W.t())
+        else:
+            torch.matmul(X, W.t(), out=Y)
     elif code == 0:
         L.gemm_splitk_force(split)
-        L.gemm(X, W, Y, None, 0)
+        L.gemm(X, W, Y, R, 0)
         L.gemm_splitk_force(-1)
-    else:
-        L.gemm_variant(X, W, Y, 49 if code == 1 else 51)
+    else:                                  # AGPR kernel at the height of plan code 1..5
+        L.gemm(X, W, Y, R, 8 + code)
 
 
 def time_ms(fn, Ws, reps=10):
@@ -77,10 +90,13 @@ def time_ms(fn, Ws, reps=10):
 
 
 result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
-          "mstep": MSTEP, "codes": "0=128x128, 1=AGPR 256-row tiles, 2=AGPR 192-row tiles",
+          "mstep": MSTEP,
+          "codes": "0=128x128, 1..5=AGPR 256/192/160/224/128-row tiles",
           "splits": "measured split-K of code 0 per bucket (0 = the rule)",
           "flex": "measured flex tile per bucket (gemm_flex.hip candidate, +32 = 4-stage; -1 = none)",
+          "ref_us": "[ours, hipBLASLt] us per bucket, yardstick only",
           "generated": time.strftime("%Y-%m-%d"), "shapes": []}
+RESIDUAL.update({(4096, 4096), (4096, 14336), (8192, 8192), (8192, 28672)})
 t0 = time.time()
 for (N, K) in SHAPES:
     Xf = torch.randn(m_max, K, device=dev).bfloat16()
@@ -88,28 +104,37 @@ for (N, K) in SHAPES:
     Wcold = [W] + [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
                    for _ in range(int(1.5e9 // (N * K * 2)))]
     Yf = torch.empty(m_max, N, device=dev, dtype=torch.bfloat16)
-    codes, tf, splits, flex = [], [], [], []
+    Rf = torch.randn(m_max, N, device=dev).bfloat16() if (N, K) in RESIDUAL else None
+    codes, tf, splits, flex, ref = [], [], [], [], []
     for b in range(m_max // MSTEP):
         M = (b + 1) * MSTEP
         X, Y = Xf[:M], Yf[:M]
+        # residual shapes: y = x W^T + y in place, as the model runs them
+        R = Y if Rf is not None else None
+        if R is not None:
+            Y.copy_(Rf[:M])
         Ws = Wcold if (M <= FLEX_MAX or COLD_ALL) else [W]
         # code-0 candidates: (0, split)
         svals = ([2, 4, 8] if M <= 128 else [1, 2, 4, 8]) if M <= M_SPLIT_MAX else [-1]
         cands = [(0, sv) for sv in svals]
         if M >= M_MIN and K % 128 == 0 and N % 256 == 0:
-            cands += [(1, -1), (2, -1)]
+            cands += [(c, -1) for c in (1, 2, 3, 4, 5)]
         fl = []
         if FLEX_MIN <= M <= FLEX_MAX and N not in SWIGLU_N:   # gate|up runs the SwiGLU epilogue
-            fl = [(3, f) for f in list(range(NFLEX)) + [32 + f for f in range(NFLEX)]]
-        best = {c: float("inf") for c in cands + fl}
+            fl = [("flex", f) for f in list(range(NFLEX)) + [32 + f for f in range(NFLEX)]]
+        allc = cands + fl + [("lib", -1)]
+        best = {c: float("inf") for c in allc}
         for _ in range(3):
-            for c in cands + fl:
-                best[c] = min(best[c], time_ms(lambda w, c=c: run(c[0], X, w, Y, c[1]), Ws))
+            for c in allc:
+                best[c] = min(best[c], time_ms(lambda w, c=c: run(c[0], X, w, Y, c[1], R), Ws))
+        lib_ms = best.pop(("lib", -1))
         c0 = min((c for c in cands if c[0] == 0), key=lambda c: best[c])
         splits.append(max(c0[1], 0))
         ref_ms = min(best[c] for c in cands)
         fbest = min(fl, key=lambda c: best[c]) if fl else None
         flex.append(fbest[1] if fbest and best[fbest] * 1.01 < ref_ms else -1)
+        ours_ms = min(ref_ms, best[fbest]) if fbest else ref_ms
+        ref.append([round(ours_ms * 1e3, 1), round(lib_ms * 1e3, 1)])
         if M < M_MIN:
             codes.append(-1)
             tf.append({f"0s{c[1]}": round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
@@ -124,10 +149,10 @@ for (N, K) in SHAPES:
         codes.append(win)
         tf.append({str(c): round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
     result["shapes"].append({"N": N, "K": K, "codes": codes, "splits": splits, "flex": flex,
-                             "tflops": tf})
+                             "tflops": tf, "ref_us": ref})
     print(json.dumps({"N": N, "K": K, "codes": codes, "flex": flex, "s": round(time.time() - t0, 1)}),
           flush=True)
-    del Xf, W, Yf, Wcold
+    del Xf, W, Yf, Wcold, Rf
 with open(out_path, "w") as f:
     json.dump(result, f, indent=None, separators=(",", ":"))
     f.write("\n")
