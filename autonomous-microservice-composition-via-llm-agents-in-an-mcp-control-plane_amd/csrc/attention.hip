@@ -83,7 +83,123 @@ struct AttnArgs {
   // block id % 8 (the XCD) is the kv head when Hkv = 8: each XCD's L2 then
   // holds one head's prefix K/V (352 KiB) instead of all eight
   int head_major;
+  // MIXED split launch (split-KV steps): blocks [0, nwork4) run the 4-wave
+  // list (work_seq / work_q0), blocks [nwork4, ...) the 1-wave list
+  // (work_seq1 / work_q01) as 4-wave blocks whose waves 1-3 hold no rows;
+  // split_cnt (per block x kv head arrival tickets, zero between launches):
+  // the last split to arrive merges every split's partial (no combine kernel)
+  const int* work_seq1;
+  const int* work_q01;
+  int nwork4;
+  int* split_cnt;
 };
+
+// Fused split-KV combine (MIXED launches).  Every split writes its
+// normalised fp32 partial O and its log2-sum-exp write-through (sc1 buffer
+// stores), drains them, and lane 0 takes the (block, kv head) ticket; the
+// split whose ticket is the last merges all partials with LSE weights (sc1
+// loads: the hand-off of MI355X_MICROARCH.md "Valid forms", row 1 - the same
+// protocol as gemm_stream.hip's split-K) and writes the bf16 rows.  Split 0
+// folds in the cascade prefix partial exactly as the unfused KSPLIT path.
+// Every wave reaches both barriers (rows without a query are predicated off,
+// never returned early).
+template <int NW, int G>
+DEV void split_fused_epilogue(const AttnArgs& a, f32x4 (&o)[8], float m_run, float l_tot,
+                              bool qvalid, size_t row, int s, int fq, bf16* smem) {
+  const int nz = gridDim.z, z = blockIdx.z;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  float lse = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
+  const bool merge_pre = a.pre_o != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0;
+  float wa = 0.f, wb = 1.f;
+  if (z == 0 && merge_pre && qvalid) {
+    const float lse_a = a.pre_lse[row];
+    const float mx = fmaxf(lse_a, lse);
+    const float ea = exp2f(lse_a - mx), eb = lse == -INFINITY ? 0.f : exp2f(lse - mx);
+    wa = ea / (ea + eb);
+    wb = eb / (ea + eb);
+    lse = mx + __log2f(ea + eb);
+  }
+  const auto rso = __builtin_amdgcn_make_buffer_rsrc(a.split_o, (short)0, 0x7FFFFFFF, 0x00020000);
+  const auto rsl = __builtin_amdgcn_make_buffer_rsrc(a.split_lse, (short)0, 0x7FFFFFFF, 0x00020000);
+  if (qvalid) {
+    const bf16* pp = (z == 0 && merge_pre) ? a.pre_o + row * D + 4 * fq : nullptr;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      f32x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = o[dt][r] * inv * wb;
+      if (pp) {
+        const bf16x4 pa = *reinterpret_cast<const bf16x4*>(pp + dt * 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] += (float)pa[r] * wa;
+      }
+      o[dt] = w;                                      // this split's partial, kept for the merge
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(u32x4, w), rso,
+          (unsigned)((((size_t)z * a.rows + row) * D + 4 * fq + 16 * dt) * 4), 0, 16);
+    }
+    if (fq == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lse), rsl,
+                                            (unsigned)(((size_t)z * a.rows + row) * 4), 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                   // every wave's partial is out
+  int* flag = reinterpret_cast<int*>(smem);          // the K/V ring is free after the loop
+  if (threadIdx.x == 0) {
+    int* cnt = a.split_cnt + (size_t)blockIdx.x * gridDim.y + blockIdx.y;
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == nz - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag || !qvalid) return;
+  // ---- last arriver: LSE-weighted sum over the splits, this lane's row
+  float mx = lse;
+  for (int j = 0; j < nz; ++j) {
+    if (j == z) continue;
+    const float lj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        rsl, (unsigned)(((size_t)j * a.rows + row) * 4), 0, 16));
+    mx = fmaxf(mx, lj);
+  }
+  const float mu = mx == -INFINITY ? 0.f : mx;
+  // summed in split order whichever split arrives last (deterministic output);
+  // this split's own partial comes from registers
+  float den = 0.f;
+  f32x4 acc[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < nz; ++j) {
+    float lj = lse;
+    f32x4 pj[8];
+    if (j == z) {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) pj[dt] = o[dt];
+    } else {
+      lj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+          rsl, (unsigned)(((size_t)j * a.rows + row) * 4), 0, 16));
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        pj[dt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+            rso, (unsigned)((((size_t)j * a.rows + row) * D + 4 * fq + 16 * dt) * 4), 0, 16));
+    }
+    const float wj = lj == -INFINITY ? 0.f : exp2f(lj - mu);   // 0 for empty splits
+    den += wj;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) acc[dt] += pj[dt] * wj;
+  }
+  const float dinv = den > 0.f ? 1.f / den : 0.f;
+  if (a.own_lse != nullptr && fq == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0)
+    a.own_lse[row] = den > 0.f ? mu + __log2f(den) : -INFINITY;
+  bf16* op = a.out + row * D + 4 * fq;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    bf16x4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[dt][r] * dinv);
+    *reinterpret_cast<bf16x4*>(op + dt * 16) = w;
+  }
+}
 
 // MODE 0: per (sequence, q-tile) work item, causal over keys
 //         [kv_begin[s], ctx_len[s]); merges the prefix partial when present.
@@ -91,9 +207,11 @@ struct AttnArgs {
 //         sequence that shares one registry prefix, 16-token tiles that mix
 //         sequences (they attend to the same K/V), no mask (every query sits
 //         after the prefix).  Writes normalised O and its LSE.
-template <int NW, int G, int MODE, int NBUF_ = 0, bool KSPLIT = false, int WPE = 1>
+template <int NW, int G, int MODE, int NBUF_ = 0, bool KSPLIT = false, int WPE = 1,
+          bool MIXED = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void attn_kernel(const AttnArgs a) {
+  static_assert(!MIXED || (NW == 4 && MODE == 0 && KSPLIT), "mixed lists: 4-wave split items");
   constexpr int TPW = 16 / G;                 // tokens per wave
   constexpr int QT = NW * TPW;                // tokens per work item
   constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
@@ -133,16 +251,25 @@ void attn_kernel(const AttnArgs a) {
       ntiles = span * (z + 1) / nz;
     }
   } else {
-    s = a.work_seq[blockIdx.x];
-    const int q0 = a.work_q0[blockIdx.x];
+    int q0, item_waves = NW;
+    if constexpr (MIXED) {
+      const int b = blockIdx.x;
+      const bool wide = b < a.nwork4;
+      s = wide ? a.work_seq[b] : a.work_seq1[b - a.nwork4];
+      q0 = wide ? a.work_q0[b] : a.work_q01[b - a.nwork4];
+      item_waves = wide ? NW : 1;
+    } else {
+      s = a.work_seq[blockIdx.x];
+      q0 = a.work_q0[blockIdx.x];
+    }
     qs = a.q_start[s];
     ql = a.q_len[s];
     cl = a.ctx_len[s];
     bt = a.block_table + (size_t)s * a.max_blocks;
     tok = q0 + wave * TPW + fr / G;                       // index inside the query span
-    qvalid = tok < ql;
+    qvalid = tok < ql && wave < item_waves;
     qpos = cl - ql + tok;
-    const int last_tok = min(q0 + QT, ql) - 1;
+    const int last_tok = min(q0 + item_waves * TPW, ql) - 1;
     const int kv_end = cl - ql + last_tok + 1;
     ntiles = (kv_end + KT - 1) / KT;
     kt0 = a.kv_begin ? a.kv_begin[s] / KT : 0;
@@ -268,6 +395,11 @@ void attn_kernel(const AttnArgs a) {
   // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + r]
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
+  if constexpr (MIXED) {
+    split_fused_epilogue<NW, G>(a, o, m_run, l_tot, qvalid, (size_t)(qs + (qvalid ? tok : 0)) * Hq + head,
+                                s, fq, smem);
+    return;
+  }
   if (!qvalid) return;
   const size_t row = (size_t)(qs + tok) * Hq + head;
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
@@ -505,6 +637,18 @@ void attn_dispatch(int nw, const AttnArgs& a, int nwork, hipStream_t s, int nspl
     attn_kernel<4, G, 0><<<grid, 256, 0, s>>>(a);
 }
 
+// per-device arrival tickets of the fused split-KV launch (zeroed once here,
+// at library load - never inside a graph capture; each last arriver re-arms
+// its own ticket)
+constexpr int SPLIT_CNT_MAX = 1 << 16;
+int* g_split_cnt[64] = {};
+
+int* split_counters() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return g_split_cnt[d & 63];
+}
+
 int prefix_nw() {
   static int nw = 0;
   if (!nw) {
@@ -546,6 +690,18 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
 }  // namespace
 
 int attn_tokens_per_item(int nw, int group) { return nw * (16 / group); }
+
+int attn_split_init() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  if (g_split_cnt[d & 63]) return 0;
+  int* p = nullptr;
+  if (hipMalloc(&p, SPLIT_CNT_MAX * sizeof(int)) != hipSuccess) return 1;
+  if (hipMemset(p, 0, SPLIT_CNT_MAX * sizeof(int)) != hipSuccess) return 1;
+  (void)hipDeviceSynchronize();
+  g_split_cnt[d & 63] = p;
+  return 0;
+}
 
 #define ATTN_SWITCH_G(G_, CALL)                     \
   switch (G_) {                                     \
@@ -591,6 +747,58 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
   a.rows = rows;
   a.own_lse = own_lse;
   ATTN_SWITCH_G(Hq / Hkv, attn_dispatch<GG>(nw, a, nwork, s, nsplit))
+  return 0;
+}
+
+// Split-KV step in ONE launch: both work lists (4-wave items, then 1-wave
+// items run as 4-wave blocks) x Hkv x nsplit, the combine fused in (last
+// arriver per item and kv head).  Returns nonzero (caller falls back to the
+// per-list launches + attn_split_combine) when the tickets or the 2 GiB
+// buffer range of the partials do not cover the launch.
+int launch_paged_attention_mixed(const void* q, const void* k_cache, const void* v_cache,
+                                 void* out, const int* q_start, const int* q_len,
+                                 const int* ctx_len, const int* block_table, int max_blocks,
+                                 const int* work_seq4, const int* work_q04, int nwork4,
+                                 const int* work_seq1, const int* work_q01, int nwork1, int Hq,
+                                 int Hkv, int head_dim, float scale, const int* kv_begin,
+                                 const void* pre_o, const float* pre_lse, hipStream_t s,
+                                 int nsplit, float* split_o, float* split_lse, int rows,
+                                 float* own_lse) {
+  if (head_dim != D) return 1;
+  if (nsplit < 2 || !split_o || !split_lse) return 4;
+  const int nitems = nwork4 + nwork1;
+  if (nitems <= 0) return 0;
+  int* cnt = split_counters();
+  if (!cnt || (long long)nitems * Hkv > SPLIT_CNT_MAX) return 5;
+  if ((long long)nsplit * rows * D * 4 >= (1ll << 31)) return 6;
+  AttnArgs a{};
+  a.q = (const bf16*)q;
+  a.kc = (const bf16*)k_cache;
+  a.vc = (const bf16*)v_cache;
+  a.out = (bf16*)out;
+  a.q_start = q_start;
+  a.q_len = q_len;
+  a.ctx_len = ctx_len;
+  a.block_table = block_table;
+  a.max_blocks = max_blocks;
+  a.work_seq = work_seq4;
+  a.work_q0 = work_q04;
+  a.work_seq1 = work_seq1;
+  a.work_q01 = work_q01;
+  a.nwork4 = nwork4;
+  a.split_cnt = cnt;
+  a.Hq = Hq;
+  a.Hkv = Hkv;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.kv_begin = kv_begin;
+  a.pre_o = (const bf16*)pre_o;
+  a.pre_lse = pre_lse;
+  a.split_o = split_o;
+  a.split_lse = split_lse;
+  a.rows = rows;
+  a.own_lse = own_lse;
+  const dim3 grid(nitems, Hkv, nsplit);
+  ATTN_SWITCH_G(Hq / Hkv, (attn_kernel<4, GG, 0, 2, true, 1, true><<<grid, 256, 0, s>>>(a)))
   return 0;
 }
 

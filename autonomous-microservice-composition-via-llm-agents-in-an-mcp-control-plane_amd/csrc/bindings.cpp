@@ -293,6 +293,69 @@ void paged_attention(const at::Tensor& q, const at::Tensor& k_cache, const at::T
   check_launch("paged_attention");
 }
 
+// split-KV step as ONE launch (both work lists, combine fused); false = not
+// launched (ticket / range limits), the caller runs the per-list path
+bool paged_attention_mixed(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                           at::Tensor& out, const at::Tensor& q_start, const at::Tensor& q_len,
+                           const at::Tensor& ctx_len, const at::Tensor& block_table,
+                           const at::Tensor& work_seq4, const at::Tensor& work_q04,
+                           const at::Tensor& work_seq1, const at::Tensor& work_q01, double scale,
+                           int64_t nsplit, at::Tensor& split_o, at::Tensor& split_lse,
+                           const c10::optional<at::Tensor>& kv_begin,
+                           const c10::optional<at::Tensor>& pre_o,
+                           const c10::optional<at::Tensor>& pre_lse,
+                           const c10::optional<at::Tensor>& own_lse) {
+  CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
+  CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
+  CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq4); CHECK_I32_TENSOR(work_q04);
+  CHECK_I32_TENSOR(work_seq1); CHECK_I32_TENSOR(work_q01);
+  TORCH_CHECK(q.dim() == 3, "q must be [T, Hq, D]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64, "cache block size must be 64");
+  const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
+  TORCH_CHECK(block_table.dim() == 2, "block_table [S, max_blocks]");
+  TORCH_CHECK(work_seq4.numel() == work_q04.numel() && work_seq1.numel() == work_q01.numel(),
+              "work lists");
+  TORCH_CHECK(nsplit >= 2, "mixed launch is the split-KV path");
+  TORCH_CHECK(split_o.scalar_type() == at::kFloat && split_o.is_contiguous() &&
+              split_o.numel() >= nsplit * q.numel(), "split_o [nsplit, T, Hq, D] f32");
+  TORCH_CHECK(split_lse.scalar_type() == at::kFloat && split_lse.is_contiguous() &&
+              split_lse.numel() >= nsplit * q.size(0) * Hq, "split_lse [nsplit, T, Hq] f32");
+  const int* kb = nullptr;
+  const void* po = nullptr;
+  const float* pl = nullptr;
+  float* ol = nullptr;
+  if (kv_begin.has_value()) {
+    CHECK_I32_TENSOR((*kv_begin));
+    TORCH_CHECK(kv_begin->numel() == q_len.numel(), "kv_begin [S]");
+    kb = kv_begin->data_ptr<int>();
+    if (own_lse.has_value()) {
+      TORCH_CHECK(own_lse->scalar_type() == at::kFloat && own_lse->is_contiguous() &&
+                      own_lse->numel() == q.size(0) * Hq, "own_lse [T, Hq] f32");
+      ol = own_lse->data_ptr<float>();
+    } else {
+      TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "kv_begin needs pre_o / pre_lse or own_lse");
+      CHECK_BF16_TENSOR((*pre_o));
+      TORCH_CHECK(pre_o->sizes() == q.sizes(), "pre_o shape");
+      TORCH_CHECK(pre_lse->scalar_type() == at::kFloat && pre_lse->numel() == q.size(0) * Hq, "pre_lse [T, Hq]");
+      po = pre_o->data_ptr();
+      pl = pre_lse->data_ptr<float>();
+    }
+  }
+  const int rc = launch_paged_attention_mixed(
+      q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
+      q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
+      block_table.size(1), work_seq4.data_ptr<int>(), work_q04.data_ptr<int>(), work_seq4.numel(),
+      work_seq1.data_ptr<int>(), work_q01.data_ptr<int>(), work_seq1.numel(), Hq, Hkv, D,
+      (float)scale, kb, po, pl, stream(), (int)nsplit, split_o.data_ptr<float>(),
+      split_lse.data_ptr<float>(), (int)(q.size(0) * Hq), ol);
+  TORCH_CHECK(rc != 1 && rc != 3 && rc != 4, "paged_attention_mixed: unsupported config (code ", rc, ")");
+  if (rc != 0) return false;
+  check_launch("paged_attention_mixed");
+  return true;
+}
+
 void cascade_merge(at::Tensor& out, const at::Tensor& own_lse, const at::Tensor& pre_o,
                    const at::Tensor& pre_lse, int64_t pre_tokens,
                    const c10::optional<at::Tensor>& pre_dims) {
@@ -529,6 +592,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scale"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
         py::arg("pre_lse") = py::none(), py::arg("nsplit") = 1, py::arg("split_o") = py::none(),
         py::arg("split_lse") = py::none(), py::arg("own_lse") = py::none());
+  m.def("paged_attention_mixed", &paged_attention_mixed, py::arg("q"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("out"), py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"),
+        py::arg("block_table"), py::arg("work_seq4"), py::arg("work_q04"), py::arg("work_seq1"),
+        py::arg("work_q01"), py::arg("scale"), py::arg("nsplit"), py::arg("split_o"),
+        py::arg("split_lse"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
+        py::arg("pre_lse") = py::none(), py::arg("own_lse") = py::none(),
+        "split-KV attention step in one launch (both work lists, combine fused); False = not launched");
+  m.def("attn_split_init", &attn_split_init, "allocate the fused split-KV tickets (outside graph capture)");
   m.def("cascade_merge", &cascade_merge, py::arg("out"), py::arg("own_lse"), py::arg("pre_o"),
         py::arg("pre_lse"), py::arg("pre_tokens"), py::arg("pre_dims") = py::none());
   m.def("prefix_attention", &prefix_attention, py::arg("q"), py::arg("k_cache"), py::arg("v_cache"),

@@ -111,6 +111,16 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            const float* pre_lse, hipStream_t s, int nsplit = 1,
                            float* split_o = nullptr, float* split_lse = nullptr, int rows = 0,
                            float* own_lse = nullptr);
+int attn_split_init();
+int launch_paged_attention_mixed(const void* q, const void* k_cache, const void* v_cache,
+                                 void* out, const int* q_start, const int* q_len,
+                                 const int* ctx_len, const int* block_table, int max_blocks,
+                                 const int* work_seq4, const int* work_q04, int nwork4,
+                                 const int* work_seq1, const int* work_q01, int nwork1, int Hq,
+                                 int Hkv, int head_dim, float scale, const int* kv_begin,
+                                 const void* pre_o, const float* pre_lse, hipStream_t s,
+                                 int nsplit, float* split_o, float* split_lse, int rows,
+                                 float* own_lse);
 int launch_cascade_merge(void* out, const float* own_lse, const void* pre_o, const float* pre_lse,
                          int pre_tokens, const int* pre_dims, int Hq, int head_dim, hipStream_t s);
 int launch_prefix_attention(const void* q, const void* k_cache, const void* v_cache, void* out,

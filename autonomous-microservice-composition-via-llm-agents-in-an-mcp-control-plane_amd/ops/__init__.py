@@ -43,6 +43,8 @@ def lib():
             # fp32 split-K partials of small-M projections (gemm.hip); allocated
             # here, never inside a hipGraph capture
             mod.gemm_splitk_init(int(os.environ.get("MCP_GEMM_SPLITK_MB", "256")) << 20)
+        if torch.cuda.is_available() and hasattr(mod, "attn_split_init"):
+            mod.attn_split_init()          # fused split-KV tickets (outside any capture)
         _LIB = mod
     return _LIB
 
@@ -197,6 +199,9 @@ def rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D):
 
 
 _SIDE = {}
+# split-KV steps as one launch with the combine fused (attention.hip MIXED);
+# MCP_ATTN_MIXED=0 keeps a launch + combine per work list
+_MIXED_SPLIT = os.environ.get("MCP_ATTN_MIXED", "1") == "1"
 
 
 def _side_stream(device):
@@ -276,6 +281,23 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
                                    meta.pre_tokens, scale, pre_dims=pre_dims, **kw_split)
                 kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         ns = int(getattr(meta, "kv_splits", 1))
+        if ns > 1 and _MIXED_SPLIT and hasattr(L, "paged_attention_mixed"):
+            # split-KV step (few sequences, long own contexts: config 2 / low
+            # QPS) in ONE launch: both work lists, the combine fused in
+            lists = {nw: (ws, wq) for nw, ws, wq in meta.work_lists()}
+            e = torch.empty(0, dtype=torch.int32, device=q.device)
+            ws4, wq4 = lists.get(4, (e, e))
+            ws1, wq1 = lists.get(1, (e, e))
+            so = torch.empty(ns, *q.shape, device=q.device, dtype=torch.float32)
+            sl = torch.empty(ns, q.shape[0], q.shape[1], device=q.device, dtype=torch.float32)
+            if L.paged_attention_mixed(q, k_cache, v_cache, out, meta.q_start, meta.q_len,
+                                       meta.ctx_len, meta.block_table, ws4, wq4, ws1, wq1, scale,
+                                       ns, so, sl, **kw):
+                if concurrent:
+                    main.wait_stream(side)
+                    L.cascade_merge(out, kw["own_lse"], pre_o, pre_lse, meta.pre_tokens,
+                                    pre_dims=pre_dims)
+                return out
         for nw, ws, wq in meta.work_lists():
             if ns > 1:
                 # split-KV (K6): fp32 partials + LSE per split, merged by a second kernel

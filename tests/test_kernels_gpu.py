@@ -204,6 +204,24 @@ def test_paged_attention_split_kv_uneven():
         assert rel_err(out, exp) < 2e-2
 
 
+@pytest.mark.parametrize("mixed", [True, False])
+def test_paged_attention_split_fused_vs_per_list(mixed, monkeypatch):
+    """Split-KV step as ONE launch (both work lists, last-arriver combine fused,
+    ops._MIXED_SPLIT) and as per-list launches + attn_split_combine: both match
+    fp32, and repeated launches re-arm the arrival tickets (same output)."""
+    monkeypatch.setattr(ops, "_MIXED_SPLIT", mixed)
+    q_lens, ctx_lens = [1, 3, 9, 70, 2], [5000, 65, 900, 700, 1200]
+    outs = []
+    for _ in range(3):
+        out, exp = _attn_case(q_lens, ctx_lens, 32, 8, seed=9, kv_splits=6)
+        assert rel_err(out, exp) < 2e-2
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    for Hq, Hkv in ((8, 1), (64, 8)):             # GQA groups 8 (70B TP=8 / TP=1)
+        out, exp = _attn_case([1, 5], [3000, 800], Hq, Hkv, seed=10, kv_splits=4)
+        assert rel_err(out, exp) < 2e-2
+
+
 def test_paged_attention_spike():
     # a single large score forces the online-softmax rescale path (rule 26)
     out, exp = _attn_case([40], [300], 32, 8, seed=3)
