@@ -154,35 +154,29 @@ DEV void split_fused_epilogue(const AttnArgs& a, f32x4 (&o)[8], float m_run, flo
   }
   __syncthreads();
   if (!*flag || !qvalid) return;
-  // ---- last arriver: LSE-weighted sum over the splits, this lane's row
-  float mx = lse;
-  for (int j = 0; j < nz; ++j) {
-    if (j == z) continue;
-    const float lj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-        rsl, (unsigned)(((size_t)j * a.rows + row) * 4), 0, 16));
-    mx = fmaxf(mx, lj);
-  }
+  // ---- last arriver: LSE-weighted sum over the splits, this lane's row.
+  //      Every split (its own too) is read back from the workspace, in split
+  //      order - deterministic whichever split arrives last - with the loads
+  //      of 8 (LSE) / 4 (O) splits in flight instead of one L2 round trip each
+  float mx = -INFINITY;
+#pragma unroll 8
+  for (int j = 0; j < nz; ++j)
+    mx = fmaxf(mx, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                       rsl, (unsigned)(((size_t)j * a.rows + row) * 4), 0, 16)));
   const float mu = mx == -INFINITY ? 0.f : mx;
-  // summed in split order whichever split arrives last (deterministic output);
-  // this split's own partial comes from registers
   float den = 0.f;
   f32x4 acc[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
   for (int j = 0; j < nz; ++j) {
-    float lj = lse;
+    const float lj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        rsl, (unsigned)(((size_t)j * a.rows + row) * 4), 0, 16));
     f32x4 pj[8];
-    if (j == z) {
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) pj[dt] = o[dt];
-    } else {
-      lj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-          rsl, (unsigned)(((size_t)j * a.rows + row) * 4), 0, 16));
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
-        pj[dt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-            rso, (unsigned)((((size_t)j * a.rows + row) * D + 4 * fq + 16 * dt) * 4), 0, 16));
-    }
+    for (int dt = 0; dt < 8; ++dt)
+      pj[dt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+          rso, (unsigned)((((size_t)j * a.rows + row) * D + 4 * fq + 16 * dt) * 4), 0, 16));
     const float wj = lj == -INFINITY ? 0.f : exp2f(lj - mu);   // 0 for empty splits
     den += wj;
 #pragma unroll

@@ -42,6 +42,24 @@ void check_launch(const char* op) {
 #define CHECK_BF16_TENSOR(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_BF16(t)
 #define CHECK_I32_TENSOR(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_I32(t)
 
+// fused RMSNorm operands (kernels.h NormEpi): ss_out [M] int64 += the rows'
+// sums of squares (residual GEMMs); ss_in [M] int64: rows scaled by
+// rsqrt(ss_in / K + eps) (the GEMMs consuming the normed rows)
+NormEpi make_norm_epi(int M, int K, const c10::optional<at::Tensor>& ss_out,
+                      const c10::optional<at::Tensor>& ss_in, double eps) {
+  NormEpi ne;
+  for (const auto* t : {&ss_out, &ss_in}) {
+    if (!t->has_value()) continue;
+    CHECK_DEV((**t)); CHECK_CONTIG((**t));
+    TORCH_CHECK((*t)->scalar_type() == at::kLong && (*t)->numel() >= M, "ss buffers: int64 [M]");
+  }
+  if (ss_out.has_value()) ne.ss_out = reinterpret_cast<unsigned long long*>(ss_out->data_ptr<int64_t>());
+  if (ss_in.has_value()) ne.ss_in = reinterpret_cast<const unsigned long long*>(ss_in->data_ptr<int64_t>());
+  ne.inv_h = 1.f / (float)K;
+  ne.eps = (float)eps;
+  return ne;
+}
+
 void rmsnorm(const at::Tensor& x, const at::Tensor& w, at::Tensor& out, double eps) {
   CHECK_BF16_TENSOR(x); CHECK_BF16_TENSOR(w); CHECK_BF16_TENSOR(out);
   const int H = x.size(-1);
@@ -101,7 +119,8 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slo
 // AGPR kernel serves the shape, else GEMM into ``qkv`` (scratch) + rope_kv
 void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const at::Tensor& pos,
               const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& q_out,
-              at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D) {
+              at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D,
+              const c10::optional<at::Tensor>& ss_in, double norm_eps) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(qkv);
   CHECK_I32_TENSOR(pos); CHECK_I32_TENSOR(slots);
   CHECK_BF16_TENSOR(q_out); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache);
@@ -121,12 +140,22 @@ void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const a
   RopeArgs ra{pos.data_ptr<int>(), slots.data_ptr<int>(), cos_sin.data_ptr<float>(),
               q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv,
               (int)k_cache.size(2)};
+  NormEpiScope scope(make_norm_epi(M, K, c10::nullopt, ss_in, norm_eps));
   launch_qkv_rope(X.data_ptr(), W.data_ptr(), qkv.data_ptr(), M, N, K, (int)D, ra, stream());
   check_launch("qkv_rope");
 }
 
+void row_sumsq(const at::Tensor& x, at::Tensor& ss) {
+  CHECK_BF16_TENSOR(x); CHECK_DEV(ss); CHECK_CONTIG(ss);
+  const int H = x.size(-1), T = x.numel() / H;
+  TORCH_CHECK(H % 8 == 0 && ss.scalar_type() == at::kLong && ss.numel() >= T, "row_sumsq shapes");
+  launch_row_sumsq(x.data_ptr(), reinterpret_cast<unsigned long long*>(ss.data_ptr<int64_t>()), T, H,
+                   stream());
+  check_launch("row_sumsq");
+}
+
 void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::optional<at::Tensor>& R,
-          int64_t algo) {
+          int64_t algo, const c10::optional<at::Tensor>& ss_out) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
   const int K = X.size(-1);
   const int M = X.numel() / K;
@@ -141,16 +170,20 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
     TORCH_CHECK(R->numel() == Y.numel(), "R shape");
     rp = R->data_ptr();
   }
+  TORCH_CHECK(!ss_out.has_value() || rp, "ss_out (fused RMSNorm statistic) needs the residual R");
+  NormEpiScope scope(make_norm_epi(M, K, ss_out, c10::nullopt, 0.0));
   launch_gemm_tn_algo(X.data_ptr(), W.data_ptr(), Y.data_ptr(), rp, M, N, K, (int)algo, stream());
   check_launch("gemm");
 }
 
-void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
+void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y,
+               const c10::optional<at::Tensor>& ss_in, double norm_eps) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
   const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K && N % 64 == 0, "gemm_silu: W [N, K], N % 64 == 0");
   TORCH_CHECK(Y.numel() == (int64_t)M * (N / 2), "gemm_silu: Y [M, N/2]");
   TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_silu: unsupported shape");
+  NormEpiScope scope(make_norm_epi(M, K, c10::nullopt, ss_in, norm_eps));
   TORCH_CHECK(launch_gemm_silu(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, stream()) == 0,
               "gemm_silu failed");
   check_launch("gemm_silu");
@@ -557,9 +590,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding", &embedding);
   m.def("rope_kv", &rope_kv);
   m.def("gemm", &gemm, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none(),
-        py::arg("algo") = -1);
+        py::arg("algo") = -1, py::arg("ss_out") = py::none());
+  m.def("row_sumsq", &row_sumsq, "per-row sum of squares, int64 fixed point (fused RMSNorm statistic)");
   m.def("gemm_select", &gemm_select);
-  m.def("qkv_rope", &qkv_rope);
+  m.def("qkv_rope", &qkv_rope, py::arg("X"), py::arg("W"), py::arg("qkv"), py::arg("pos"),
+        py::arg("slots"), py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
+        py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
   m.def("gemm_plan_set_splits", &gemm_plan_set_splits_py,
@@ -578,7 +615,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_stream_force_splits", &gemm_stream_force_splits, "split count of the K2 stream kernel: 0 auto");
   m.def("gemm_stream_splits", &gemm_stream_splits);
   m.def("gemm_splitk_force", &gemm_splitk_force, "split-K count of the 128^2 path: -1 auto, <= 1 off, S forced");
-  m.def("gemm_silu", &gemm_silu);
+  m.def("gemm_silu", &gemm_silu, py::arg("X"), py::arg("W"), py::arg("Y"),
+        py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("gemm_f32out", &gemm_f32out);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("topk_fused", &topk_fused, py::arg("Q"), py::arg("E"), py::arg("k"), py::arg("cand_v"),

@@ -66,3 +66,85 @@ DEV float uniform01(uint64_t seed, uint64_t a, uint64_t b) {
   uint64_t h = mix64(seed ^ mix64(a * 0x100000001B3ull + b));
   return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
 }
+
+// RMSNorm fused into GEMM epilogues (kernels.h NormEpi, passed to kernels by
+// value).  The per-row sums of squares are 64-bit fixed point (2^-28 units):
+// integer atomic adds are order-independent, so the fused norm is bitwise
+// deterministic whatever order the producing tiles finish in (fp32 atomics
+// would not be), with 2^36 of headroom over a 4096-wide row of |x| ~ 1e3.
+constexpr float SS_FIX = 268435456.f;                 // 2^28
+DEV void ss_atomic_add(unsigned long long* p, float v) {
+  __hip_atomic_fetch_add(p, (unsigned long long)__float2ull_rn(v * SS_FIX), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+// row scale of a consumer epilogue (1 when no norm is fused)
+template <class NE>
+DEV float norm_row_scale(const NE& ne, int m) {
+  if (!ne.ss_in) return 1.f;
+  const float ss = (float)ne.ss_in[m] * (1.f / SS_FIX);
+  return rsqrtf(ss * ne.inv_h + ne.eps);
+}
+// sum of squares of the bf16-rounded values a residual epilogue stores
+DEV float sumsq_bf16x4(const bf16x4& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += (float)v[j] * (float)v[j];
+  return s;
+}
+DEV float sumsq_bf16x8(const bf16x8& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += (float)v[j] * (float)v[j];
+  return s;
+}
+
+// Plain / residual epilogue of an MFMA 16x16x32 accumulator grid in the direct
+// layout: lane (fr = lane & 15, fq = lane >> 4) holds rows mb + 16 mt + fr,
+// columns nb + 16 nt + 4 fq .. +3.  EPI 1 adds R, whose rows are all loaded up
+// front (clamped, no branch) so their latency overlaps instead of serialising
+// behind the per-row guards (cdna_hip_programming.md §5 "Projection GEMM at
+// M = 256" item 4(c)); with ne.ss_out it also adds each stored row's sum of
+// squares (the fused RMSNorm statistic: the 4 fq lanes of a row, then one
+// atomic per row and wave).  N % 4 == 0.
+template <int EPI, int MT, int NT, class NE>
+DEV void store_direct(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y,
+                      const bf16* __restrict__ R, int M, int N, int mb, int nb, int fr, int fq,
+                      const NE& ne) {
+  bf16x4 rres[EPI == 1 ? MT : 1][EPI == 1 ? NT : 1];
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int m = min(mb + mt * 16 + fr, M - 1);
+        const int n = min(nb + nt * 16 + fq * 4, N - 4);
+        rres[mt][nt] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
+      }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mb + mt * 16 + fr;
+    float ss = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = nb + nt * 16 + fq * 4;
+      f32x4 v = acc[mt][nt];
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += (float)rres[mt][nt][j];
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+      if (m < M && n < N) {
+        *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+        if (EPI == 1) ss += sumsq_bf16x4(o);
+      }
+    }
+    if (EPI == 1 && ne.ss_out) {
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (fq == 0 && m < M) ss_atomic_add(ne.ss_out + m, ss);
+    }
+  }
+}

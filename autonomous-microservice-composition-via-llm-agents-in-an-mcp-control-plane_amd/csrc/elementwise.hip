@@ -116,6 +116,31 @@ void launch_silu_mul(const void* x, void* y, int T, int F, hipStream_t s) {
   silu_mul_kernel<<<grid, 256, 0, s>>>((const bf16*)x, (bf16*)y, T, F);
 }
 
+// ------------------------------------------- fused-RMSNorm launch context
+NormEpi& norm_epi() {
+  static NormEpi ne;
+  return ne;
+}
+
+// per-row sum of squares (the fused norm's statistic of a row nobody's GEMM
+// epilogue wrote: the embedding output of layer 0); one wave per row
+__global__ __launch_bounds__(256) void row_sumsq_kernel(const bf16* __restrict__ x,
+                                                        unsigned long long* __restrict__ ss, int T,
+                                                        int H) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const int lane = threadIdx.x & 63;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * H);
+  float acc = 0.f;
+  for (int c = lane; c < (H >> 3); c += 64) acc += sumsq_bf16x8(xr[c]);
+  acc = wave_sum(acc);
+  if (lane == 0) ss[row] = (unsigned long long)__float2ull_rn(acc * SS_FIX);
+}
+
+void launch_row_sumsq(const void* x, unsigned long long* ss, int T, int H, hipStream_t s) {
+  if (T > 0) row_sumsq_kernel<<<(T + 3) / 4, 256, 0, s>>>((const bf16*)x, ss, T, H);
+}
+
 // ---------------------------------------------------------------- K8 embedding
 __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ ids,
                                                         const bf16* __restrict__ table,
@@ -140,7 +165,7 @@ template <int D>
 __global__ __launch_bounds__(256) void rope_kv_kernel(
     const bf16* __restrict__ qkv, const int* __restrict__ pos, const int* __restrict__ slots,
     const float2* __restrict__ cos_sin, bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
-    bf16* __restrict__ v_cache, int T, int Hq, int Hkv, int BS) {
+    bf16* __restrict__ v_cache, int T, int Hq, int Hkv, int BS, const NormEpi ne) {
   constexpr int CH = D / 16;                 // 8-wide chunks in the first half
   const int heads = Hq + 2 * Hkv;
   const size_t total = (size_t)T * heads * CH;
@@ -153,13 +178,22 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
   const int d0 = c * 8;
   const bf16x8 lo = *reinterpret_cast<const bf16x8*>(src + d0);
   const bf16x8 hi = *reinterpret_cast<const bf16x8*>(src + d0 + D / 2);
+  const float rs = norm_row_scale(ne, t);    // fused RMSNorm of the projected row (1 if none)
   if (h >= Hq + Hkv) {                       // V: copy into the cache
     const int slot = slots[t];
     if (slot < 0) return;
     const int hv = h - Hq - Hkv;
     bf16* dst = v_cache + (((size_t)(slot / BS) * Hkv + hv) * BS + (slot % BS)) * D;
-    *reinterpret_cast<bf16x8*>(dst + d0) = lo;
-    *reinterpret_cast<bf16x8*>(dst + d0 + D / 2) = hi;
+    bf16x8 vlo = lo, vhi = hi;
+    if (ne.ss_in) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        vlo[j] = (bf16)((float)lo[j] * rs);
+        vhi[j] = (bf16)((float)hi[j] * rs);
+      }
+    }
+    *reinterpret_cast<bf16x8*>(dst + d0) = vlo;
+    *reinterpret_cast<bf16x8*>(dst + d0 + D / 2) = vhi;
     return;
   }
   const float2* cs = cos_sin + (size_t)pos[t] * (D / 2) + d0;
@@ -167,7 +201,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float2 r = cs[j];
-    const float a = (float)lo[j], b = (float)hi[j];
+    const float a = (float)lo[j] * rs, b = (float)hi[j] * rs;
     olo[j] = (bf16)(a * r.x - b * r.y);
     ohi[j] = (bf16)(b * r.x + a * r.y);
   }
@@ -193,11 +227,11 @@ void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const voi
   if (D == 128)
     rope_kv_kernel<128><<<grid, 256, 0, s>>>((const bf16*)qkv, pos, slots, (const float2*)cos_sin,
                                              (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, T, Hq,
-                                             Hkv, BS);
+                                             Hkv, BS, norm_epi());
   else if (D == 64)
     rope_kv_kernel<64><<<grid, 256, 0, s>>>((const bf16*)qkv, pos, slots, (const float2*)cos_sin,
                                             (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, T, Hq,
-                                            Hkv, BS);
+                                            Hkv, BS, norm_epi());
 }
 
 // ------------------------------------------------------------ residual add

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
                                                       const bf16* __restrict__ W,
                                                       OutT* __restrict__ Y,
                                                       const bf16* __restrict__ R, int M, int N,
-                                                      int K) {
+                                                      int K, const NormEpi ne) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE_ELEMS];   // [buf][A|B][128][64]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -115,17 +115,22 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
   }
 
   // ---- epilogue: lane holds Y[m][n..n+3]
+  if constexpr (sizeof(OutT) == 2 && EPI != 2) {
+    store_direct<EPI>(acc, (bf16*)Y, R, M, N, m0 + wm * 64, n0 + wn * 64, fr, fq, ne);
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     const int m = m0 + wm * 64 + mt * 16 + fr;
     if (m >= M) continue;
     if constexpr (EPI == 2) {
       const int F = N >> 1;
+      const float rs = norm_row_scale(ne, m);        // fused RMSNorm of the input row
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int f = ((n0 + wn * 64) >> 1) + p * 16 + fq * 4;
         if (f >= F) continue;
-        const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
+        const f32x4 gv = acc[mt][2 * p] * rs, uv = acc[mt][2 * p + 1] * rs;
         bf16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
@@ -161,12 +166,15 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ ws, int S,
                                                      bf16* __restrict__ Y,
-                                                     const bf16* __restrict__ R, int M, int N) {
+                                                     const bf16* __restrict__ R, int M, int N,
+                                                     const NormEpi ne) {
   const int NO = EPI == 2 ? N / 2 : N;               // output columns
+  const size_t total = (size_t)M * NO / 4;
   const size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i4 >= (size_t)M * NO / 4) return;
-  const int m = (int)(i4 / (NO / 4));
-  const int c = (int)(i4 % (NO / 4)) * 4;            // first output column
+  const bool valid = i4 < total;
+  const size_t iv = valid ? i4 : total - 1;
+  const int m = (int)(iv / (NO / 4));
+  const int c = (int)(iv % (NO / 4)) * 4;            // first output column
   const size_t MN = (size_t)M * N;
   bf16x4 o;
   if constexpr (EPI == 2) {
@@ -177,6 +185,9 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
       g += *reinterpret_cast<const f32x4*>(p + s * MN);
       u += *reinterpret_cast<const f32x4*>(p + s * MN + 16);
     }
+    const float rs = norm_row_scale(ne, m);          // fused RMSNorm of the input row
+    g *= rs;
+    u *= rs;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = (bf16)(g[j] / (1.f + __expf(-g[j])) * u[j]);
   } else {
@@ -191,7 +202,20 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ w
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
   }
-  *reinterpret_cast<bf16x4*>(Y + (size_t)m * NO + c) = o;
+  if (valid) *reinterpret_cast<bf16x4*>(Y + (size_t)m * NO + c) = o;
+  if (EPI == 1 && ne.ss_out) {
+    // fused RMSNorm statistic: one atomic per wave when the wave's 64 threads
+    // cover one row (NO / 4 a multiple of 64), else one per thread
+    float ss = valid ? sumsq_bf16x4(o) : 0.f;
+    const size_t w0 = i4 & ~(size_t)63;
+    const bool one_row = (NO / 4) % 64 == 0 && w0 < total;
+    if (one_row) {
+      ss = wave_sum(ss);
+      if ((threadIdx.x & 63) == 0) ss_atomic_add(ne.ss_out + m, ss);
+    } else if (valid) {
+      ss_atomic_add(ne.ss_out + m, ss);
+    }
+  }
 }
 
 }  // namespace
@@ -294,6 +318,10 @@ int gemm_plan_lookup(int M, int N, int K) {
 
 int gemm_select(int M, int N, int K) {
   if (M < 256 || N < 256 || K < 128) return 0;
+  // a fused RMSNorm needs an epilogue that implements it: the 256^2
+  // ping-pong fallback (shapes the AGPR kernel rejects) does not
+  const NormEpi& ne = norm_epi();
+  if ((ne.ss_in || ne.ss_out) && gemm256d_ok(M, N, K) != 0) return 0;
   const int plan = gemm_plan_lookup(M, N, K);
   if (plan >= 0 && (plan == 0 || gemm256d_ok(M, N, K) == 0)) return plan == 0 ? 0 : 1;
   const double G = (double)gemm256_num_cus();
@@ -423,13 +451,13 @@ static bool launch_gemm_128_split(const void* X, const void* W, void* Y, const v
   if (S <= 1) return false;
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   gemm_tn_128<0, float, true><<<dim3(nm * nn, S), 256, 0, s>>>(
-      (const bf16*)X, (const bf16*)W, g_splitk_ws, nullptr, M, N, K);
+      (const bf16*)X, (const bf16*)W, g_splitk_ws, nullptr, M, N, K, NormEpi{});
   const size_t n4 = (size_t)M * (epi == 2 ? N / 2 : N) / 4;
   const dim3 rg((unsigned)((n4 + 255) / 256));
   switch (epi) {
-    case 0: splitk_reduce<0><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N); break;
-    case 1: splitk_reduce<1><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, (const bf16*)R, M, N); break;
-    default: splitk_reduce<2><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N); break;
+    case 0: splitk_reduce<0><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N, norm_epi()); break;
+    case 1: splitk_reduce<1><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, (const bf16*)R, M, N, norm_epi()); break;
+    default: splitk_reduce<2><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N, norm_epi()); break;
   }
   return true;
 }
@@ -441,10 +469,10 @@ static void launch_gemm_tn_128(const void* X, const void* W, void* Y, const void
   const dim3 grid(nm * nn);
   if (R)
     gemm_tn_128<1><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                        (const bf16*)R, M, N, K);
+                                        (const bf16*)R, M, N, K, norm_epi());
   else
     gemm_tn_128<0><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr, M, N,
-                                        K);
+                                        K, norm_epi());
 }
 
 // fp32-output variant (retrieval scores: bf16 would tie near-equal cosines)
@@ -452,7 +480,7 @@ void launch_gemm_tn_f32out(const void* X, const void* W, float* Y, int M, int N,
                            hipStream_t s) {
   const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
   gemm_tn_128<0, float><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, Y,
-                                                      nullptr, M, N, K);
+                                                      nullptr, M, N, K, NormEpi{});
 }
 
 // A few rows (single-intent decode): the skinny kernel streams the weights at
@@ -521,7 +549,7 @@ int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K,
   } else if (!launch_gemm_128_split(X, W, Y, nullptr, M, N, K, 2, s)) {
     const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
     gemm_tn_128<2><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                 nullptr, M, N, K);
+                                                 nullptr, M, N, K, norm_epi());
   }
   return 0;
 }

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
-                                                       int K, const RopeArgs ra) {
+                                                       int K, const RopeArgs ra, const NormEpi ne) {
   static_assert(BMT % 32 == 0 && BMT >= 128 && BMT <= 256, "tile height");
   constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (4..8)
   constexpr int WROWS = BMT / 2;                    // rows per wave (64..128)
@@ -299,6 +299,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
 #pragma unroll
       for (int mt = 0; mt < MTW; ++mt) rpos[mt] = ra.pos[min(m0 + wm * WROWS + mt * 16 + fr, M - 1)];
     }
+    // EPI 2 / 3: fused RMSNorm of the input rows (1 when none), loaded up front
+    float rsc[EPI >= 2 ? MTW : 1];
+    if constexpr (EPI >= 2) {
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) rsc[mt] = norm_row_scale(ne, min(m0 + wm * WROWS + mt * 16 + fr, M - 1));
+    }
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt) {
       const int row = mt * 16 + fr;
@@ -320,7 +326,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
           for (int j = 0; j < 4; ++j) {
             const f32x4 cc = c4[nt_][j >> 1];
             const float rc = cc[(j & 1) * 2], rs = cc[(j & 1) * 2 + 1];
-            const float x1 = acc[mt][nt_][j], x2 = acc[mt][nt_ + 4][j];
+            const float x1 = acc[mt][nt_][j] * rsc[mt], x2 = acc[mt][nt_ + 4][j] * rsc[mt];
             o1[j] = (bf16)(x1 * rc - x2 * rs);
             o2[j] = (bf16)(x2 * rc + x1 * rs);
           }
@@ -332,7 +338,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
       if constexpr (EPI == 2) {
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          const f32x4 gv = acc[mt][2 * p], uv = acc[mt][2 * p + 1];
+          const f32x4 gv = acc[mt][2 * p] * rsc[mt], uv = acc[mt][2 * p + 1] * rsc[mt];
           bf16x4 o;
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
@@ -343,7 +349,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
         for (int nt_ = 0; nt_ < 8; ++nt_) {
           bf16x4 o;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[mt][nt_][j];
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)(EPI == 3 ? acc[mt][nt_][j] * rsc[mt] : acc[mt][nt_][j]);
           put(row, nt_ * 16 + fq * 4, o);
         }
       }
@@ -376,13 +382,20 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
         *reinterpret_cast<bf16x8*>(dst + lc * 8) = v;
         continue;
       }
-      if (m < M) {
-        const size_t off = (size_t)m * ldy + col0 + lc * 8;
-        if constexpr (EPI == 1) {
+      if constexpr (EPI == 1) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rres[i][j]);
-        }
-        *reinterpret_cast<bf16x8*>(Y + off) = v;
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)rres[i][j]);
+      }
+      if (m < M) *reinterpret_cast<bf16x8*>(Y + (size_t)m * ldy + col0 + lc * 8) = v;
+      if (EPI == 1 && ne.ss_out) {
+        // fused RMSNorm statistic: the row's 128 columns sit in the NCH = 16
+        // lanes lr * 16 + lc; one atomic per row and wave
+        float ss = m < M ? sumsq_bf16x8(v) : 0.f;
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        ss += __shfl_xor(ss, 4, 64);
+        ss += __shfl_xor(ss, 8, 64);
+        if (lc == 0 && m < M) ss_atomic_add(ne.ss_out + m, ss);
       }
     }
   }
@@ -490,10 +503,10 @@ static int launch_height(const void* X, const void* W, void* Y, const void* R, i
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
   switch (epi) {
-    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra); return 0;
-    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
-    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra); return 0;
+    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra, norm_epi()); return 0;
+    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra, norm_epi()); return 0;
+    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra, norm_epi()); return 0;
+    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra, norm_epi()); return 0;
     default: return 2;
   }
 }

@@ -60,16 +60,17 @@ DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
 // the epilogue for one accumulator row mt from per-element values v(nt)
 template <int EPI, class V>
 DEV void store_row(bf16* __restrict__ Y, const bf16* __restrict__ R, int M, int N, int m0, int n0,
-                   int wm, int wn, int fr, int fq, int mt, V&& v) {
+                   int wm, int wn, int fr, int fq, int mt, const NormEpi& ne, V&& v) {
   const int m = m0 + wm * 128 + mt * 16 + fr;
-  if (m >= M) return;
+  if (m >= M) return;                                // the 4 fq lanes of the row together
   if constexpr (EPI == 2) {
     const int F2 = N >> 1;
+    const float rs = norm_row_scale(ne, m);          // fused RMSNorm of the input row
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int f = ((n0 + wn * 128) >> 1) + p * 16 + fq * 4;
       if (f >= F2) continue;
-      const f32x4 gv = v(2 * p), uv = v(2 * p + 1);
+      const f32x4 gv = v(2 * p) * rs, uv = v(2 * p + 1) * rs;
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
@@ -77,20 +78,31 @@ DEV void store_row(bf16* __restrict__ Y, const bf16* __restrict__ R, int M, int 
     }
     return;
   }
+  bf16x4 rr[8];
+  if (EPI == 1) {                                    // residual up front (N % 256 == 0)
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+      rr[nt] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n0 + wn * 128 + nt * 16 + fq * 4);
+  }
+  float ss = 0.f;
 #pragma unroll
   for (int nt = 0; nt < 8; ++nt) {
     const int n = n0 + wn * 128 + nt * 16 + fq * 4;
-    if (n >= N) continue;
     f32x4 x = v(nt);
     if (EPI == 1) {
-      const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] += (float)r[j];
+      for (int j = 0; j < 4; ++j) x[j] += (float)rr[nt][j];
     }
     bf16x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = (bf16)x[j];
     *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+    if (EPI == 1) ss += sumsq_bf16x4(o);
+  }
+  if (EPI == 1 && ne.ss_out) {                       // fused RMSNorm statistic of the row
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (fq == 0) ss_atomic_add(ne.ss_out + m, ss);
   }
 }
 
@@ -100,7 +112,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256sk(const bf16* __restrict__
                                                         bf16* __restrict__ Y,
                                                         const bf16* __restrict__ R, int M, int N,
                                                         int K, f32x4* __restrict__ ws,
-                                                        int* __restrict__ cnt, int tile0) {
+                                                        int* __restrict__ cnt, int tile0,
+                                                        const NormEpi ne) {
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT_B];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -275,7 +288,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256sk(const bf16* __restrict__
           }
 #pragma unroll
           for (int h = 0; h < 2; ++h)
-            store_row<EPI>(Y, R, M, N, m0, n0, wm, wn, fr, fq, 2 * rb + h,
+            store_row<EPI>(Y, R, M, N, m0, n0, wm, wn, fr, fq, 2 * rb + h, ne,
                            [&](int nt) { return P[h * 8 + nt]; });
         }
       }
@@ -370,9 +383,9 @@ int launch_gemm_tn_256sk(const void* X, const void* W, void* Y, const void* R, i
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
   switch (epi) {
-    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, 0); return 0;
-    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt, 0); return 0;
-    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, 0); return 0;
+    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, 0, norm_epi()); return 0;
+    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt, 0, norm_epi()); return 0;
+    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, 0, norm_epi()); return 0;
     default: return 5;
   }
 }
@@ -399,9 +412,9 @@ int launch_gemm_tn_256sk_tail(const void* X, const void* W, void* Y, const void*
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
   switch (epi) {
-    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, tile0); return 0;
-    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt, tile0); return 0;
-    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, tile0); return 0;
+    case 0: gemm_tn_256sk<0><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, tile0, norm_epi()); return 0;
+    case 1: gemm_tn_256sk<1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, st->ws, st->cnt, tile0, norm_epi()); return 0;
+    case 2: gemm_tn_256sk<2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, st->ws, st->cnt, tile0, norm_epi()); return 0;
     default: return 5;
   }
 }

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_flex(const bf16* __restrict__ 
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
-                                                       int K) {
+                                                       int K, const NormEpi ne) {
   static_assert(TM % 32 == 0 && TN % 32 == 0, "tile dims are multiples of 32");
   static_assert(2 * (TM + TN) * FBK * 2 <= 80 * 1024, "two workgroups per CU");
   constexpr int MT = TM / 32, NT = TN / 32;        // 16-row MFMA tiles per wave
@@ -112,26 +112,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_flex(const bf16* __restrict__ 
   }
 
   // ---- epilogue: lane holds Y[m][n .. n+3]
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = m0 + wm * (TM / 2) + mt * 16 + fr;
-    if (m >= M) continue;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int n = n0 + wn * (TN / 2) + nt * 16 + fq * 4;
-      if (n >= N) continue;
-      f32x4 v = acc[mt][nt];
-      if (EPI == 1) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-      *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
-    }
-  }
+  store_direct<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
 }
 
 // One workgroup per CU, NST LDS stages with NST - 2 k-tiles in flight across
@@ -145,7 +126,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_flexp(const bf16* __restrict__
                                                         const bf16* __restrict__ W,
                                                         bf16* __restrict__ Y,
                                                         const bf16* __restrict__ R, int M, int N,
-                                                        int K) {
+                                                        int K, const NormEpi ne) {
   static_assert(TM % 32 == 0 && TN % 32 == 0, "tile dims are multiples of 32");
   static_assert(NST * (TM + TN) * FBK * 2 <= 160 * 1024, "LDS");
   constexpr int MT = TM / 32, NT = TN / 32;
@@ -233,26 +214,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_flexp(const bf16* __restrict__
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing re-loads land before exit
 
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = m0 + wm * (TM / 2) + mt * 16 + fr;
-    if (m >= M) continue;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int n = n0 + wn * (TN / 2) + nt * 16 + fq * 4;
-      if (n >= N) continue;
-      f32x4 v = acc[mt][nt];
-      if (EPI == 1) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-      *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
-    }
-  }
+  store_direct<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
 }
 
 template <int TM, int TN>
@@ -262,18 +224,18 @@ void flex_launch(const void* X, const void* W, void* Y, const void* R, int M, in
   if (pipe) {
     if (R)
       gemm_tn_flexp<1, TM, TN, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                       (const bf16*)R, M, N, K);
+                                                       (const bf16*)R, M, N, K, norm_epi());
     else
       gemm_tn_flexp<0, TM, TN, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                       nullptr, M, N, K);
+                                                       nullptr, M, N, K, norm_epi());
     return;
   }
   if (R)
     gemm_tn_flex<1, TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                 (const bf16*)R, M, N, K);
+                                                 (const bf16*)R, M, N, K, norm_epi());
   else
     gemm_tn_flex<0, TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr,
-                                                 M, N, K);
+                                                 M, N, K, norm_epi());
 }
 
 }  // namespace

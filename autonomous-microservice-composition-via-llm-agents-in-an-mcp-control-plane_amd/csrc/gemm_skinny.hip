@@ -39,7 +39,7 @@ __global__ __launch_bounds__(512) void gemm_skinny(const bf16* __restrict__ X,
                                                    const bf16* __restrict__ W,
                                                    bf16* __restrict__ Y,
                                                    const bf16* __restrict__ R, int M, int N, int K,
-                                                   int nx, int ny) {
+                                                   int nx, int ny, const NormEpi ne) {
   constexpr int RB = EPI == 2 ? 2 : 1;               // 16-row weight blocks per workgroup
   __shared__ f32x4 red[SK_WAVES][RB][MB][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -103,20 +103,19 @@ __global__ __launch_bounds__(512) void gemm_skinny(const bf16* __restrict__ X,
   }
   // C layout: lane holds rows (weight n) 4g..4g+3 of column (token) r
   const int m = m0 + mb * 16 + r;
-  if (m >= M) return;
+  if (m >= M) return;                                // all four g lanes of token r together
   if constexpr (EPI == 2) {
-    const int F = N >> 1, f = (n0 >> 1) + 4 * g;
-    if (f >= F) return;
+    const int F = N >> 1, f = (n0 >> 1) + 4 * g;     // f < F: N % 32 == 0 (skinny_ok)
+    const float rs = norm_row_scale(ne, m);
     bf16x4 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float gv = tot[0][q], uv = tot[1][q];
+      const float gv = tot[0][q] * rs, uv = tot[1][q] * rs;
       o[q] = (bf16)(gv / (1.f + __expf(-gv)) * uv);
     }
     *reinterpret_cast<bf16x4*>(Y + (size_t)m * F + f) = o;
   } else {
-    const int n = n0 + 4 * g;
-    if (n >= N) return;
+    const int n = n0 + 4 * g;                        // n < N: N % 16 == 0 (skinny_ok)
     f32x4 v = tot[0];
     if (EPI == 1) {
       const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
@@ -127,6 +126,13 @@ __global__ __launch_bounds__(512) void gemm_skinny(const bf16* __restrict__ X,
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[q] = (bf16)v[q];
     *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+    if (EPI == 1 && ne.ss_out) {
+      // fused RMSNorm statistic: the 16 columns of token r sit in lanes r + 16 g
+      float ss = sumsq_bf16x4(o);
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (g == 0) ss_atomic_add(ne.ss_out + m, ss);
+    }
   }
 }
 
@@ -136,7 +142,8 @@ void launch_mb(const void* X, const void* W, void* Y, const void* R, int M, int 
   constexpr int RB = EPI == 2 ? 2 : 1;
   const int nx = (N + 16 * RB - 1) / (16 * RB), ny = (M + 16 * MB - 1) / (16 * MB);
   gemm_skinny<EPI, MB><<<nx * ny, 64 * SK_WAVES, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                          (const bf16*)R, M, N, K, nx, ny);
+                                                          (const bf16*)R, M, N, K, nx, ny,
+                                                          norm_epi());
 }
 
 template <int EPI>

@@ -50,7 +50,8 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
                                                       bf16* __restrict__ Y,
                                                       const bf16* __restrict__ R, int M, int N,
                                                       int K, int S, float* __restrict__ ws,
-                                                      int* __restrict__ tickets, const RopeArgs ra) {
+                                                      int* __restrict__ tickets, const RopeArgs ra,
+                                                      const NormEpi ne) {
   static_assert(NF % 2 == 0, "fragment pairs");
   constexpr int NQ = NF * MF;                        // fragments per tile
   constexpr int FPU = (EPI >= 2) ? 2 : 1;            // fragments per epilogue unit
@@ -191,9 +192,14 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
     }
     __syncthreads();
     if (!s_last) return;
+    // every split's partial (this one's too) summed in split order: the
+    // output is bit-identical whichever split arrives last
+#pragma unroll
+    for (int a = 0; a < UPW; ++a)
+#pragma unroll
+      for (int j = 0; j < FPU; ++j) sum[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
-    for (int jj = 1; jj < S; ++jj) {
-      const int js = (sp + jj) % S;
+    for (int js = 0; js < S; ++js) {
       f32x4 p[UPW][FPU];
 #pragma unroll
       for (int a = 0; a < UPW; ++a) {
@@ -220,10 +226,11 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
     const int f0 = FPU == 1 ? u / MF : 2 * (u / MF);
     const int mm = u % MF;
     const int m = 16 * MF * mh + 16 * mm + r;
-    if (m >= M) continue;
+    if (m >= M) continue;                            // the four g lanes of token r together
+    const float rs = EPI >= 2 ? norm_row_scale(ne, m) : 1.f;   // fused RMSNorm of the input row
     if constexpr (EPI == 2) {
       // gate fragment f0, up fragment f0 + 1: output features n0/2 + 8 f0 + 4 g + i
-      const f32x4 gv = sum[a][0], uv = sum[a][1];
+      const f32x4 gv = sum[a][0] * rs, uv = sum[a][1] * rs;
       bf16x4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] = (bf16)(gv[i] / (1.f + __expf(-gv[i])) * uv[i]);
@@ -231,7 +238,7 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
     } else if constexpr (EPI == 3) {
       const int head = tile >> 1;
       const int d = 32 * (tile & 1) + 16 * (f0 >> 1) + 4 * g;       // first of 4 dims (< 64)
-      const f32x4 x1 = sum[a][0], x2 = sum[a][1];
+      const f32x4 x1 = sum[a][0] * rs, x2 = sum[a][1] * rs;
       bf16x4 o1, o2;
       const bool is_v = head >= ra.Hq + ra.Hkv;
       if (is_v) {
@@ -277,6 +284,13 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (bf16)v[i];
         *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
+        if (EPI == 1 && ne.ss_out) {
+          // fused RMSNorm statistic: token r's 16 rows of this fragment sit in lanes r + 16 g
+          float ss = sumsq_bf16x4(o);
+          ss += __shfl_xor(ss, 16, 64);
+          ss += __shfl_xor(ss, 32, 64);
+          if (g == 0) ss_atomic_add(ne.ss_out + m, ss);
+        }
       }
     }
   }
@@ -294,11 +308,12 @@ void launch_v(const void* X, const void* W, void* Y, const void* R, int M, int N
   }
   if (g_stream_nt)
     gemm_stream<EPI, MF, NF, DEPTH, MH, true><<<tiles * S, 256 * MH, 0, s>>>(
-        (const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, S, ws, tk, ra);
+        (const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, S, ws, tk, ra,
+        norm_epi());
   else
   gemm_stream<EPI, MF, NF, DEPTH, MH, false><<<tiles * S, 256 * MH, 0, s>>>((const bf16*)X, (const bf16*)W,
                                                              (bf16*)Y, (const bf16*)R, M, N, K, S,
-                                                             ws, tk, ra);
+                                                             ws, tk, ra, norm_epi());
 }
 
 template <int EPI>

@@ -5,7 +5,29 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+// RMSNorm fused into the GEMM epilogues (TP = 1 forward, models/llama.py):
+// the residual projections (EPI 1) add the sum of squares of every bf16 row
+// they write to ss_out[row] (atomic), and the projections that consume a
+// normed activation (SwiGLU EPI 2, QKV + RoPE EPI 3, rope_kv) scale each row
+// of their fp32 accumulators by rsqrt(ss_in[row] * inv_h + eps) - the norm's
+// per-column weight is folded into those weights once at load.  Set for the
+// duration of one launcher call (NormEpiScope); every kernel launcher copies
+// it into its kernel's arguments, so it is safe under hipGraph capture.
+struct NormEpi {
+  unsigned long long* ss_out = nullptr;     // [M] fixed point (common.h SS_FIX), zeroed by the caller
+  const unsigned long long* ss_in = nullptr;
+  float inv_h = 0.f, eps = 0.f;
+};
+NormEpi& norm_epi();                     // the current launch's (host, not thread-shared)
+struct NormEpiScope {
+  NormEpi saved;
+  explicit NormEpiScope(const NormEpi& ne) : saved(norm_epi()) { norm_epi() = ne; }
+  ~NormEpiScope() { norm_epi() = saved; }
+};
+
 // elementwise.hip
+// per-row sum of squares (ss[t] = sum_h x[t, h]^2, NormEpi fixed point) of a bf16 [T, H] matrix
+void launch_row_sumsq(const void* x, unsigned long long* ss, int T, int H, hipStream_t s);
 void launch_rmsnorm(const void* x, const void* w, void* out, int T, int H, float eps,
                     hipStream_t s);
 void launch_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int H,

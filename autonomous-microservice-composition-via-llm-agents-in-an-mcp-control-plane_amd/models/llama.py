@@ -246,6 +246,28 @@ def random_weights(cfg: LlamaConfig, device, dtype=torch.bfloat16, seed: int = 0
                         lm_head=embed if cfg.tie_embeddings else rnd((cfg.vocab_size, H), base + 13))
 
 
+def fold_norm_weights(w: "LlamaWeights") -> "LlamaWeights":
+    """Fold each layer's RMSNorm weights into the projections that consume the
+    normed rows (Wqkv <- Wqkv diag(attn_norm), W_gate_up <- W_gate_up
+    diag(mlp_norm)) and set the norm weights to ones: the same model, in the
+    form the fused-norm forward needs (the GEMM epilogues apply only the
+    per-row rsqrt).  In place and idempotent (a second fold multiplies by
+    ones), so weights shared by several models, checkpoints written from them
+    and reference forwards stay consistent.  Random-init norms are ones
+    already (nothing to fold)."""
+    for lw in w.layers:
+        for norm, name in ((lw.attn_norm, "wqkv"), (lw.mlp_norm, "w_gate_up")):
+            if bool((norm == 1).all()):
+                continue
+            mat = getattr(lw, name)
+            g = norm.float()[None, :]
+            for r0 in range(0, mat.shape[0], 4096):       # bounded fp32 temporaries
+                blk = mat[r0:r0 + 4096]
+                blk.copy_((blk.float() * g).to(mat.dtype))
+            norm.fill_(1)
+    return w
+
+
 class LlamaModel:
     """Stateless forward over weights + an external paged KV cache."""
 
@@ -264,6 +286,12 @@ class LlamaModel:
                                       "not served by the gfx950 kernels (need d=128, group | 16; "
                                       "models.llama.pad_gqa pads the query heads)")
         self.hq, self.hkv = cfg.heads // tp, cfg.kv_heads // tp
+        # RMSNorm fused into the GEMM epilogues (TP = 1, no sequence parallel):
+        # residual projections accumulate each row's sum of squares, the
+        # consumers scale their accumulators by the row's rsqrt; the norm
+        # weights are folded into Wqkv / W_gate_up.  MCP_FUSED_NORM=0: the
+        # standalone RMSNorm kernel between the projections.
+        fold_norm_weights(self.w)
         self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device,
                                         cfg.rope_scaling)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
@@ -274,6 +302,8 @@ class LlamaModel:
         if seq_parallel is None:
             seq_parallel = os.environ.get("MCP_SEQ_PARALLEL", "0") == "1"
         self.seq_parallel = bool(seq_parallel) and tp > 1
+        self.fused_norm = (tp == 1 and not self.seq_parallel
+                           and os.environ.get("MCP_FUSED_NORM", "1") == "1")
         self._sp = sp_collectives          # (reduce_scatter, all_gather), injectable
         if self.seq_parallel and sp_collectives is None:
             from ..parallel.comm import make_sp_collectives
@@ -328,6 +358,8 @@ class LlamaModel:
         T = step.token_ids.numel()
         x = ops.embedding(step.token_ids, self.w.embed)
         L = cfg.layers
+        if self.fused_norm:
+            return self._forward_fused_norm(step, kv, x)
         sp = self.seq_parallel
         if sp:
             # x: this rank's Tp rows of the residual stream (T padded to tp*Tp)
@@ -380,3 +412,39 @@ class LlamaModel:
             if l + 1 < L:
                 h = ops.rmsnorm(x, self.w.layers[l + 1].attn_norm, cfg.eps)
         return ops.rmsnorm(x, self.w.final_norm, cfg.eps)
+
+    def _forward_fused_norm(self, step, kv, x) -> torch.Tensor:
+        """TP = 1 forward with every RMSNorm but the final one fused into the
+        GEMM epilogues (no normed copy of the residual stream is written):
+        ``ss[l, 0]`` / ``ss[l, 1]`` are the fixed-point row sums of squares of
+        layer l's attention / MLP input, produced by the previous residual
+        GEMM (the embedding: ``row_sumsq``) and consumed by QKV + RoPE /
+        SwiGLU, which scale their accumulators per row (norm weights folded
+        into their weights, ``fold_norm_weights``)."""
+        cfg, D = self.cfg, self.cfg.head_dim
+        T = x.shape[0]
+        L, eps = cfg.layers, cfg.eps
+        rows = step.logit_rows
+        # rows: the tokens, or the last layer's selected rows (a hipGraph
+        # bucket's row capacity can exceed its token capacity)
+        ss = torch.zeros(L + 1, 2, max(T, rows.numel()), dtype=torch.int64, device=x.device)
+        ops.row_sumsq(x, ss[0, 0])
+        q = torch.empty(T, self.hq, D, device=x.device, dtype=x.dtype)
+        for l in range(L):
+            lw = self.w.layers[l]
+            kc, vc = kv.layer(l)
+            ops.qkv_rope(x, lw.wqkv, step.positions, step.slots, self.cos_sin, q, kc, vc,
+                         self.hq, self.hkv, D, ss_in=ss[l, 0], eps=eps)
+            a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
+            if l + 1 == L:
+                # last layer: only the sampled rows go on (see ``forward``)
+                if rows.numel() == 0:
+                    return x.new_empty(0, cfg.hidden)
+                ri = rows.long()
+                x = x.index_select(0, ri)
+                a = a.view(T, self.hq * D).index_select(0, ri)
+                T = ri.numel()
+            x = ops.gemm(a.view(T, self.hq * D), lw.wo, R=x, out=x, ss_out=ss[l, 1])
+            act = ops.gemm_silu(x, lw.w_gate_up, ss_in=ss[l, 1], eps=eps)
+            x = ops.gemm(act, lw.w_down, R=x, out=x, ss_out=ss[l + 1, 0])
+        return ops.rmsnorm(x, self.w.final_norm, eps)

@@ -150,42 +150,65 @@ def embedding(ids, table, out=None):
     return r if out is None else out.copy_(r)
 
 
-def gemm(X, W, R=None, out=None, algo: int = -1):
+def gemm(X, W, R=None, out=None, algo: int = -1, ss_out=None):
     """Y = X @ W^T (+ R).  X [M, K], W [N, K].  algo: -1 auto (the measured
-    plan), 0 = 128^2, 1 = 256^2 path, 9..13 = AGPR kernel at plan code algo - 8."""
+    plan), 0 = 128^2, 1 = 256^2 path, 9..13 = AGPR kernel at plan code algo - 8.
+    ``ss_out`` (int64 [M], residual GEMMs only): += each output row's sum of
+    squares, fixed point - the fused RMSNorm statistic of the next layer input."""
     if X.is_cuda:
         if _TRACE is not None:
             _trace(X, W, "gemm" if R is None else "gemm+res")
         out = X.new_empty(*X.shape[:-1], W.shape[0]) if out is None else out
-        lib().gemm(X, W, out, R, algo)
+        lib().gemm(X, W, out, R, algo, ss_out)
         return out
     r = ref.gemm(X, W, R)
+    if ss_out is not None:
+        ss_out[:r.shape[0]] += ref.row_sumsq(r)
     return r if out is None else out.copy_(r)
 
 
-def gemm_silu(X, W, out=None):
+def gemm_silu(X, W, out=None, ss_in=None, eps: float = 0.0):
     """SwiGLU projection: silu(X Wg^T) * (X Wu^T) with W = interleave_gate_up(Wg, Wu)
-    ([2F, K], 16-row groups); the activation is fused into the MFMA GEMM epilogue."""
+    ([2F, K], 16-row groups); the activation is fused into the MFMA GEMM epilogue.
+    ``ss_in`` (int64 [M]): fused RMSNorm - the accumulators of row m are scaled
+    by rsqrt(ss_in[m] / K + eps) first (the norm weight folded into W)."""
     if X.is_cuda:
         if _TRACE is not None:
             _trace(X, W, "swiglu")
         out = X.new_empty(*X.shape[:-1], W.shape[0] // 2) if out is None else out
-        lib().gemm_silu(X, W, out)
+        lib().gemm_silu(X, W, out, ss_in, eps)
         return out
-    r = ref.gemm_silu(X, W)
+    r = ref.gemm_silu(X, W, ss_in, eps)
     return r if out is None else out.copy_(r)
 
 
-def qkv_rope(h, wqkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, qkv=None):
+def row_sumsq(x, ss):
+    """ss[t] = sum of x[t]^2 (int64 fixed point): the fused-norm statistic of a
+    row no GEMM epilogue produced (the embedding output)."""
+    if x.is_cuda:
+        lib().row_sumsq(x, ss)
+    else:
+        ss[:x.shape[0]] = ref.row_sumsq(x)
+    return ss
+
+
+def qkv_rope(h, wqkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, qkv=None,
+             ss_in=None, eps: float = 0.0):
     """q_out, K/V cache <- rope(h wqkv^T).  On the GPU the rotation and the
     paged K/V write run in the QKV GEMM's epilogue when the AGPR kernel serves
-    the shape (``qkv`` is then untouched scratch); otherwise GEMM + rope_kv."""
+    the shape (``qkv`` is then untouched scratch); otherwise GEMM + rope_kv.
+    ``ss_in``: fused RMSNorm of the rows of ``h`` (see ``gemm_silu``)."""
     if h.is_cuda:
         T = h.numel() // h.shape[-1]
         qkv = h.new_empty(T, wqkv.shape[0]) if qkv is None else qkv
-        lib().qkv_rope(h, wqkv, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
+        lib().qkv_rope(h, wqkv, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D,
+                       ss_in, eps)
         return q_out
-    qkv = ref.gemm(h, wqkv)
+    if ss_in is not None:
+        qkv = ((h.float() @ wqkv.float().t())
+               * ref.norm_row_scale(ss_in[:h.shape[0]], h.shape[-1], eps)).to(h.dtype)
+    else:
+        qkv = ref.gemm(h, wqkv)
     ref.rope_kv(qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D)
     return q_out
 

@@ -46,8 +46,23 @@ def deinterleave_gate_up(w: torch.Tensor):
     return v[:, 0].reshape(F2 // 2, H), v[:, 1].reshape(F2 // 2, H)
 
 
-def gemm_silu(X, W_interleaved):
+SS_FIX = float(1 << 28)         # fixed-point unit of the fused-norm row statistics (csrc/common.h)
+
+
+def row_sumsq(x: torch.Tensor) -> torch.Tensor:
+    """Per-row sum of squares of a bf16 [T, H] matrix as int64 fixed point."""
+    return torch.round(x.float().pow(2).sum(-1) * SS_FIX).to(torch.int64)
+
+
+def norm_row_scale(ss: torch.Tensor, H: int, eps: float) -> torch.Tensor:
+    """[T, 1] fp32 rsqrt(mean(x^2) + eps) from fixed-point row statistics."""
+    return torch.rsqrt(ss.double().div(SS_FIX).float() / H + eps).unsqueeze(-1)
+
+
+def gemm_silu(X, W_interleaved, ss_in=None, eps: float = 0.0):
     y = (X.float() @ W_interleaved.float().t())
+    if ss_in is not None:                      # fused RMSNorm: rows scaled after the GEMM
+        y = y * norm_row_scale(ss_in[:X.shape[0]], X.shape[-1], eps)
     T, F2 = y.shape
     y = y.view(T, F2 // (2 * GU_GROUP), 2, GU_GROUP)
     g, u = y[:, :, 0], y[:, :, 1]

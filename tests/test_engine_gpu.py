@@ -186,11 +186,22 @@ def test_llama3_8b_full_width_layers_match_fp32():
     from mcp_amd.models.llama import CONFIGS, LayerWeights, LlamaWeights, random_weights
     cfg = dataclasses.replace(CONFIGS["llama3-8b"], name="8b-2layer", layers=2)
     w = random_weights(cfg, "cuda", seed=11, std=0.02)
-    model = LlamaModel(cfg, w, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(4)
+    for lw in w.layers:                  # non-trivial RMSNorm weights (folded by the GPU model)
+        lw.attn_norm.copy_(1 + 0.2 * torch.randn(lw.attn_norm.shape, device="cuda", generator=g))
+        lw.mlp_norm.copy_(1 + 0.2 * torch.randn(lw.mlp_norm.shape, device="cuda", generator=g))
     f32 = lambda t: t.float().cpu()
     wc = LlamaWeights(f32(w.embed), [LayerWeights(*[f32(getattr(l, fl.name)) for fl in dataclasses.fields(l)])
                                      for l in w.layers], f32(w.final_norm), f32(w.lm_head))
-    cpu = LlamaModel(cfg, wc, "cpu")
+    model = LlamaModel(cfg, w, "cuda")             # fused-norm forward (TP = 1)
+    assert model.fused_norm
+    import os
+    os.environ["MCP_FUSED_NORM"] = "0"             # the fp32 reference: standalone RMSNorm
+    try:
+        cpu = LlamaModel(cfg, wc, "cpu")
+    finally:
+        del os.environ["MCP_FUSED_NORM"]
+    assert not cpu.fused_norm
     nb = 16
     kv = KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, nb, "cuda")
     kvc = KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, nb, "cpu", dtype=torch.float32)

@@ -688,3 +688,102 @@ def test_qkv_rope_fused_every_height(M):
     finally:
         L.gemm_plan_clear()
         ops._load_gemm_plan(L)
+
+
+# ---------------------------------------------------------------- fused RMSNorm
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (5, 4096, 14336), (24, 4096, 4096),
+                                   (100, 4096, 4096), (300, 4096, 14336), (700, 4096, 4096),
+                                   (2600, 4096, 4096), (2600, 4096, 14336)])
+def test_fused_norm_residual_statistic(M, N, K):
+    """Residual GEMMs (y += x W^T) with ``ss_out``: every path the dispatcher
+    can take (skinny / stream / split-K 128^2 / flex / AGPR at every height,
+    algo -1 and forced) adds each output row's sum of squares (int64 fixed
+    point) matching the fp32 sum over the stored bf16 row; repeated runs give
+    bit-identical statistics (integer atomics)."""
+    torch.manual_seed(21)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    algos = [-1, 0] + ([9, 10, 11, 12, 13] if M >= 256 else [])
+    for algo in algos:
+        outs = []
+        for _ in range(2):
+            y = R.clone()
+            ss = torch.zeros(M, dtype=torch.int64, device=DEV)
+            ops.gemm(X, W, R=y, out=y, algo=algo, ss_out=ss)
+            exp = y.float().pow(2).sum(-1) * ref.SS_FIX
+            assert ((ss.double() - exp.double()).abs() / exp.double()).max().item() < 1e-5, algo
+            outs.append(ss)
+        assert torch.equal(outs[0], outs[1]), algo
+        assert rel_err(y, ref.gemm(X, W, R)) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 6, 20, 48, 200, 700, 2600])
+def test_fused_norm_swiglu_and_qkv(M):
+    """SwiGLU and QKV + RoPE with ``ss_in``: the accumulators of row m scaled
+    by rsqrt(ss[m] / H + eps) equal the GEMMs of the explicitly RMS-normed
+    rows (norm weight folded into W) against fp32, on every path the
+    dispatcher picks at this M (and every AGPR height for QKV)."""
+    torch.manual_seed(22)
+    L = ops.lib()
+    H, F, eps = 4096, 14336, 1e-5
+    x = (torch.randn(M, H, device=DEV) * 3).bfloat16()
+    gw = (torch.rand(H, device=DEV) + 0.5)                 # a non-trivial norm weight
+    ss = ref.row_sumsq(x.cpu()).to(DEV)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps) * gw
+    Wg = (torch.randn(2 * F, H, device=DEV) / math.sqrt(H)).bfloat16()
+    Wf = (Wg.float() * gw).bfloat16()                      # folded
+    y = ops.gemm_silu(x, Wf, ss_in=ss, eps=eps)
+    g, u = ref.deinterleave_gate_up(Wg.float())
+    e = torch.nn.functional.silu(xn @ g.t()) * (xn @ u.t())
+    assert rel_err(y, e) < 2e-2
+    Hq, Hkv, D, BS = 32, 8, 128, 64
+    Wq = (torch.randn((Hq + 2 * Hkv) * D, H, device=DEV) / math.sqrt(H)).bfloat16()
+    Wqf = (Wq.float() * gw).bfloat16()
+    nb = (M + BS - 1) // BS + 1
+    pos = torch.randint(0, 8000, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * BS, device=DEV)[:M].to(torch.int32)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, DEV)
+    qkv = (xn.cpu() @ Wq.float().cpu().t()).bfloat16()
+    qr, kr, vr = (torch.zeros(M, Hq, D), torch.zeros(nb, Hkv, BS, D), torch.zeros(nb, Hkv, BS, D))
+    ref.rope_kv(qkv, pos.cpu(), slots.cpu(), cs.cpu(), qr, kr, vr, Hq, Hkv, D)
+    codes = (None, 1, 2, 3, 4, 5) if M >= 256 else (None,)
+    try:
+        for code in codes:
+            if code is not None:
+                L.gemm_plan_set(Wqf.shape[0], H, [code] * 64)
+            q = torch.empty(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+            kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+            vc = torch.zeros_like(kc)
+            ops.qkv_rope(x, Wqf, pos, slots, cs, q, kc, vc, Hq, Hkv, D, ss_in=ss, eps=eps)
+            assert rel_err(q.cpu(), qr) < 2e-2, code
+            assert rel_err(kc.cpu(), kr) < 2e-2 and rel_err(vc.cpu(), vr) < 2e-2, code
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)
+
+
+def test_fused_norm_qkv_fallback_rope_kv(monkeypatch):
+    """QKV through the unfused path (plain GEMM into qkv scratch + rope_kv,
+    MCP_QKV_ROPE_FUSED routing off via a shape the AGPR kernel rejects):
+    rope_kv applies the row scale to q, K and V."""
+    torch.manual_seed(23)
+    M, H, eps = 100, 320, 1e-5              # M > 64: no stream path; K % 128 != 0: no AGPR path
+    Hq, Hkv, D, BS = 4, 2, 128, 64
+    x = torch.randn(M, H, device=DEV).bfloat16()
+    ss = ref.row_sumsq(x.cpu()).to(DEV)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps)
+    W = (torch.randn((Hq + 2 * Hkv) * D, H, device=DEV) / math.sqrt(H)).bfloat16()
+    nb = 2
+    pos = torch.arange(M, device=DEV, dtype=torch.int32)
+    slots = torch.arange(M, device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(512, D, 500000.0, DEV)
+    qkv = (xn.cpu() @ W.float().cpu().t()).bfloat16()
+    qr, kr, vr = (torch.zeros(M, Hq, D), torch.zeros(nb, Hkv, BS, D), torch.zeros(nb, Hkv, BS, D))
+    ref.rope_kv(qkv, pos.cpu(), slots.cpu(), cs.cpu(), qr, kr, vr, Hq, Hkv, D)
+    q = torch.empty(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+    kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    ops.qkv_rope(x, W, pos, slots, cs, q, kc, vc, Hq, Hkv, D, ss_in=ss, eps=eps)
+    assert rel_err(q.cpu(), qr) < 2e-2
+    assert rel_err(kc.cpu(), kr) < 2e-2 and rel_err(vc.cpu(), vr) < 2e-2

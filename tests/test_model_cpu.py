@@ -8,6 +8,7 @@ layer's MLP."""
 import math
 
 import numpy as np
+import pytest
 import torch
 
 from mcp_amd.engine.batch import StepInputs, pack
@@ -50,11 +51,24 @@ def _dense_forward(cfg, w, ids):
     return norm(x, w.final_norm)
 
 
-def test_paged_forward_matches_dense():
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_paged_forward_matches_dense(fused, monkeypatch):
+    """Non-trivial RMSNorm weights; ``fused`` = the fused-norm forward (norm
+    weights folded into Wqkv / W_gate_up, row statistics from the residual
+    GEMMs) or the standalone-RMSNorm forward, against the dense reference of
+    the original (unfolded) weights."""
+    import copy
+    monkeypatch.setenv("MCP_FUSED_NORM", fused)
     torch.manual_seed(0)
     cfg = get_config("tiny")
     w = random_weights(cfg, "cpu", dtype=torch.float32, seed=11, std=0.05)
+    g = torch.Generator().manual_seed(5)
+    for lw in w.layers:
+        lw.attn_norm.copy_(1 + 0.3 * torch.randn(lw.attn_norm.shape, generator=g))
+        lw.mlp_norm.copy_(1 + 0.3 * torch.randn(lw.mlp_norm.shape, generator=g))
+    w_ref = copy.deepcopy(w)                       # the model folds its weights in place
     model = LlamaModel(cfg, w, "cpu")
+    assert model.fused_norm == (fused == "1")
     kv = KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, 16, "cpu", dtype=torch.float32)
     BS = 64
     rng = np.random.default_rng(1)
@@ -90,6 +104,6 @@ def test_paged_forward_matches_dense():
     h = model.forward(pack(step, cfg.group, "cpu"), kv).float()
     assert h.shape == (3, cfg.hidden)
     for s in range(3):
-        exp = _dense_forward(cfg, w, hist[s])[-1]
+        exp = _dense_forward(cfg, w_ref, hist[s])[-1]
         err = ((h[s] - exp).norm() / exp.norm()).item()
         assert err < 1e-4, (s, err)
