@@ -89,7 +89,12 @@ def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
     sum_tokens = max(sum(q_lens), 1)
     while ns > 1 and ns * sum_tokens * hq * 128 * 4 > max_bytes:
         ns //= 2
-    return max(ns, 1)
+    # a power of two: the split count is part of the hipGraph key, and a
+    # handful of values can all be captured at start-up (engine/graphs.py)
+    p2 = 1
+    while p2 * 2 <= ns:
+        p2 *= 2
+    return p2
 
 
 def build_work(q_len: Sequence[int], group: int, small_cutoff: Optional[int] = None):

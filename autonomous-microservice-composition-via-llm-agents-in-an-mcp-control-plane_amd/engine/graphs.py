@@ -96,6 +96,7 @@ class GraphRunner:
         self.replays = 0
         self.captures = 0
         self.capture_s = 0.0
+        self.warmed = False     # warm() ran: split keys are no longer captured lazily
 
     # ---------------------------------------------------------------- layout
     def _seq_cap(self, b: int, sb: Optional[int]) -> int:
@@ -256,14 +257,30 @@ class GraphRunner:
         self.capture_s += time.perf_counter() - t0
         return e
 
+    # split-KV keys captured at start-up: the power-of-two split counts
+    # (batch.choose_kv_splits) of few-sequence decode steps, in the buckets of
+    # such steps; any other split key runs eagerly (no lazy capture on the
+    # request path)
+    WARM_SPLITS = (2, 4, 8)
+    WARM_SPLIT_MAX_TOKENS = 64
+
     def warm(self, max_tokens: Optional[int] = None, contexts: Sequence[int] = (2048,),
              kv_splits: Sequence[int] = (1,)) -> int:
         """Capture every bucket up to ``max_tokens`` for the block-table width
         classes of ``contexts`` (tokens) ahead of serving, so no request waits
-        on a lazy capture.  Returns the number of graphs captured."""
+        on a lazy capture; plus the split-KV keys of small-batch decode
+        (``WARM_SPLITS`` for the smallest sequence class of the buckets up to
+        ``WARM_SPLIT_MAX_TOKENS``).  Returns the number of graphs captured."""
         n0 = self.captures
         widths = sorted({self.width_for((c + BLOCK_SIZE - 1) // BLOCK_SIZE) or self.mblk
                          for c in contexts})
+
+        def cap(key, b, w, sb):
+            if self.bcast is not None:                  # workers capture in lockstep
+                self._launch_tp(key, self.pack_static(None, b, w, sb=sb))
+            else:
+                self._get(key)
+
         for b in self.buckets:
             if max_tokens is not None and b > max_tokens:
                 break
@@ -271,11 +288,16 @@ class GraphRunner:
                 for w in widths:
                     for ns in kv_splits:
                         for casc in (0, 1):
-                            key = (b, sb, w, int(ns), casc)
-                            if self.bcast is not None:      # workers capture in lockstep
-                                self._launch_tp(key, self.pack_static(None, b, w, sb=sb))
-                            else:
-                                self._get(key)
+                            cap((b, sb, w, int(ns), casc), b, w, sb)
+            if b <= self.WARM_SPLIT_MAX_TOKENS and self.device.type == "cuda":
+                sb = self.seq_classes(b)[0]
+                for w in widths:
+                    for ns in self.WARM_SPLITS:
+                        if ns in kv_splits:
+                            continue
+                        for casc in (0, 1):
+                            cap((b, sb, w, int(ns), casc), b, w, sb)
+        self.warmed = True
         return self.captures - n0
 
     def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1) -> Optional[torch.Tensor]:
@@ -295,6 +317,8 @@ class GraphRunner:
             return None
         casc = int(step.pre_tokens > 0 and step.pre_bt is not None and len(step.pre_bt) > 0)
         key = (b, sb, w, int(kv_splits), casc)
+        if kv_splits > 1 and self.warmed and key not in self._b:
+            return None        # an uncommon split key: eager, never a lazy capture mid-serving
         if self.bcast is not None:
             e = self._launch_tp(key, host)
         else:
