@@ -279,7 +279,10 @@ std::vector<std::vector<int>> topo_generations(int n, const std::vector<std::pai
 
 void register_grammar(py::module_& m);     // grammar.cpp
 
+void register_embed(py::module_& m);   // embed.cpp
+
 PYBIND11_MODULE(MODULE_NAME, m) {
+  register_embed(m);
   m.doc() = "native CPU runtime of the MI355X planner engine";
   py::register_exception<OutOfBlocks>(m, "OutOfBlocks", PyExc_RuntimeError);
   py::class_<BlockAllocator>(m, "BlockAllocator")

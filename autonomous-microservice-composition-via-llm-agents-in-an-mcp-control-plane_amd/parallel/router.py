@@ -80,12 +80,18 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     kw = {"num_blocks": cfg.num_blocks} if cfg.num_blocks else {}
     eng = LLMEngine(m, max_batch=cfg.max_batch, max_step_tokens=cfg.max_step_tokens,
                     temperature=cfg.temperature, seed=cfg.seed + idx, **kw)
+    if os.environ.get("MCP_GRAPH_WARM", "1") == "1":
+        # capture the hipGraph buckets before reporting ready: the replica's
+        # first requests replay instead of paying lazy captures
+        eng.warm_graphs(max_tokens=cfg.max_step_tokens)
     if cfg.redis_url:
         registry = RedisRegistry(cfg.redis_url, **({"prefix": cfg.services_prefix}
                                                    if cfg.services_prefix else {}))
     else:
         registry = _VersionedMemoryRegistry(records, version)
     retriever = SchemaIndex(registry, dim=cfg.embed_dim, device=device)
+    retriever.refresh()
+    retriever.start_background()
     from ..planner.tokenizer import tokenizer_for
     planner = LocalPlanner(eng, registry, tokenizer=tokenizer_for(cfg.model),
                            max_nodes=cfg.max_nodes, retriever=retriever,

@@ -133,6 +133,8 @@ class TPPlanner(LocalPlanner):
                         temperature=settings.temperature if temperature is None else temperature,
                         seed=settings.seed, bcast=bc)
         retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)
+        retr.refresh()
+        retr.start_background()
         planner = cls(eng, registry, tokenizer=tokenizer_for(settings.model),
                       max_nodes=settings.max_nodes, retriever=retr,
                       retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)

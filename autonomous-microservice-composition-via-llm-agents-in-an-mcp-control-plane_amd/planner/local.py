@@ -91,6 +91,8 @@ class LocalPlanner(Planner):
             # capture the hipGraph buckets at start-up, not under the first requests
             eng.warm_graphs(max_tokens=settings.max_step_tokens)
         retr = SchemaIndex(registry, dim=settings.embed_dim, device=dev)
+        retr.refresh()                     # embed the registry once, before serving
+        retr.start_background()            # later registrations: incremental, off the engine thread
         tok = tokenizer_for(settings.model)
         if tok.vocab_size > model.cfg.vocab_size:
             raise ValueError(f"tokenizer vocabulary {tok.vocab_size} exceeds the model's "

@@ -61,13 +61,17 @@ class BaseRegistry:
 
 
 class MemoryRegistry(BaseRegistry):
+    CHANGELOG = 65536          # (version, name) entries kept for changes_since
+
     def __init__(self, records: Iterable = (), prefix: str = SERVICES_PREFIX):
+        import collections
         self.prefix = prefix
         self._recs: Dict[str, ServiceRecord] = {}
         self._tel: Dict[str, Dict[str, float]] = {}
         self._version = 0
         self._lock = threading.Lock()
         self._sorted: Optional[List[ServiceRecord]] = None
+        self._log = collections.deque(maxlen=self.CHANGELOG)
         self.register_many(records)
 
     def register(self, rec) -> None:
@@ -75,6 +79,7 @@ class MemoryRegistry(BaseRegistry):
         with self._lock:
             self._recs[rec.name] = rec
             self._version += 1
+            self._log.append((self._version, rec.name))
             self._sorted = None
 
     def unregister(self, name: str) -> bool:
@@ -82,8 +87,21 @@ class MemoryRegistry(BaseRegistry):
             ok = self._recs.pop(name, None) is not None
             if ok:
                 self._version += 1
+                self._log.append((self._version, name))
                 self._sorted = None
             return ok
+
+    def changes_since(self, version: int):
+        """(current version, names registered / re-registered / removed after
+        ``version``) - O(changes), for incremental consumers (the schema
+        index); None when the change log no longer reaches back that far."""
+        with self._lock:
+            cur = self._version
+            if version == cur:
+                return cur, []
+            if not self._log or self._log[0][0] > version + 1:
+                return None
+            return cur, list({nm: None for v, nm in self._log if v > version})
 
     def list_services(self) -> List[ServiceRecord]:
         with self._lock:
