@@ -81,16 +81,25 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
         if planner is not None:
             return planner
         if settings.planner_backend == "local":
+            if settings.replicas > 1:
+                # request-level DP over replicas, each a TP group of
+                # settings.tp ranks (MCP_REPLICAS=2 MCP_TP=4: two TP=4 planners)
+                from ..parallel.router import ReplicaConfig, ReplicaRouter, group_devices
+                cfg = ReplicaConfig(model=settings.model, max_batch=settings.max_batch,
+                                    max_nodes=settings.max_nodes, seed=settings.seed,
+                                    num_blocks=settings.kv_blocks or None,
+                                    max_step_tokens=settings.max_step_tokens,
+                                    temperature=settings.temperature,
+                                    retrieval_threshold=settings.retrieval_threshold,
+                                    topk=settings.topk, embed_dim=settings.embed_dim,
+                                    tp=max(1, int(settings.tp)))
+                return ReplicaRouter(group_devices(settings.replicas, cfg.tp), settings.model,
+                                     registry, config=cfg)
             if settings.tp > 1:
                 # this process becomes TP rank 0 (driver); ranks 1..tp-1 are
                 # spawned worker processes (parallel/tp_serve.py)
                 from ..parallel.tp_serve import TPPlanner
                 return TPPlanner.launch(settings, registry)
-            if settings.replicas > 1:
-                from ..parallel.router import ReplicaRouter, default_devices
-                return ReplicaRouter(default_devices(settings.replicas), settings.model, registry,
-                                     max_batch=settings.max_batch, max_nodes=settings.max_nodes,
-                                     seed=settings.seed)
             from ..planner.local import LocalPlanner
             return LocalPlanner.from_settings(settings, registry)
         if settings.planner_backend == "openai":

@@ -373,6 +373,36 @@ class NativeDecoder {
   }
 };
 
+// Every index the decoder later uses without a bound check (used_[], pos[][],
+// alt_name[][], the live-mask bits, fb_trie[]) is checked once here, so a
+// malformed payload raises ValueError instead of reading out of range.
+void validate(const NativeSpec& sp) {
+  auto need = [](bool ok, const char* what) {
+    if (!ok) throw std::invalid_argument(std::string("grammar spec: ") + what);
+  };
+  const int S = sp.S;
+  need(S >= 1, "S must be >= 1");
+  need(sp.min_nodes >= 1 && sp.max_nodes >= sp.min_nodes, "need 1 <= min_nodes <= max_nodes");
+  need((int)sp.jnames.size() == S, "jnames must hold S names");
+  need((int)sp.name_trie->alts.size() == S, "name_trie must hold S alternatives");
+  need(!sp.retry_trie->alts.empty(), "retry_trie is empty");
+  need(sp.cont_trie->alts.size() == 2, "cont_trie must hold 2 alternatives");
+  need((int)sp.endpoint.size() == S && (int)sp.keys.size() == S && (int)sp.fb_trie.size() == S,
+       "services must hold S entries");
+  for (auto& f : sp.fb_trie) need(!f || f->alts.size() == 2, "a fallback trie must hold 2 alternatives");
+  const int nk = (int)sp.key_first.size();
+  for (auto& k : sp.keys)
+    for (int id : k) need(id >= 0 && id < nk, "key id out of range");
+  for (int k = 0; k < nk; ++k) {
+    const int na = (int)sp.src_trie[k]->alts.size();
+    need(na >= 1, "a source trie is empty");
+    need((int)sp.pos[k].size() == S, "pos[key] must hold S entries");
+    for (int p : sp.pos[k]) need(p >= -1 && p < na, "pos entry out of range");
+    need((int)sp.alt_name[k].size() == na, "alt_name[key] must match the source trie");
+    for (int a : sp.alt_name[k]) need(a >= -1 && a < S, "alt_name entry out of range");
+  }
+}
+
 // spec dict (planner/grammar.py GrammarSpec.native_payload) -> NativeSpec
 std::shared_ptr<NativeSpec> make_spec(const py::dict& d) {
   auto sp = std::make_shared<NativeSpec>();
@@ -411,9 +441,7 @@ std::shared_ptr<NativeSpec> make_spec(const py::dict& d) {
     sp->pos.push_back(k["pos"].cast<std::vector<int>>());
     sp->alt_name.push_back(k["alt_name"].cast<std::vector<int>>());
   }
-  for (auto& k : sp->keys)
-    for (int id : k)
-      if (id < 0 || id >= (int)sp->key_first.size()) throw std::invalid_argument("key id out of range");
+  validate(*sp);
   sp->encode = d["encode"];
   return sp;
 }

@@ -196,5 +196,24 @@ expect(ValueError, rt.grammar_spec, bad)
 bad = spec.native_payload()
 bad["services"][0]["keys"] = [10 ** 6]                           # key id out of range
 expect(ValueError, rt.grammar_spec, bad)
+bad = spec.native_payload()
+bad["keys"] and bad["keys"][0]["pos"].append(0)                # pos row longer than S
+bad["keys"] and expect(ValueError, rt.grammar_spec, bad)
+bad = spec.native_payload()
+bad["cont_trie"] = (["a"], [[1]])                              # cont needs 2 alternatives
+expect(ValueError, rt.grammar_spec, bad)
+
+# ---- feature-hashing embedder (embed.cpp): random ASCII, empty texts, odd dims
+alphabet = "abcXYZ019 _-#.,{}\"\t"
+for _ in range(ITERS):
+    texts = ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 80)))
+             for _ in range(rng.randint(0, 6))]
+    dim = rng.randint(1, 70)
+    out = rt.hash_embed_sums(texts, dim)
+    assert out.shape == (len(texts), dim) and np.isfinite(out).all()
+    for t, row in zip(texts, out):
+        if not any(c.isalnum() for c in t):
+            assert not row.any()
+expect(ValueError, rt.hash_embed_sums, ["x"], 0)
 
 print(f"sanitize_fuzz OK ({ITERS} iterations)")

@@ -6,7 +6,8 @@
 // runtime.cpp in with -fsanitize=address,undefined, registers the module as a
 // built-in (_runtime_san) and embeds the interpreter to run a fuzz script
 // (sanitize_fuzz.py) against it.  Any heap overflow, use-after-free or UB in
-// the allocator, the step packer, the topological sort or the grammar decoder
+// the allocator, the step packer, the topological sort, the grammar decoder or the
+// feature-hashing embedder
 // aborts the run.
 //
 // Build + run: tests/test_runtime_sanitize_cpu.py (host only; GPU sanitizers
@@ -14,6 +15,7 @@
 #define MODULE_NAME _runtime_san
 #include "runtime.cpp"
 #include "grammar.cpp"
+#include "embed.cpp"
 
 #include <pybind11/embed.h>
 

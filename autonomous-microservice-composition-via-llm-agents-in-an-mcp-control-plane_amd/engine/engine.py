@@ -93,6 +93,20 @@ class _Launch:
 _SPIN_WAIT = os.environ.get("MCP_SPIN_WAIT", "0") == "1"
 
 
+def tp_graph_safe(model) -> bool:
+    """TP: workers mirror the driver's graphs, so every collective a bucket
+    runs must be capturable - the all-reduces (K12 / RCCL, not gloo on GPU
+    tensors) and, with sequence parallelism, the reduce-scatter / all-gather
+    pair (``parallel.comm.make_sp_collectives`` tags them)."""
+    from .graphs import BUCKETS
+    safe = getattr(getattr(model, "_allreduce", None), "graph_safe", None)
+    if safe is None or not safe(max(BUCKETS) * model.cfg.hidden * 2):
+        return False
+    if getattr(model, "seq_parallel", False):
+        return all(getattr(f, "graph_safe", False) for f in (model._sp or ()))
+    return True
+
+
 class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
@@ -125,14 +139,7 @@ class LLMEngine:
         if graphs is None:
             graphs = self.device.type == "cuda" and os.environ.get("MCP_GRAPHS", "1") == "1"
             if graphs and getattr(model, "tp", 1) > 1:
-                # TP: workers mirror the driver's graphs; every all-reduce of a
-                # bucket must be capturable (K12 / RCCL, not gloo on GPU tensors)
-                from .graphs import BUCKETS
-                ar = getattr(model, "_allreduce", None)
-                safe = getattr(ar, "graph_safe", None)
-                graphs = (bcast is not None and safe is not None
-                          and safe(max(BUCKETS) * model.cfg.hidden * 2)
-                          and not getattr(model, "seq_parallel", False))
+                graphs = bcast is not None and tp_graph_safe(model)
         self._graphs_wanted = graphs
         self.graphs = None          # engine.graphs.GraphRunner, created after the KV cache
         if num_blocks is not None:
@@ -308,10 +315,11 @@ class LLMEngine:
             seq.prefix_entry.computed = True
         else:
             t_parse = time.perf_counter()
-            try:
-                seq.result = seq.decoder.result()
-            except Exception as e:  # pragma: no cover - grammar guarantees JSON
-                seq.error = repr(e)
+            if seq.error is None:
+                try:
+                    seq.result = seq.decoder.result()
+                except Exception as e:  # pragma: no cover - grammar guarantees JSON
+                    seq.error = repr(e)
             METRICS.observe("parse_s", time.perf_counter() - t_parse)
             METRICS.plan_done(seq.t_done - seq.t_submit)
             # per-request phases: queue (submit -> admitted), first sampled
@@ -544,8 +552,17 @@ class LLMEngine:
             seq.n_samples += 1
             seq.decoder.feed(int(tok))
             seq.pending += seq.decoder.advance()
+        max_pos = getattr(self.model.cfg, "max_pos", None)
         for seq, _ in batch_seqs:
-            if not seq.is_prefix_job and seq.decoder.done and not seq.done:
+            if seq.is_prefix_job or seq.done:
+                continue
+            if seq.decoder.done:
+                self._finish(seq)
+            elif max_pos is not None and seq.num_cached + len(seq.pending) >= max_pos:
+                # the grammar's output does not fit the context left: fail the
+                # request instead of running positions past the RoPE table
+                seq.error = (f"context exhausted: the plan reached the model's {max_pos}-token "
+                             f"limit ({seq.num_cached} cached + {len(seq.pending)} pending)")
                 self._finish(seq)
         self.running = [s for s in self.running if not s.done]
 

@@ -432,8 +432,11 @@ def topk_cosine(queries, corpus, k: int, seg_len: int = 4096, n_valid: Optional[
             return vals, idx
     else:
         if N % 4:
-            raise ValueError("unfused top-k path: pad the corpus rows to a multiple of 4 "
-                             "once at index build (retrieval.store.SchemaIndex does)")
+            # the scoring GEMM writes 16-B column groups: pad a copy (slow path;
+            # the indexes pad once at build, retrieval.store / retrieval.sharded)
+            corpus = torch.cat([corpus, corpus.new_zeros(4 - N % 4, corpus.shape[1])])
+            n_valid = N if n_valid is None else n_valid
+            N = corpus.shape[0]
         vals = torch.empty(B, N, device=queries.device, dtype=torch.float32)
         L_.gemm_f32out(queries, corpus, vals)
         if n_valid is not None and n_valid < N:

@@ -162,7 +162,11 @@ def make_sp_collectives(group, device):
     move the same bytes as the all-reduce they replace (C1/C2), but the
     residual stream and the RMSNorms in between touch only ``Tp`` rows per rank.
     GPU: the direct RCCL communicator; CPU: gloo in fp32 (gloo has no
-    reduce-scatter, so it is all-reduce + slice there)."""
+    reduce-scatter, so it is all-reduce + slice there).
+
+    Each function carries ``graph_safe``: whether it can be captured in a
+    hipGraph (RCCL on the capture stream is; gloo is host code and is not),
+    which is what lets the engine capture sequence-parallel steps."""
     device = torch.device(device)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     if device.type != "cuda":
@@ -176,7 +180,7 @@ def make_sp_collectives(group, device):
             parts = [torch.empty_like(x, dtype=torch.float32) for _ in range(world)]
             dist.all_gather(parts, x.float().contiguous(), group=group)
             return torch.cat(parts).to(x.dtype)
-        return cpu_rs, cpu_ag
+        return _tag(cpu_rs, cpu_ag, safe=False)
     if os.environ.get("MCP_COMM", "native") == "native":
         comm = NativeComm(group, device)
 
@@ -185,7 +189,7 @@ def make_sp_collectives(group, device):
 
         def gpu_ag(x: torch.Tensor) -> torch.Tensor:
             return comm.all_gather(x).view(world * x.shape[0], *x.shape[1:])
-        return gpu_rs, gpu_ag
+        return _tag(gpu_rs, gpu_ag, safe=True)
 
     def torch_rs(y: torch.Tensor) -> torch.Tensor:
         out = y.new_empty(y.shape[0] // world, *y.shape[1:])
@@ -196,7 +200,12 @@ def make_sp_collectives(group, device):
         out = x.new_empty(world * x.shape[0], *x.shape[1:])
         dist.all_gather_into_tensor(out, x.contiguous(), group=group)
         return out
-    return torch_rs, torch_ag
+    return _tag(torch_rs, torch_ag, safe=not _is_gloo(group))
+
+
+def _tag(rs, ag, safe: bool):
+    rs.graph_safe = ag.graph_safe = safe
+    return rs, ag
 
 
 class StepBroadcaster:

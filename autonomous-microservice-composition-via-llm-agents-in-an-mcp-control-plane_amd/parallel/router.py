@@ -26,6 +26,15 @@ its own device) and implements the planner interface:
   ``max_respawns`` times per slot); a request that exceeds
   ``request_timeout`` fails with TimeoutError (HTTP 500 at the API).
 
+Replicas of TP groups (``tp > 1``, e.g. 2 replicas of a TP=4 planner on one
+8-GPU node): each replica is a group of ``tp`` processes with its own process
+group on its own rendezvous port - the replica process is TP rank 0, the
+driver (``LLMEngine(bcast=...)`` as in ``parallel.tp_serve``), and the router
+spawns ranks 1..tp-1 as ``tp_serve`` workers next to it.  A group is one
+failure unit: when any of its processes dies (or the driver stops sending
+heartbeats with requests in flight - a rank lost mid-collective hangs the
+others), every process of the group is killed and the group is respawned.
+
 Queues carry only intent strings, registry records and DAG dicts produced by
 this process tree.
 """
@@ -59,11 +68,20 @@ class ReplicaConfig:
     redis_url: Optional[str] = None     # replicas read Redis themselves when set
     services_prefix: Optional[str] = None
     heartbeat_s: float = 0.5
+    tp: int = 1                         # ranks per replica (TP group size)
+    tp_backend: Optional[str] = None    # default: nccl (RCCL) on GPUs, gloo on CPU
+    full_weights_seed: Optional[int] = None   # tests: shard one full init (tp_serve.build_rank)
+
+
+def _backend(cfg: ReplicaConfig, device: str) -> str:
+    return cfg.tp_backend or ("nccl" if device.startswith("cuda") else "gloo")
 
 
 def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, version: int,
-                  inq, outq):
-    """Replica process: owns one engine; plans batches of whatever is queued."""
+                  inq, outq, port: Optional[int] = None):
+    """Replica process: owns one engine; plans batches of whatever is queued.
+    With ``cfg.tp > 1`` it is rank 0 (the driver) of its group's process
+    group at ``port``; the router has spawned the other ranks."""
     import torch
     from ..engine.engine import LLMEngine
     from ..models.llama import LlamaModel
@@ -72,14 +90,30 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     from ..retrieval.store import SchemaIndex
     if device.startswith("cuda"):
         torch.cuda.set_device(torch.device(device))
-    if os.path.isdir(cfg.model):                       # an HF checkpoint directory
-        from ..models.weights import model_from_checkpoint
-        m = model_from_checkpoint(cfg.model, device)
+    bcast = None
+    if cfg.tp > 1:
+        import torch.distributed as dist
+        from .tp_serve import build_rank
+        backend = _backend(cfg, device)
+        kwd = {"device_id": torch.device(device)} if backend == "nccl" else {}
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=cfg.tp, **kwd)
+        m, nb, bcast = build_rank(cfg.model, 0, cfg.tp, device, cfg.seed, cfg.num_blocks,
+                                  cfg.full_weights_seed)
+        kw = {"num_blocks": nb}
     else:
-        m = LlamaModel.random(cfg.model, device, seed=cfg.seed)
-    kw = {"num_blocks": cfg.num_blocks} if cfg.num_blocks else {}
+        if os.path.isdir(cfg.model):                   # an HF checkpoint directory
+            from ..models.weights import model_from_checkpoint
+            m = model_from_checkpoint(cfg.model, device)
+        elif cfg.full_weights_seed is not None:
+            from ..models.llama import get_config, random_weights
+            mc = get_config(cfg.model)
+            m = LlamaModel(mc, random_weights(mc, device, seed=cfg.full_weights_seed), device)
+        else:
+            m = LlamaModel.random(cfg.model, device, seed=cfg.seed)
+        kw = {"num_blocks": cfg.num_blocks} if cfg.num_blocks else {}
     eng = LLMEngine(m, max_batch=cfg.max_batch, max_step_tokens=cfg.max_step_tokens,
-                    temperature=cfg.temperature, seed=cfg.seed + idx, **kw)
+                    temperature=cfg.temperature, seed=cfg.seed + idx, bcast=bcast, **kw)
     if os.environ.get("MCP_GRAPH_WARM", "1") == "1":
         # capture the hipGraph buckets before reporting ready: the replica's
         # first requests replay instead of paying lazy captures
@@ -106,6 +140,11 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
             item = None
         while item is not None:
             if item == "stop":
+                if bcast is not None:                  # release the worker ranks
+                    import torch.distributed as dist
+                    retriever.stop_background()
+                    eng.shutdown_workers()
+                    dist.destroy_process_group()
                 return
             if item[0] == "registry":                  # ("registry", version, records)
                 registry.replace(item[2], item[1])
@@ -156,7 +195,10 @@ class _VersionedMemoryRegistry:
 
 
 class ReplicaRouter(Planner):
-    def __init__(self, devices: List[str], model: str, registry, max_batch: int = 256,
+    """``devices``: one device per replica (``tp = 1``), or one list of
+    ``tp`` devices per replica (replicas of TP groups, ``group_devices``)."""
+
+    def __init__(self, devices: List, model: str, registry, max_batch: int = 256,
                  max_nodes: int = 6, seed: int = 0, num_blocks: Optional[int] = None,
                  request_timeout: float = 120.0, start_timeout: float = 600.0,
                  watchdog_s: float = 60.0, max_respawns: int = 3,
@@ -166,9 +208,13 @@ class ReplicaRouter(Planner):
         self.start_timeout = start_timeout
         self.watchdog_s = watchdog_s
         self.max_respawns = max_respawns
-        self.devices = list(devices)
+        self.groups = [[d] if isinstance(d, str) else list(d) for d in devices]
+        self.devices = [g[0] for g in self.groups]    # each replica's driver device
         cfg = config or ReplicaConfig(model=model, max_batch=max_batch, max_nodes=max_nodes,
-                                      seed=seed, num_blocks=num_blocks)
+                                      seed=seed, num_blocks=num_blocks,
+                                      tp=len(self.groups[0]) if self.groups else 1)
+        if any(len(g) != cfg.tp for g in self.groups):
+            raise ValueError(f"every replica needs tp={cfg.tp} devices, got {self.groups}")
         from ..registry import RedisRegistry
         if isinstance(registry, RedisRegistry) and not cfg.redis_url:
             cfg = dataclasses.replace(cfg, redis_url=registry.client.url, services_prefix=registry.prefix)
@@ -178,6 +224,7 @@ class ReplicaRouter(Planner):
         n = len(devices)
         self._inqs: List = [None] * n
         self._procs: List = [None] * n
+        self._workers: List[List] = [[] for _ in range(n)]   # TP ranks 1..tp-1 per replica
         self.alive = [False] * n
         self.respawns = [0] * n
         self._last_msg = [time.monotonic()] * n
@@ -200,7 +247,8 @@ class ReplicaRouter(Planner):
                     self._last_msg[idx] = time.monotonic()
             except queue.Empty:
                 for i, p in enumerate(self._procs):
-                    if not p.is_alive():
+                    if not self._group_alive(i):
+                        self._kill_group(i)
                         raise RuntimeError(f"replica {i} died during start-up")
         self._thread = threading.Thread(target=self._pump, daemon=True, name="mcp-router")
         self._thread.start()
@@ -215,11 +263,39 @@ class ReplicaRouter(Planner):
     def _spawn(self, i: int):
         version, recs = self._snapshot()
         q = self._ctx.Queue()
+        port = None
+        workers = []
+        if self.cfg.tp > 1:
+            from .launch import free_port
+            from .tp_serve import _worker_main
+            port = free_port()
+            env = {k: v for k, v in os.environ.items() if k.startswith(("MCP_", "HSA_"))}
+            for r in range(1, self.cfg.tp):
+                dev = self.groups[i][r]
+                w = self._ctx.Process(target=_worker_main, daemon=True,
+                                      args=(r, self.cfg.tp, port, dev, _backend(self.cfg, dev),
+                                            self.cfg.model, self.cfg.seed, self.cfg.num_blocks,
+                                            env, self.cfg.full_weights_seed))
+                w.start()
+                workers.append(w)
         p = self._ctx.Process(target=_replica_main, daemon=True,
-                              args=(i, self.devices[i], self.cfg, recs, version, q, self._outq))
+                              args=(i, self.devices[i], self.cfg, recs, version, q, self._outq,
+                                    port))
         p.start()
-        self._inqs[i], self._procs[i] = q, p
+        self._inqs[i], self._procs[i], self._workers[i] = q, p, workers
         self._last_msg[i] = time.monotonic()
+
+    def _group_alive(self, i: int) -> bool:
+        p = self._procs[i]
+        return p is not None and p.is_alive() and all(w.is_alive() for w in self._workers[i])
+
+    def _kill_group(self, i: int):
+        for proc in [self._procs[i]] + self._workers[i]:
+            if proc is not None and proc.is_alive():
+                proc.kill()
+        for proc in [self._procs[i]] + self._workers[i]:
+            if proc is not None:
+                proc.join(timeout=10)
 
     # -------------------------------------------------------------- routing
     def _pick(self) -> int:
@@ -279,14 +355,14 @@ class ReplicaRouter(Planner):
         for i, p in enumerate(self._procs):
             if p is None:
                 continue
-            dead = not p.is_alive()
+            dead = not self._group_alive(i)
             hung = (not dead and self.alive[i] and self.inflight[i]
                     and now - self._last_msg[i] > self.watchdog_s)
             if not dead and not hung:
                 continue
-            if hung:                                  # stalled GPU step: replace the process
-                p.kill()
-                p.join(timeout=10)
+            # a dead rank leaves the rest of its group blocked in a collective,
+            # a stalled step leaves the whole group hung: replace every process
+            self._kill_group(i)
             was_live = self.alive[i]
             with self._lock:
                 self.alive[i] = False
@@ -322,16 +398,18 @@ class ReplicaRouter(Planner):
         self._procs[i].kill()
 
     async def aclose(self):
+        self.close()
+
+    def close(self):
         self._stop.set()
         for q, p in zip(self._inqs, self._procs):
             if p is not None and p.is_alive():
                 q.put("stop")
-        for p in self._procs:
-            if p is None:
-                continue
-            p.join(timeout=10)
-            if p.is_alive():
-                p.kill()
+        for i, p in enumerate(self._procs):
+            for proc in ([p] if p is not None else []) + self._workers[i]:
+                proc.join(timeout=30)
+                if proc.is_alive():
+                    proc.kill()
 
 
 def _resolve(fut, val, exc):
@@ -348,3 +426,20 @@ def default_devices(n: int) -> List[str]:
     if torch.cuda.is_available():
         return [f"cuda:{i}" for i in range(min(n, torch.cuda.device_count()))]
     return ["cpu"] * n
+
+
+def group_devices(replicas: int, tp: int) -> List:
+    """Device groups for ``replicas`` TP groups of ``tp`` ranks: replica i
+    takes GPUs i*tp .. i*tp+tp-1 (contiguous, so a TP=4 group sits on one
+    xGMI-adjacent half of the node); plain device strings when tp == 1.
+    Counting devices does not initialise HIP, so the router can still spawn
+    its children afterwards."""
+    import torch
+    if tp <= 1:
+        return default_devices(replicas)
+    n = torch.cuda.device_count()
+    if n == 0:
+        return [["cpu"] * tp for _ in range(replicas)]
+    if replicas * tp > n:
+        raise RuntimeError(f"{replicas} replicas x TP={tp} need {replicas * tp} GPUs, found {n}")
+    return [[f"cuda:{i * tp + r}" for r in range(tp)] for i in range(replicas)]

@@ -92,3 +92,28 @@ def test_spec_decoder_factory(monkeypatch):
     spec2 = GrammarSpec(reg, get_tokenizer(), max_nodes=2)
     assert isinstance(spec2.decoder(), DagDecoder)
     json.dumps(spec.native_payload()["chunks"])        # the payload is plain data (+ encode)
+
+
+@pytest.mark.parametrize("corrupt", [
+    lambda p: p["keys"][0]["pos"].append(0),                       # pos row longer than S
+    lambda p: p["keys"][0]["pos"].__setitem__(0, 10 ** 4),         # pos entry past the trie
+    lambda p: p["keys"][0]["alt_name"].pop(),                      # alt_name shorter than the trie
+    lambda p: p["keys"][0]["alt_name"].__setitem__(0, 10 ** 4),    # alt_name names no service
+    lambda p: p.__setitem__("cont_trie", (["a"], [[1]])),          # continue needs 2 alternatives
+    lambda p: p["services"].pop(),                                 # fewer services than S
+    lambda p: p.__setitem__("jnames", p["jnames"][:-1]),
+    lambda p: p.__setitem__("min_nodes", 0),
+    lambda p: p["services"][0].__setitem__("fallback", (["x"], [[5]])),  # 1-alternative fallback
+])
+def test_native_spec_rejects_malformed_payload(corrupt):
+    """Malformed payloads raise ValueError at spec build time instead of
+    indexing out of range later inside the decoder."""
+    reg = [dict(s) for s in synthetic_registry(5, seed=2)]
+    reg[1]["input_schema"] = {"type": "object", "properties": {"q": {"type": "string"}}}
+    spec = GrammarSpec(reg, get_tokenizer(), max_nodes=3)
+    p = spec.native_payload()
+    assert p["keys"], "the registry must give at least one input key"
+    native._RT.grammar_spec(p)                                     # the intact payload builds
+    corrupt(p)
+    with pytest.raises(ValueError):
+        native._RT.grammar_spec(p)

@@ -318,6 +318,23 @@ def test_topk_cosine(B, N, D, k, fused):
     assert (vals[:, :-1] >= vals[:, 1:]).all()
 
 
+@pytest.mark.parametrize("B,N,D", [(70, 1001, 1024), (3, 4099, 256)])
+def test_topk_cosine_unpadded_corpus_unfused(B, N, D):
+    """The unfused scoring path (B > 64, or D outside {512, 1024}) on a corpus
+    whose row count is not a multiple of 4 pads a copy instead of raising."""
+    torch.manual_seed(3)
+    corpus = torch.randn(N, D, device=DEV).bfloat16()
+    ops.l2norm_rows(corpus)
+    q = torch.randn(B, D, device=DEV).bfloat16()
+    ops.l2norm_rows(q)
+    vals, idx = ops.topk_cosine(q, corpus, 16, fused=False)
+    assert int(idx.max()) < N and int(idx.min()) >= 0
+    ref_s = q.float() @ corpus.float().t()
+    rv, _ = torch.topk(ref_s, k=16, dim=-1)
+    assert torch.allclose(vals, rv, atol=1e-4)
+    assert torch.allclose(ref_s.gather(1, idx.long()), rv, atol=1e-4)
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
 @pytest.mark.parametrize("kv_splits", [1, 4])
 @pytest.mark.parametrize("prefix_split", ["0", "-1", "3"])

@@ -402,3 +402,35 @@ def test_launch_ahead_matches_plain_submit():
         assert eng.alloc.num_free == eng.kv.num_blocks and not eng.inflight
         out.append([s.result for s in seqs])
     assert out[0] == out[1]
+
+
+def test_context_exhaustion_fails_the_request():
+    """A plan that would run past the model's max_pos fails with a clear error
+    (no step is ever issued at positions beyond the RoPE table), the blocks go
+    back to the allocator and the engine keeps serving."""
+    import dataclasses
+    from mcp_amd.models.llama import get_config, random_weights
+    reg = MemoryRegistry(synthetic_registry(4, seed=3))
+    cfg = get_config("tiny")
+    probe = LocalPlanner(LLMEngine(LlamaModel(cfg, random_weights(cfg, "cpu", seed=1), "cpu"),
+                                   num_blocks=64, max_batch=4, graphs=False), reg, max_nodes=3)
+    _, ptoks, stoks = probe.prepare("charge the order")
+    n_prompt = len(ptoks) + len(stoks)
+    small = dataclasses.replace(cfg, max_pos=n_prompt + 6)
+    eng = LLMEngine(LlamaModel(small, random_weights(small, "cpu", seed=1), "cpu"),
+                    num_blocks=64, max_batch=4, temperature=0.0, graphs=False)
+    seen = []
+    real_step = eng.step
+
+    def step():
+        for s in eng.running:
+            seen.append(s.num_cached + len(s.pending))
+        return real_step()
+    eng.step = step
+    planner = LocalPlanner(eng, reg, max_nodes=3)
+    free0 = eng.alloc.num_free
+    with pytest.raises(RuntimeError, match="context exhausted"):
+        planner.plan_many(["charge the order"])
+    assert max(seen) <= small.max_pos
+    assert eng.alloc.num_free == free0 and not eng.running
+    planner._stop.set()

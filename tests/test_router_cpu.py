@@ -92,3 +92,59 @@ def test_router_large_registry_is_retrieval_bounded():
             validate_dag(d, names)
         await router.aclose()
     asyncio.run(go())
+
+
+@pytest.mark.timeout(900)
+def test_router_replicas_of_tp_groups_match_local_planner(monkeypatch):
+    """2 replicas x a gloo TP=2 group (4 processes: each replica is the TP
+    driver, the router spawns its worker rank) plan exactly what one
+    ``LocalPlanner`` on the unsharded weights plans at temperature 0; losing a
+    worker rank takes its whole group down, the group is respawned and serves
+    again."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    from mcp_amd.engine.engine import LLMEngine
+    from mcp_amd.models.llama import LlamaModel, get_config, random_weights
+    from mcp_amd.parallel.router import group_devices
+    from mcp_amd.planner.local import LocalPlanner
+    reg = MemoryRegistry(synthetic_registry(5, seed=9))
+    names = [s.name for s in reg.list_services()]
+    intents = [synthetic_intent(i) for i in range(4)]
+    cfg = ReplicaConfig(model="tiny-tp", max_batch=8, max_nodes=3, num_blocks=256,
+                        temperature=0.0, tp=2, full_weights_seed=5, max_step_tokens=2048)
+    groups = group_devices(2, 2)
+    assert groups == [["cpu", "cpu"], ["cpu", "cpu"]]
+    router = ReplicaRouter(groups, "tiny-tp", reg, request_timeout=600, config=cfg)
+    used = set()
+    real_dispatch = router._dispatch
+
+    def dispatch(rid, intent):
+        real_dispatch(rid, intent)
+        used.update(i for i, d in router.inflight.items() if rid in d)
+    router._dispatch = dispatch
+
+    async def go():
+        dags = await asyncio.gather(*[router.plan(x) for x in intents])
+        assert all(len(w) == 1 and w[0].is_alive() for w in router._workers)
+        router._workers[1][0].kill()                  # a worker rank of replica 1 dies
+        t0 = time.time()
+        while router.respawns[1] == 0 and time.time() - t0 < 60:
+            await asyncio.sleep(0.2)
+        t0 = time.time()
+        while not all(router.alive) and time.time() - t0 < 300:
+            await asyncio.sleep(0.2)
+        assert router.respawns == [0, 1] and router.alive == [True, True]
+        router.inflight[0]["pin"] = "x"              # route the next plan to replica 1
+        again = await router.plan(intents[0])
+        router.inflight[0].pop("pin")
+        await router.aclose()
+        return dags, again
+    dags, again = asyncio.run(go())
+    assert used == {0, 1}
+    for d in dags:
+        validate_dag(d, names)
+    mc = get_config("tiny-tp")
+    eng = LLMEngine(LlamaModel(mc, random_weights(mc, "cpu", seed=5), "cpu"), num_blocks=256,
+                    max_batch=8, max_step_tokens=2048, temperature=0.0)
+    ref = LocalPlanner(eng, reg, max_nodes=3).plan_many(intents)
+    assert dags == ref
+    assert again == ref[0]
