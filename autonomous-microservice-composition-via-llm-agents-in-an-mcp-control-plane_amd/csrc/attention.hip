@@ -460,6 +460,169 @@ void attn_kernel(const AttnArgs a) {
   }
 }
 
+// Shared-prefix pass with RT row tiles per wave.  The one-tile form
+// (attn_kernel MODE 1) reads the whole 32 KiB K|V tile from LDS per 16 query
+// rows: 1 KiB of LDS reads per 16x16x32 MFMA, so the four SIMDs of a CU ask
+// for ~4x the LDS port at MFMA peak and the pass ran at ~0.5 PF/s.  Here each
+// K fragment (S^T = K Q^T) and each transposed V fragment (O^T += V^T P^T)
+// read from LDS feeds RT MFMAs, one per row tile, which cuts the LDS bytes
+// per FLOP by RT.  Every query of the pass sits after the prefix, so there is
+// no mask (pre_keys is a multiple of 64).  Same row layout, online softmax,
+// swizzled double-buffered LDS-DMA ring and outputs (normalised O + LSE) as
+// MODE 1; the key-split form for few tokens stays on attn_kernel.
+template <int NW, int G, int RT>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(RT >= 4 ? 1 : 2)))
+void attn_prefix_kernel(const AttnArgs a) {
+  constexpr int TPT = 16 / G;                 // tokens per 16-row tile
+  constexpr int QT = NW * RT * TPT;           // tokens per block
+  constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
+  static_assert(PIECES % NW == 0, "pieces split evenly");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];   // [buf][K|V][64][128]
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kvh = a.head_major ? blockIdx.x : blockIdx.y;
+  const int qblk = a.head_major ? blockIdx.y : blockIdx.x;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int head = kvh * G + fr % G;
+  const int Hq = a.Hq, Hkv = a.Hkv;
+  const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
+  const int pre_keys = a.pre_dims ? a.pre_dims[1] : a.pre_keys;
+  if (qblk * QT >= pre_tokens) return;        // whole block idle (before any barrier)
+  const int ntiles = pre_keys / KT;
+
+  int tok[RT];
+  bf16x8 qf[RT][4];                           // B operands: Q[row fr][d = 32ks + 8fq + j]
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    tok[r] = qblk * QT + (wave * RT + r) * TPT + fr / G;
+    const bool v = tok[r] < pre_tokens;
+    const bf16* qp = a.q + ((size_t)(v ? tok[r] : 0) * Hq + head) * D + 8 * fq;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qf[r][ks] = *reinterpret_cast<const bf16x8*>(qp + 32 * ks);
+      if (!v) qf[r][ks] = bf16x8{};
+    }
+  }
+
+  const int srow = lane >> 4;
+  auto stage = [&](int kt, int buf) {
+    const size_t blk = (size_t)a.pre_bt[kt];
+    const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
+    const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
+    bf16* base = smem + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < PIECES / NW; ++i) {
+      const int p = wave * (PIECES / NW) + i;
+      const int tile = p >> 4, pr = p & 15;
+      const int row = pr * 4 + srow;
+      const int chunk = (lane & 15) ^ (row & 15);
+      glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
+    }
+  };
+
+  f32x4 o[RT][8];
+  float m_run[RT], l_part[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[r][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run[r] = -INFINITY;
+    l_part[r] = 0.f;
+  }
+
+  if (ntiles > 0) stage(0, 0);
+  __syncthreads();
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
+    const bf16* Kl = smem + cur * 2 * TILE;
+    const bf16* Vl = Kl + TILE;
+
+    // ---- S^T = K Q^T: each K fragment feeds the RT row tiles
+    f32x4 sacc[RT][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) sacc[r][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int row = nt * 16 + fr;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c = ks * 4 + fq;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * D + ((c ^ (row & 15)) << 3));
+#pragma unroll
+        for (int r = 0; r < RT; ++r) sacc[r][nt] = mfma16x16x32(kf, qf[r][ks], sacc[r][nt]);
+      }
+    }
+    // ---- online softmax per row tile (lane: query row fr, keys 16nt + 4fq + r)
+    bf16x8 pf[RT][2];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sacc[r][nt][e] *= a.scale_log2;
+          tmax = fmaxf(tmax, sacc[r][nt][e]);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_run[r], tmax);
+      const float alpha = exp2f(m_run[r] - m_new);
+      m_run[r] = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = exp2f(sacc[r][nt][e] - m_new);
+          psum += p;
+          pf[r][nt >> 1][(nt & 1) * 4 + e] = (bf16)p;
+        }
+      l_part[r] = l_part[r] * alpha + psum;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
+    }
+    // ---- O^T += V^T P^T: each transposed V fragment feeds the RT row tiles
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int col = dt * 16 + tp * 4;
+      const int chunk = col >> 3, half = (col & 7);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int key0 = k2 * 32 + fq * 4 + tq;
+        const int key1 = key0 + 16;
+        const bf16x4 v0 = tr_read(Vl + key0 * D + ((chunk ^ (key0 & 15)) << 3) + half);
+        const bf16x4 v1 = tr_read(Vl + key1 * D + ((chunk ^ (key1 & 15)) << 3) + half);
+        const bf16x8 vf = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int r = 0; r < RT; ++r) o[r][dt] = mfma16x16x32(vf, pf[r][k2], o[r][dt]);
+      }
+    }
+    __syncthreads();             // its fence also drains the next tile's LDS-DMA
+  }
+
+  // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + e]
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    float l_tot = l_part[r] + __shfl_xor(l_part[r], 16, 64);
+    l_tot += __shfl_xor(l_tot, 32, 64);
+    if (tok[r] >= pre_tokens) continue;
+    const size_t row = (size_t)tok[r] * Hq + head;
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    if (fq == 0) a.lse_out[row] = m_run[r] + __log2f(l_tot);
+    bf16* op = a.out + row * D + 4 * fq;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      bf16x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[r][dt][e] * inv);
+      *reinterpret_cast<bf16x4*>(op + dt * 16) = w;
+    }
+  }
+}
+
 // Merge of the split-KV partials of 1-wave items: one workgroup per (item,
 // kv head) = 16 rows (TPW tokens x G heads).  Wave w takes splits w, w + 4,
 // ...; lane = (row l & 15, 32-wide d slice).  Each wave keeps its own running
@@ -666,6 +829,24 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
     attn_kernel<8, G, 1, 0, true><<<grid, 512, 0, s>>>(a);
     const long long n = (long long)a.pre_tokens * a.Hq * (D / 8);
     attn_prefix_combine<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, nsplit);
+    return;
+  }
+  // MCP_ATTN_PREFIX_RT: row tiles per wave of the prefix pass (2 = default,
+  // 1 = the attn_kernel MODE 1 forms below, A/B)
+  // (read per launch: the GPU tests compare the forms in one process)
+  const char* rt_env = getenv("MCP_ATTN_PREFIX_RT");
+  const int rt = rt_env ? atoi(rt_env) : 2;
+  if (rt == 2 || rt == 4) {
+    auto grid_for = [&](int qt) {
+      const int nblk = (a.pre_tokens + qt - 1) / qt;
+      return a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
+    };
+    if (rt == 4)
+      attn_prefix_kernel<4, G, 4><<<grid_for(4 * 4 * (16 / G)), 256, 0, s>>>(a);
+    else if (prefix_nw() == 4)
+      attn_prefix_kernel<4, G, 2><<<grid_for(4 * 2 * (16 / G)), 256, 0, s>>>(a);
+    else
+      attn_prefix_kernel<8, G, 2><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     return;
   }
   if (prefix_nw() == 4) {

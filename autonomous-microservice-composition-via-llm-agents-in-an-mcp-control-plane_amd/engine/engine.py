@@ -57,6 +57,12 @@ class Sequence:
         self.blocks: List[int] = []
         self.num_cached = 0                    # tokens whose KV is in this sequence's blocks
         self.pending: List[int] = list(prompt_tokens)
+        # every token of the request after its shared prefix (prompt + grammar
+        # output); ``pending`` is always a suffix of it - a preempted request
+        # recomputes prefix + tokens
+        self.tokens: List[int] = list(prompt_tokens)
+        self.base = 0                          # leading tokens (shared prefix) not in `tokens`
+        self.evicted = False                   # preempted during the current schedule
         self.n_samples = 0
         self.done = False
         self.result = None
@@ -69,7 +75,9 @@ class Sequence:
         self.is_prefix_job = decoder is None
         self.cohort = 0                        # launch cohort (pipelined engine)
         if decoder is not None:
-            self.pending += decoder.advance()
+            first = decoder.advance()
+            self.pending += first
+            self.tokens += first
 
     @property
     def wants_sample(self) -> bool:
@@ -163,7 +171,7 @@ class LLMEngine:
             self.graphs = GraphRunner(model, self.kv, temperature, seed, max_seqs=max_batch,
                                       bcast=bcast)
         self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "graph_cow_steps": 0,
-                      "graph_split_steps": 0, "kv_split_steps": 0,
+                      "graph_split_steps": 0, "kv_split_steps": 0, "preemptions": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
@@ -186,7 +194,12 @@ class LLMEngine:
             while len(self.prefixes) >= self.max_prefixes:   # evict the LRU entry
                 old = next(iter(self.prefixes))
                 self.alloc.free(self.prefixes.pop(old).blocks)
-            blocks = self.alloc.alloc((len(tokens) + BLOCK_SIZE - 1) // BLOCK_SIZE)
+            need = (len(tokens) + BLOCK_SIZE - 1) // BLOCK_SIZE
+            # a full pool: drop cached prefixes before giving up sharing -
+            # with retrieval every request may bring its own prefix
+            if not self._evict_prefixes(need):
+                return None             # the request carries its whole prompt instead
+            blocks = self.alloc.alloc(need)
             e = PrefixEntry(tokens=tokens, blocks=blocks, length=len(tokens))
             self.prefixes[tokens] = e
             job = Sequence(None, list(tokens))
@@ -196,6 +209,61 @@ class LLMEngine:
             self.waiting.insert(0, job)
         self._last_prefix = (src, e)
         return e
+
+    def _evict_prefixes(self, need: int) -> bool:
+        """Drop cached prefix entries, least recently used first, until
+        ``need`` blocks are free (requests still using a prefix keep its
+        blocks alive).  Returns whether they are."""
+        a = self.alloc
+        while a.num_free < need and self.prefixes:
+            old = next(iter(self.prefixes))
+            a.free(self.prefixes.pop(old).blocks)
+        return a.num_free >= need
+
+    def _alloc_pressure(self, need: int, protect: set) -> Optional[List[int]]:
+        """``need`` blocks when the pool is short: evict cached prefixes, then
+        preempt running requests (most recently admitted first) that are
+        neither in ``protect`` (this step's batch) nor in a launch still in
+        flight.  None when even that does not free enough."""
+        if not self._evict_prefixes(need):
+            busy = set(protect)
+            for L in self.inflight.values():
+                busy.update(id(q) for q, _ in L.batch_seqs)
+            for seq in reversed(self.running):
+                if self.alloc.num_free >= need:
+                    break
+                if seq.is_prefix_job or seq.evicted or not seq.blocks or id(seq) in busy:
+                    continue
+                self._preempt(seq)
+            if self.alloc.num_free < need:
+                return None
+        return self.alloc.alloc(need)
+
+    def _preempt(self, seq: Sequence):
+        """Preemption by recompute: keep the shared full blocks of the
+        request's prefix, free the rest and queue it at the front of
+        ``waiting`` with everything after them (the prefix's partial tail
+        block + its own tokens) pending again; its grammar state and sample
+        counter carry on."""
+        keep = seq.base // BLOCK_SIZE
+        head = list(seq.prefix.tokens[keep * BLOCK_SIZE:seq.base]) if seq.base % BLOCK_SIZE else []
+        self.alloc.free(seq.blocks[keep:])
+        del seq.blocks[keep:]
+        seq.pending = head + seq.tokens
+        seq.tokens = list(seq.pending)
+        seq.base = seq.num_cached = keep * BLOCK_SIZE
+        seq.prefix = None                      # no cascade for it: its keys are its own
+        seq.evicted = True
+        self.running.remove(seq)
+        self.waiting.insert(0, seq)
+        self.stats["preemptions"] += 1
+
+    def _blocks_to_admit(self, seq: Sequence) -> int:
+        """Blocks a waiting request needs for the tokens it already has."""
+        if seq.materialized:
+            return (seq.num_cached + len(seq.pending) + BLOCK_SIZE - 1) // BLOCK_SIZE - len(seq.blocks)
+        e = seq.prefix                         # shares e's full blocks, copies the tail
+        return (e.length + len(seq.pending) + BLOCK_SIZE - 1) // BLOCK_SIZE - e.length // BLOCK_SIZE
 
     def drop_prefixes(self):
         """Release prefix entries (their blocks stay alive while requests use them)."""
@@ -209,14 +277,20 @@ class LLMEngine:
         the partial tail block (device copy queued before the next forward)."""
         e = seq.prefix
         n_full, tail = divmod(e.length, BLOCK_SIZE)
+        nb = None
+        if tail:
+            got = self.alloc.alloc(1) if self.alloc.num_free else self._alloc_pressure(1, set())
+            if got is None:
+                return False                   # pool exhausted: retry on a later step
+            nb = got[0]
         seq.blocks = list(e.blocks[:n_full])
         if tail:
-            nb = self.alloc.alloc(1)[0]
             copies.append((e.blocks[-1], nb))
             seq.blocks.append(nb)
             self.alloc.free([e.blocks[-1]])    # the reference taken at submit
-        seq.num_cached = e.length
+        seq.num_cached = seq.base = e.length
         seq.materialized = True
+        return True
 
     # ------------------------------------------------------------ requests
     def submit(self, decoder, prompt_tokens: List[int], prefix_tokens: Optional[List[int]] = None,
@@ -296,9 +370,27 @@ class LLMEngine:
 
     # ---------------------------------------------------------------- step
     def _admit(self):
+        """FIFO admission while the batch has room and the pool holds the
+        blocks of the admitted requests' current tokens (an empty batch admits
+        regardless; a request the whole pool cannot hold fails at schedule)."""
+        free = None
         while self.waiting and len(self.running) < self.max_batch:
-            seq = self.waiting.pop(0)
-            seq.t_admit = time.perf_counter()
+            seq = self.waiting[0]
+            if not seq.is_prefix_job:
+                need = self._blocks_to_admit(seq)
+                if free is None:
+                    free = self.alloc.num_free
+                if need > free:
+                    before = self.alloc.num_free
+                    self._evict_prefixes(before + need - free)
+                    free += self.alloc.num_free - before
+                    if need > free and self.running:
+                        break
+                free -= need
+            self.waiting.pop(0)
+            seq.evicted = False
+            if seq.t_admit is None:
+                seq.t_admit = time.perf_counter()
             self.running.append(seq)
 
     def _ensure_blocks(self, seq: Sequence, total_tokens: int):
@@ -399,6 +491,8 @@ class LLMEngine:
         for seq in pool:
             if not seq.materialized and seq.prefix.computed:
                 self._materialize(seq, copies)
+        if any(q.evicted for q in pool):     # preempted while materialising
+            pool = [q for q in pool if not q.evicted]
         budget = self.max_step_tokens
         entries, sample_seqs, batch_seqs = [], [], []
         T = 0
@@ -431,12 +525,13 @@ class LLMEngine:
             order = first + rest
         pre_tokens = 0
         casc_keys = (casc.length // BLOCK_SIZE) * BLOCK_SIZE if casc is not None else 0
-        alloc = self.alloc.alloc
+        alloc, pool_free = self.alloc.alloc, self.alloc
+        blocked = None
         add_entry, add_batch, add_sample = entries.append, batch_seqs.append, sample_seqs.append
         # the per-request loop of every step (host critical path): locals bound,
         # _ensure_blocks / wants_sample inlined
         for seq in order:
-            if not seq.materialized:           # waiting for its prefix job
+            if not seq.materialized or seq.evicted:   # waiting for its prefix job / preempted
                 continue
             pend = seq.pending
             n = len(pend)
@@ -451,7 +546,14 @@ class LLMEngine:
             blocks = seq.blocks
             need = (start + take + BLOCK_SIZE - 1) // BLOCK_SIZE - len(blocks)
             if need > 0:
-                blocks += alloc(need)
+                if need <= pool_free.num_free:
+                    blocks += alloc(need)
+                else:                          # memory pressure (rare): evict / preempt
+                    got = self._alloc_pressure(need, {id(q) for q, _ in batch_seqs} | {id(seq)})
+                    if got is None:
+                        blocked = blocked or seq
+                        continue
+                    blocks += got
             T += take
             if casc is not None and seq.prefix is casc:
                 pre_tokens = T
@@ -468,6 +570,14 @@ class LLMEngine:
         if T == 0:
             if copies:     # copy-on-write blocks still have to land before later steps
                 self._launch(*pack_step([], BLOCK_SIZE, group, copies))
+            if blocked is not None and not self.inflight:
+                # nothing else holds blocks that could be reclaimed: the
+                # request does not fit the pool at all
+                blocked.error = (f"KV cache exhausted: the request needs "
+                                 f"{self._blocks_to_admit(blocked) + len(blocked.blocks)} blocks, "
+                                 f"the pool has {self.kv.num_blocks}")
+                self._finish(blocked)
+                self.running = [q for q in self.running if not q.done]
             return None
         allowed = ctr = None
         if sample_seqs:            # grammar masks go in the same single H2D copy
@@ -551,7 +661,9 @@ class LLMEngine:
                 seq.t_first = time.perf_counter()
             seq.n_samples += 1
             seq.decoder.feed(int(tok))
-            seq.pending += seq.decoder.advance()
+            new = seq.decoder.advance()
+            seq.pending += new
+            seq.tokens += new
         max_pos = getattr(self.model.cfg, "max_pos", None)
         for seq, _ in batch_seqs:
             if seq.is_prefix_job or seq.done:

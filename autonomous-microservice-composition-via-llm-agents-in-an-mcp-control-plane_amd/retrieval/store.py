@@ -232,7 +232,10 @@ class SchemaIndex:
         cap = 0 if self.vectors is None else self.vectors.shape[0]
         need = -(-max(u.n, 1) // 4) * 4
         if need > cap:
-            new_cap = max(need, -(-int(cap * 1.5) // 4) * 4, 64)
+            # headroom: registrations after the first build land in spare rows
+            # instead of re-allocating + copying the whole corpus on the engine
+            # thread (a synchronous copy on the CPU tier)
+            new_cap = max(-(-int(need * 1.25) // 4) * 4, -(-int(cap * 1.5) // 4) * 4, 64)
             nv = torch.zeros(new_cap, self.dim, device=self.device, dtype=torch.bfloat16)
             if self.vectors is not None and self.n:
                 nv[:self.n].copy_(self.vectors[:self.n])

@@ -3,6 +3,7 @@
 
   python bench_suite.py plumbing            # config 1: CPU, stub planner
   python bench_suite.py topk [--n 10000]    # config 3: HBM top-k cosine (GPU)
+  python bench_suite.py e2e [--n 10000]     # config 3 end to end: /plan over a 10k registry
 
 Config 1 mirrors the reference measurements in BASELINE.md / SURVEY §6 (stub
 LLM, MockTransport services, FastAPI TestClient, p50 of 30 runs):
@@ -119,14 +120,119 @@ def topk(n: int, dim: int, k: int, batches=(1, 16, 32, 64), iters: int = 50):
               flush=True)
 
 
+def e2e(n: int, model: str, runs: int, conc: int, churn: int):
+    """Config 3 end to end: ``/plan`` through the FastAPI app with the local
+    planner over an ``n``-service registry.  Every request pays retrieval
+    (HBM top-k cosine over the schema index), prompt + grammar build,
+    tokenisation, prefill + constrained decode and JSON parse.  Three phases:
+    one client in a loop, ``conc`` concurrent clients, and ``conc`` clients
+    while ``churn`` services are registered in the background (the index
+    takes them incrementally, off the engine thread)."""
+    import threading
+
+    import httpx
+    import torch
+    from fastapi.testclient import TestClient
+    from mcp_amd.api.server import create_app
+    from mcp_amd.config import Settings
+    from mcp_amd.planner.local import LocalPlanner
+    from mcp_amd.planner.prompt import synthetic_intent
+    from mcp_amd.registry import MemoryRegistry, synthetic_registry
+    from mcp_amd.utils.metrics import METRICS
+    import logging
+    logging.getLogger("httpx").setLevel(logging.WARNING)
+    cuda = torch.cuda.is_available()
+    reg = MemoryRegistry(synthetic_registry(n, seed=3))
+    st = Settings(planner_backend="local", model=model, max_batch=max(16, 2 * conc),
+                  max_nodes=6, temperature=0.2, kv_blocks=0 if cuda else 1024)
+    t0 = time.perf_counter()
+    planner = LocalPlanner.from_settings(st, reg)
+    startup_s = time.perf_counter() - t0
+    app = create_app(st, registry=reg, planner=planner,
+                     transport=httpx.MockTransport(lambda r: httpx.Response(200, json={})))
+    names_seen = set()
+
+    def client(c, base, k, lats):
+        for i in range(k):
+            t = time.perf_counter()
+            r = c.post("/plan", json={"intent": synthetic_intent(base + i)})
+            lats.append(time.perf_counter() - t)
+            assert r.status_code == 200, r.text
+            names_seen.update(x["name"] for x in r.json()["graph"]["nodes"])
+
+    def phase(c, clients, base):
+        lats, ths, errs = [], [], []
+
+        def run(j):
+            try:
+                client(c, base + j * runs, runs, lats)
+            except Exception as e:  # noqa: BLE001 - re-raised below
+                errs.append(e)
+        t = time.perf_counter()
+        for j in range(clients):
+            ths.append(threading.Thread(target=run, args=(j,)))
+            ths[-1].start()
+        for th in ths:
+            th.join()
+        if errs:
+            raise errs[0]
+        return lats, time.perf_counter() - t
+
+    def report(name, lats, wall, clients, **extra):
+        q = statistics.quantiles(lats, n=100) if len(lats) >= 2 else [lats[0]] * 99
+        ret = list(METRICS.windows["retrieval_s"].samples)[-len(lats):] \
+            if "retrieval_s" in METRICS.windows else []
+        print(json.dumps({"config": f"e2e/plan/{name}", "services": n, "model": model,
+                          "device": "cuda" if cuda else "cpu", "clients": clients,
+                          "requests": len(lats), "p50_ms": round(statistics.median(lats) * 1e3, 2),
+                          "p90_ms": round(q[89] * 1e3, 2), "p99_ms": round(q[98] * 1e3, 2),
+                          "plans_per_s": round(len(lats) / wall, 2),
+                          "retrieval_p50_ms": round(statistics.median(ret) * 1e3, 3) if ret else None,
+                          "startup_s": round(startup_s, 1), "data": "synthetic registry + intents, "
+                          "random-init weights", **extra}), flush=True)
+
+    with TestClient(app) as c:
+        phase(c, 1, 900_000)                                 # warm the request path
+        lats, wall = phase(c, 1, 0)
+        report("single", lats, wall, 1)
+        lats, wall = phase(c, conc, 100_000)
+        report("concurrent", lats, wall, conc)
+        stop = threading.Event()
+        extra = [dict(synthetic_registry(1, seed=10_000 + i)[0]) for i in range(churn)]
+
+        def register():
+            for i, rec in enumerate(extra):
+                if stop.is_set():
+                    break
+                rec["name"] = f"late-svc-{i}"
+                reg.register(rec)
+                time.sleep(0.01)
+        th = threading.Thread(target=register)
+        th.start()
+        lats, wall = phase(c, conc, 200_000)
+        stop.set()
+        th.join()
+        late = {s["name"] for s in reg.list_services() if s["name"].startswith("late-svc-")}
+        report("concurrent+registrations", lats, wall, conc, planned_services=len(names_seen),
+               registered=len(late),
+               index=dict(getattr(planner.retriever, "stats", {})))
+    planner._stop.set()
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["plumbing", "topk"])
+    ap.add_argument("which", choices=["plumbing", "topk", "e2e"])
     ap.add_argument("--n", type=int, default=10000)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--runs", type=int, default=20, help="e2e: requests per client per phase")
+    ap.add_argument("--clients", type=int, default=16, help="e2e: concurrent clients")
+    ap.add_argument("--churn", type=int, default=100, help="e2e: services registered during a phase")
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--k", type=int, default=32)
     a = ap.parse_args()
     if a.which == "plumbing":
         plumbing()
+    elif a.which == "e2e":
+        e2e(a.n, a.model, a.runs, a.clients, a.churn)
     else:
         topk(a.n, a.dim, a.k)

@@ -65,13 +65,17 @@ def main():
     from mcp_amd.parallel.comm import StepBroadcaster, init_distributed
 
     rank, world, local_rank, dev = init_distributed()
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     tp = world
     group = dist.group.WORLD if world > 1 else None
     t0 = time.time()
     if args.seq_parallel:
         os.environ["MCP_SEQ_PARALLEL"] = "1"
     model = LlamaModel.random(args.model, dev, seed=args.seed, tp_rank=rank, tp=tp, tp_group=group)
-    torch.cuda.synchronize()
+    sync()
     log(f"[rank {rank}] {args.model} TP={tp} shard ready in {time.time() - t0:.1f}s")
     cfg = get_config(args.model)
     per_block = KVCache.bytes_per_block(cfg.layers, model.hkv, cfg.head_dim)
@@ -89,7 +93,6 @@ def main():
     from mcp_amd.planner.local import LocalPlanner
     from mcp_amd.planner.prompt import synthetic_intent
     from mcp_amd.registry import MemoryRegistry, synthetic_registry
-    from mcp_amd.utils.metrics import METRICS
 
     eng = LLMEngine(model, num_blocks=nb, max_batch=args.batch + 8, max_step_tokens=16384,
                     temperature=0.2, seed=args.seed, bcast=bcast)
@@ -99,21 +102,33 @@ def main():
     t0 = time.perf_counter()
     ncap = eng.warm_graphs(contexts=(8192,))         # server start-up capture (planner.local)
     log(f"[rank 0] start-up graph capture: {ncap} graphs in {time.perf_counter() - t0:.1f}s")
+    def one_step(base):
+        """One closed batch: submit every intent, run the engine (and, through
+        the step broadcasts, every worker rank) dry."""
+        seqs = planner.submit_many([synthetic_intent(base + i) for i in range(args.batch)])
+        eng.run()
+        return seqs
+
     for w in range(args.warmup):
-        planner.plan_many([synthetic_intent(10_000 + i) for i in range(args.batch)])
-    torch.cuda.synchronize()
+        one_step(10_000 + w * args.batch)
+    sync()
     t = time.perf_counter()
-    dags = []
+    seqs_all = []
     for s in range(args.steps):
         ts = time.perf_counter()
-        dags += planner.plan_many([synthetic_intent(s * args.batch + i) for i in range(args.batch)])
+        seqs_all += one_step(s * args.batch)
         log(f"[rank 0] step {s}: {(time.perf_counter() - ts) * 1e3:.0f} ms")
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t
     eng.shutdown_workers()
-    lats = list(METRICS.windows["plan_latency_s"].samples)[-min(len(dags), 4096):]
-    for d in dags:
-        validate_dag(d, names)
+    for q in seqs_all:
+        if q.error:
+            raise RuntimeError(q.error)
+        validate_dag(q.result, names)
+    dags = [q.result for q in seqs_all]
+    # each timed request's own intent -> DAG latency (submit -> DAG parsed), as
+    # in bench.py; rank 0 is the only driver, so its requests are all of them
+    lats = [q.t_done - q.t_submit for q in seqs_all]
 
     # ---- execute every plan with injected faults: retries + ordered fallbacks
     attempts = {}
@@ -151,6 +166,8 @@ def main():
         "model": args.model, "tp": tp, "seq_parallel": model.seq_parallel, "services": args.services, "batch": args.batch,
         "plans_per_s": round(len(dags) / elapsed, 3),
         "p50_latency_ms": round(statistics.median(lats) * 1e3, 1) if lats else None,
+        "p99_latency_ms": round(statistics.quantiles(lats, n=100)[98] * 1e3, 1)
+        if len(lats) >= 2 else None,
         "tokens": eng.stats["tokens"], "execution": exec_stats,
     }), flush=True)
     if world > 1:

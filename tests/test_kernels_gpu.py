@@ -386,6 +386,34 @@ def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, concurrent, 
     assert rel_err(out, exp) < 2e-2
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 8)])
+@pytest.mark.parametrize("T", [1, 77, 300])
+@pytest.mark.parametrize("rt", ["1", "2", "4"])
+def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
+    """The shared-prefix pass alone (normalised O and its log2-sum-exp over
+    the prefix keys) in every row-tile form (1 = MODE 1 of attn_kernel, 2 / 4
+    = attn_prefix_kernel: each LDS fragment feeds 2 / 4 row tiles) against
+    fp32 softmax attention; T covers partial row tiles and blocks."""
+    monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
+    torch.manual_seed(11)
+    D, P = 128, 640
+    n_pre = P // 64
+    kc, vc = _cache(n_pre + 3, Hkv)
+    pre_bt = torch.tensor([2, 0, 5, 1, 3, 4, 6, 8, 7, 9][:n_pre], dtype=torch.int32, device=DEV)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    out = torch.empty_like(q)
+    lse = torch.empty(T, Hq, device=DEV, dtype=torch.float32)
+    scale = 1 / math.sqrt(D)
+    ops.lib().prefix_attention(q, kc, vc, out, lse, pre_bt, P, T, scale)
+    G = Hq // Hkv
+    k = kc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)      # [Hkv, P, D]
+    v = vc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    qf = q.float().view(T, Hkv, G, D)
+    s = torch.einsum("thgd,hpd->thgp", qf, k) * scale
+    exp_o = torch.einsum("thgp,hpd->thgd", torch.softmax(s, -1), v).reshape(T, Hq, D)
+    exp_lse = (torch.logsumexp(s, -1) / math.log(2)).reshape(T, Hq)
+    assert rel_err(out, exp_o) < 2e-2
+    assert torch.allclose(lse, exp_lse, atol=2e-2, rtol=1e-3)
 
 
 @pytest.mark.parametrize("M,F,K", [(7, 512, 256), (300, 1792, 4096), (3000, 14336, 4096), (520, 3584, 1024)])

@@ -1,5 +1,6 @@
 """Planner tests on CPU: grammar, engine plumbing with the tiny
 Llama config through the fp32 reference ops, API wiring of the local planner."""
+import asyncio
 import json
 import random
 
@@ -434,3 +435,54 @@ def test_context_exhaustion_fails_the_request():
     assert max(seen) <= small.max_pos
     assert eng.alloc.num_free == free0 and not eng.running
     planner._stop.set()
+
+
+def test_prefix_cache_yields_blocks_when_the_pool_is_full():
+    """With retrieval every request brings its own registry prefix; cached
+    prefixes must give their blocks back when the pool runs dry instead of
+    failing the request with OutOfBlocks."""
+    from mcp_amd.retrieval.store import SchemaIndex
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    eng = LLMEngine(model, num_blocks=24, max_batch=4, temperature=0.0, graphs=False)
+    reg = MemoryRegistry(synthetic_registry(60, seed=7))
+    retr = SchemaIndex(reg, dim=64, device="cpu")
+    retr.refresh()
+    planner = LocalPlanner(eng, reg, max_nodes=2, retriever=retr, retrieval_threshold=8, topk=4)
+    names = [s.name for s in reg.list_services()]
+    intents = [synthetic_intent(100 + i) for i in range(8)]
+    prefix_blocks = sum(len(planner.prepare(x)[1]) // 64 for x in intents)
+    assert prefix_blocks > eng.kv.num_blocks     # the distinct prefixes outgrow the pool
+
+    async def serve():                           # the server path keeps prefixes cached
+        return [await planner.plan(x) for x in intents]
+    for d in asyncio.run(serve()):
+        validate_dag(d, names)
+    planner._stop.set()
+    eng.drop_prefixes()
+    assert eng.alloc.num_free == eng.kv.num_blocks
+
+
+def test_preemption_by_recompute_under_a_small_kv_pool():
+    """A pool too small for every admitted request's growth: requests are
+    preempted (blocks freed, history recomputed later, shared prefix blocks
+    kept) and the greedy plans equal a large pool's; a pool that cannot hold
+    one request fails it cleanly; no block leaks either way."""
+    reg = MemoryRegistry(synthetic_registry(5, seed=7))
+    intents = [synthetic_intent(i) for i in range(8)]
+
+    def run(nb):
+        eng = LLMEngine(LlamaModel.random("tiny", "cpu", seed=1), num_blocks=nb, max_batch=8,
+                        temperature=0.0, graphs=False)
+        pl = LocalPlanner(eng, reg, max_nodes=4)
+        try:
+            return pl.plan_many(intents), eng
+        except RuntimeError as e:
+            return e, eng
+    big, eng_big = run(256)
+    small, eng = run(14)
+    assert eng_big.stats["preemptions"] == 0 and eng.stats["preemptions"] > 0
+    assert small == big
+    assert eng.alloc.num_free == 14
+    err, eng = run(9)
+    assert isinstance(err, RuntimeError) and "KV cache exhausted" in str(err)
+    assert eng.alloc.num_free == 9 and not eng.running and not eng.waiting
