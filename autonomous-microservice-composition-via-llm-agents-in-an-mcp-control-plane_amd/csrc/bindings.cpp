@@ -496,6 +496,18 @@ void add_inplace(at::Tensor& y, const at::Tensor& x) {
   check_launch("add_inplace");
 }
 
+// read a tensor's bytes [offset, offset + nbytes) into the Infinity Cache
+// (elementwise.hip prefetch_kernel); sink: any int32 CUDA tensor
+void prefetch(const at::Tensor& t, int64_t offset, int64_t nbytes, int64_t blocks, at::Tensor& sink) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && sink.is_cuda(), "prefetch: CUDA tensors");
+  const int64_t total = t.numel() * t.element_size();
+  TORCH_CHECK(offset >= 0 && nbytes >= 0 && offset + nbytes <= total && offset % 16 == 0,
+              "prefetch: byte range");
+  launch_prefetch((const char*)t.data_ptr() + offset, (size_t)nbytes, (int)blocks, sink.data_ptr(),
+                  stream());
+  check_launch("prefetch");
+}
+
 // ---- K12 custom all-reduce: the state is an opaque int64 handle on the Python side
 int64_t car_init(int64_t rank, int64_t world, int64_t buf_bytes, at::Tensor& handles_out) {
   TORCH_CHECK(handles_out.device().is_cpu() && handles_out.scalar_type() == at::kByte &&
@@ -650,6 +662,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_tok"), py::arg("out_logit") = py::none());
   m.def("sample_dense", &sample_dense);
   m.def("add_inplace", &add_inplace);
+  m.def("prefetch", &prefetch, "read a byte range into the Infinity Cache", py::arg("t"),
+        py::arg("offset"), py::arg("nbytes"), py::arg("blocks") = 512, py::arg("sink"));
   m.def("copy_blocks", &copy_blocks);
   m.def("car_handle_bytes", []() { return (int64_t)car_handle_bytes(); });
   m.def("car_init", &car_init);

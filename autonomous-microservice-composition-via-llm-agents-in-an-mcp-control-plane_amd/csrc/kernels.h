@@ -38,6 +38,7 @@ void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const voi
                     void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
                     int BS, hipStream_t s);
 void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
+void launch_prefetch(const void* p, size_t bytes, int blocks, void* sink, hipStream_t s);
 
 // QKV projection + RoPE + paged K/V write fused in the GEMM epilogue (K1+K4+K10)
 // serving-size M: tile shape per (M, N) filling one wave of workgroups (gemm_flex.hip)

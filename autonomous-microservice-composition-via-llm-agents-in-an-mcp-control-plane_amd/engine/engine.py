@@ -171,7 +171,7 @@ class LLMEngine:
             self.graphs = GraphRunner(model, self.kv, temperature, seed, max_seqs=max_batch,
                                       bcast=bcast)
         self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "graph_cow_steps": 0,
-                      "graph_split_steps": 0, "kv_split_steps": 0, "preemptions": 0,
+                      "graph_split_steps": 0, "graph_cascade_steps": 0, "kv_split_steps": 0, "preemptions": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
 
     # ------------------------------------------------------------- prefixes
@@ -610,6 +610,7 @@ class LLMEngine:
             self.stats["graph_steps"] += 1
             self.stats["graph_cow_steps"] += bool(copies)
             self.stats["graph_split_steps"] += kv_splits > 1
+            self.stats["graph_cascade_steps"] += cascade
             self.stats["samples"] += len(sample_seqs)
             tokens, event = self._fetch(tok_dev[:len(sample_seqs)])
         else:

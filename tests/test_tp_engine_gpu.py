@@ -6,7 +6,10 @@ this process (TPPlanner, as behind the API with MCP_TP=2), the worker rank is
 a spawned process; the group is gloo (RCCL refuses two ranks on one device),
 so MCP_COMM=torch and a K12 staging buffer large enough for every message.
 Steps that fit a hipGraph bucket replay captured graphs on both ranks (the K12
-epoch lives on the device, so replays resynchronise correctly)."""
+epoch lives on the device, so replays resynchronise correctly): a batch of 4
+intents sharing the registry prefix replays cascade and copy-on-write graph
+keys, a single intent afterwards replays split-KV keys - the worker mirrors
+each key the driver broadcasts, so equal plans mean both ranks ran them."""
 import os
 
 import pytest
@@ -43,17 +46,22 @@ def test_tp2_two_processes_one_gpu_matches_tp1(monkeypatch):
         assert ar.custom is not None and ar.native is None
         assert tp.engine.graphs is not None          # K12 all-reduces are capturable
         dags_tp = tp.plan_many(intents)
+        dags_tp += tp.plan_many([synthetic_intent(7)])        # alone: split-KV steps
         tp.engine.model.comm_check()
-        steps_tp = tp.engine.stats["steps"]
-        graph_steps_tp = tp.engine.stats["graph_steps"]
+        st_tp = dict(tp.engine.stats)
     finally:
         tp.shutdown()
-    assert steps_tp > 0 and graph_steps_tp > 0   # worker ranks replayed the driver's graphs
+    # worker ranks replayed the driver's graphs, with every attention form keyed
+    assert st_tp["steps"] > 0 and st_tp["graph_steps"] > 0
+    assert st_tp["graph_cascade_steps"] > 0, st_tp
+    assert st_tp["graph_cow_steps"] > 0, st_tp
+    assert st_tp["graph_split_steps"] > 0, st_tp
     for d in dags_tp:
         validate_dag(d, names)
 
     cfg = get_config("llama3-1b-ish")
     m1 = LlamaModel(cfg, random_weights(cfg, "cuda:0", seed=5), "cuda:0")
     eng1 = LLMEngine(m1, num_blocks=512, max_batch=8, max_step_tokens=2048, temperature=0.0)
-    dags_1 = LocalPlanner(eng1, reg, max_nodes=4).plan_many(intents)
+    lp = LocalPlanner(eng1, reg, max_nodes=4)
+    dags_1 = lp.plan_many(intents) + lp.plan_many([synthetic_intent(7)])
     assert dags_tp == dags_1
