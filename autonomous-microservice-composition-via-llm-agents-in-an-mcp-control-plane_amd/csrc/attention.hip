@@ -866,6 +866,8 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
 
 int attn_tokens_per_item(int nw, int group) { return nw * (16 / group); }
 
+int* attn_split_counters() { return split_counters(); }
+
 int attn_split_init() {
   int d = 0;
   (void)hipGetDevice(&d);

@@ -1,0 +1,430 @@
+// K6 (v2): split-KV attention for decode-sized steps - few sequences, a few
+// new query tokens each (single intent, low-QPS serving: config 2 / 5).
+//
+// Measured first (tools/bench_attention_decode.py, hipGraph-replayed,
+// profiles/attention_decode_r3_baseline.jsonl): the work-list kernel
+// (attention.hip, MIXED split launch) takes ~10-12 us warm and 19.4 us in the
+// config-2 trace for one sequence over 700-1100 keys (4.5 MB of K/V: the HBM
+// time is < 1 us; an empty kernel in a graph costs 2.2 us).  The time is a
+// chain of dependent memory round trips - work item -> sequence sizes ->
+// block table -> K/V DMA -> next tile's DMA -> partial / ticket / merge -
+// each an HBM miss during serving (the weights streamed since the last step
+// evicted everything).  Here:
+//
+//  * the key tiles of a block are fixed by its grid position alone: block z
+//    covers absolute tiles [z C, z C + C), C = 4 x tpw, wave w the tiles
+//    z C + w + 4 j.  So the block-table entry of a wave's first tile is read
+//    in the same round trip as the sequence's sizes, and its K / V loads and
+//    the Q loads go out together in the next;
+//  * the 4 waves of a block work on 4 different tiles at once: K straight
+//    into registers as the MFMA A operand (16 x 16 B per lane), V by LDS-DMA
+//    into the wave's own 16 KiB buffer (no barrier between a wave's DMA and
+//    its transposed reads; 64 KiB per block, two blocks per CU);
+//  * one 16-row tile (16 / G tokens x G heads) per block: a 4-wave work item
+//    (16 x 4 / G tokens) runs as 4 blocks, so no wave carries several row
+//    tiles through the softmax chain;
+//  * the 4 waves' (max, sum, O) merge through LDS (the V buffers hold the
+//    fp32 O afterwards), then - only when the item spans more than one block
+//    - the blocks merge by the last-arriver protocol of attention.hip (sc1
+//    partials + agent-scope ticket, block order, so the result does not
+//    depend on which block arrives last); the cascade prefix partial, if any,
+//    is folded in once by whoever writes the rows.
+// Same math as attention.hip's attn_kernel (S^T = K Q^T, online softmax per
+// lane, O^T += V^T P^T with V^T from ds_read_b64_tr_b16 and P^T straight from
+// the S^T accumulators).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int D = 128;
+constexpr int KT = 64;                     // keys per tile == cache block
+constexpr int TILE = KT * D;               // bf16 elements of a K or V tile (16 KiB)
+constexpr int NWV = 4;                     // waves per block
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+DEV bf16x4 tr_read(const bf16* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+struct DecArgs {
+  const bf16* q;
+  const bf16* kc;
+  const bf16* vc;
+  bf16* out;
+  const int* q_start;
+  const int* q_len;
+  const int* ctx_len;
+  const int* block_table;
+  int max_blocks;
+  const int* work_seq4;    // 4-wave items: blocks [0, 4 nwork4), 4 row tiles each
+  const int* work_q04;
+  int nwork4;
+  const int* work_seq1;    // 1-wave items: blocks [4 nwork4, ...)
+  const int* work_q01;
+  int Hq, Hkv;
+  float scale_log2;
+  const int* kv_begin;     // cascade: first own key per sequence (multiple of 64) or null
+  const bf16* pre_o;       // cascade: normalised prefix partial [T, Hq, D]
+  const float* pre_lse;    // cascade: its log2-sum-exp [T, Hq]
+  float* split_o;          // [nz][rows][D] fp32 partials of multi-block items
+  float* split_lse;        // [nz][rows]
+  int rows;                // T * Hq
+  int* split_cnt;          // per (block row, kv head) arrival tickets, zero between launches
+  int tpw;                 // tiles per wave
+};
+
+template <int G>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
+  constexpr int TPR = 16 / G;                        // tokens per 16-row tile
+  __shared__ __attribute__((aligned(16))) bf16 smem[NWV * TILE];   // per wave: V tile, then O
+  __shared__ float s_ml[NWV][2][16];                 // per wave: row max, row sum
+  __shared__ int s_last;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int kvh = blockIdx.y, z = blockIdx.z;
+  const int b = blockIdx.x;
+  const bool wide = b < 4 * a.nwork4;
+  const int s = wide ? a.work_seq4[b >> 2] : a.work_seq1[b - 4 * a.nwork4];
+  const int q0 = wide ? a.work_q04[b >> 2] + (b & 3) * TPR : a.work_q01[b - 4 * a.nwork4];
+  const int C = NWV * a.tpw;
+  const int* bt = a.block_table + (size_t)s * a.max_blocks;
+  bf16* vl = smem + wave * TILE;                     // this wave's V buffer
+
+  // K of cache block blk -> registers: A fragment (nt, ks) = K[key 16 nt + fr]
+  // [d 32 ks + 8 fq ..]; V -> LDS by 16 DMA pieces of 4 rows, row 4 pr + srow's
+  // 16-B chunk c at chunk c ^ (row & 15) - which depends on pr & 3 only: 4
+  // per-lane offsets, the row step in soffset
+  const int srow = lane >> 4;
+  unsigned voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) voff[i] = (unsigned)((srow * D + (((lane & 15) ^ (4 * i + srow)) << 3)) * 2);
+  const unsigned koff = (unsigned)((fr * D + 8 * fq) * 2);
+  bf16x8 kf[4][4];
+  auto load_tile = [&](int blk) {
+    blk = __builtin_amdgcn_readfirstlane(blk);
+    if (blk < 0) blk = 0;                            // never for a used tile (padding guard)
+    const size_t base = ((size_t)blk * a.Hkv + kvh) * (size_t)TILE;
+    const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)(a.kc + base), (short)0, TILE * 2, 0x00020000);
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vc + base), (short)0, TILE * 2, 0x00020000);
+#pragma unroll
+    for (int pr = 0; pr < 16; ++pr) {
+      auto* dst = (__attribute__((address_space(3))) void*)(vl + pr * 512);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, dst, 16, voff[pr & 3], pr * 4 * D * 2, 0, 0);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        kf[nt][ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rk, koff, (nt * 16 * D + 32 * ks) * 2, 0));
+  };
+
+  // the first tile's block id needs only the grid position: read in the same
+  // round trip as the sequence's sizes; its K / V and the Q loads go next
+  const int kt_first = z * C + wave;
+  const int blk0 = kt_first < a.max_blocks ? bt[kt_first] : -1;
+  const int qs = a.q_start[s], ql = a.q_len[s], cl = a.ctx_len[s];
+  const int kvb = a.kv_begin ? a.kv_begin[s] : 0;
+  const int last_tok = min(q0 + TPR, ql) - 1;
+  const int kv_end = cl - ql + last_tok + 1;
+  const int kt0 = kvb / KT, kt1 = (kv_end + KT - 1) / KT;
+  const int z_first = kt0 / C, z_last = (kt1 - 1) / C;
+  // padding items / row tiles past the span, blocks wholly outside the own keys
+  if (q0 >= ql || kt1 <= kt0 || z < z_first || z > z_last) return;
+  const int nact = z_last - z_first + 1;
+  if (kt_first >= kt0 && kt_first < kt1) load_tile(blk0);
+
+  // Q fragment (B operand): lane holds Q[row fr][d = 32 ks + 8 fq + j]
+  const int tok = q0 + fr / G;
+  const bool qvalid = tok < ql;
+  const int qpos = qvalid ? cl - ql + tok : -1;      // -1: no key passes the mask
+  bf16x8 qf[4];
+  {
+    const bf16* qp = a.q + ((size_t)(qs + (qvalid ? tok : 0)) * a.Hq + kvh * G + fr % G) * D + 8 * fq;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = qvalid ? *reinterpret_cast<const bf16x8*>(qp + 32 * ks) : bf16x8{};
+  }
+
+  f32x4 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_part = 0.f;
+
+  for (int j = 0; j < a.tpw; ++j) {
+    const int kt = z * C + wave + NWV * j;
+    const bool use = kt >= kt0 && kt < kt1;
+    if (j > 0 && use) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the last V
+      load_tile(bt[kt]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // own K / V landed (own buffer only)
+    if (!use) continue;
+
+    // ---- S^T = K Q^T
+    f32x4 sacc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sacc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) sacc[nt] = mfma16x16x32(kf[nt][ks], qf[ks], sacc[nt]);
+    }
+    // ---- mask + online softmax (lane: query row fr, keys 16 nt + 4 fq + r)
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * KT + nt * 16 + fq * 4 + r;
+        float v = sacc[nt][r] * a.scale_log2;
+        v = (key <= qpos && key < cl) ? v : -INFINITY;
+        sacc[nt][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    m_run = m_new;
+    float psum = 0.f;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sacc[nt][r] - m_use);
+        psum += p;
+        pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
+      }
+    l_part = l_part * alpha + psum;
+    // ---- O^T += V^T P^T (V^T via transposed LDS reads, permuted key order)
+    const int tq = (lane & 15) >> 2, tp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int col = dt * 16 + tp * 4;
+      const int chunk = col >> 3, half = (col & 7);
+      f32x4 acc = o[dt] * alpha;
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int key0 = k2 * 32 + fq * 4 + tq;
+        const int key1 = key0 + 16;
+        const bf16x4 v0 = tr_read(vl + key0 * D + ((chunk ^ (key0 & 15)) << 3) + half);
+        const bf16x4 v1 = tr_read(vl + key1 * D + ((chunk ^ (key1 & 15)) << 3) + half);
+        const bf16x8 vf = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        acc = mfma16x16x32(vf, pf[k2], acc);
+      }
+      o[dt] = acc;
+    }
+  }
+
+  // ---- the 4 waves' partials -> LDS: (max, sum) per row and the unnormalised
+  //      fp32 O (8 KiB) in the wave's own V buffer, rows of 128 floats with
+  //      the 16-B chunk c at c ^ (row & 15) (conflict-free MFMA-layout writes)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  {
+    float* ow = reinterpret_cast<float*>(vl);
+    float lt = l_part + __shfl_xor(l_part, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (fq == 0) {
+      s_ml[wave][0][fr] = m_run;
+      s_ml[wave][1][fr] = lt;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      *reinterpret_cast<f32x4*>(ow + fr * D + (((4 * dt + fq) ^ fr) << 2)) = o[dt];
+  }
+  __syncthreads();
+
+  // ---- merge: thread = (row r = tid / 16, 8 dims c8 = tid % 16)
+  const int r = threadIdx.x >> 4, c8 = threadIdx.x & 15;
+  const int rtok = q0 + r / G;
+  const bool rvalid = rtok < ql;
+  const size_t grow = (size_t)(qs + (rvalid ? rtok : 0)) * a.Hq + kvh * G + r % G;
+  const bool merge_pre = a.pre_o != nullptr && a.kv_begin != nullptr && kvb > 0;
+  const auto rso = __builtin_amdgcn_make_buffer_rsrc(a.split_o, (short)0, 0x7FFFFFFF, 0x00020000);
+  const auto rsl = __builtin_amdgcn_make_buffer_rsrc(a.split_lse, (short)0, 0x7FFFFFFF, 0x00020000);
+  if (rvalid) {
+    float mw[NWV], mx = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      mw[w] = s_ml[w][0][r];
+      mx = fmaxf(mx, mw[w]);
+    }
+    const float mu = mx == -INFINITY ? 0.f : mx;
+    float den = 0.f;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float e = mw[w] == -INFINITY ? 0.f : exp2f(mw[w] - mu);
+      den += e * s_ml[w][1][r];
+      const float* src = reinterpret_cast<const float*>(smem + w * TILE) + r * D;
+      acc0 += e * *reinterpret_cast<const f32x4*>(src + (((2 * c8) ^ r) << 2));
+      acc1 += e * *reinterpret_cast<const f32x4*>(src + (((2 * c8 + 1) ^ r) << 2));
+    }
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+    acc0 *= inv;
+    acc1 *= inv;
+    const float lse = den > 0.f ? mu + __log2f(den) : -INFINITY;
+    if (nact == 1) {
+      // the item's only block: fold the prefix partial in and write the row
+      if (merge_pre) {
+        const float lp = a.pre_lse[grow];
+        const float m2 = fmaxf(lp, lse);
+        const float wa = exp2f(lp - m2), wb = lse == -INFINITY ? 0.f : exp2f(lse - m2);
+        const float dn = 1.f / (wa + wb);
+        const bf16x8 pa = *reinterpret_cast<const bf16x8*>(a.pre_o + grow * D + 8 * c8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc0[i] = (acc0[i] * wb + (float)pa[i] * wa) * dn;
+          acc1[i] = (acc1[i] * wb + (float)pa[4 + i] * wa) * dn;
+        }
+      }
+      bf16x8 ov;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ov[i] = (bf16)acc0[i];
+        ov[4 + i] = (bf16)acc1[i];
+      }
+      *reinterpret_cast<bf16x8*>(a.out + grow * D + 8 * c8) = ov;
+    } else {
+      // one of several blocks: its normalised partial, write-through
+      const int zr = z - z_first;
+      const unsigned off = (unsigned)((((size_t)zr * a.rows + grow) * D + 8 * c8) * 4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc0), rso, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc1), rso, off + 16, 0, 16);
+      if (c8 == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, lse), rsl,
+                                              (unsigned)(((size_t)zr * a.rows + grow) * 4), 0, 16);
+    }
+  }
+  if (nact == 1) return;
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                   // every partial of this block is out
+  if (threadIdx.x == 0) {
+    int* cnt = a.split_cnt + (size_t)b * a.Hkv + kvh;
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == nact - 1;
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last || !rvalid) return;
+  // ---- last arriver: every block's partial in block order (deterministic)
+  float mx = -INFINITY;
+#pragma unroll 8
+  for (int jz = 0; jz < nact; ++jz)
+    mx = fmaxf(mx, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                       rsl, (unsigned)(((size_t)jz * a.rows + grow) * 4), 0, 16)));
+  float lp = -INFINITY;
+  bf16x8 pa{};
+  if (merge_pre) {
+    lp = a.pre_lse[grow];
+    pa = *reinterpret_cast<const bf16x8*>(a.pre_o + grow * D + 8 * c8);
+    mx = fmaxf(mx, lp);
+  }
+  const float mu = mx == -INFINITY ? 0.f : mx;
+  float den = 0.f;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int jz = 0; jz < nact; ++jz) {
+    const float lj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        rsl, (unsigned)(((size_t)jz * a.rows + grow) * 4), 0, 16));
+    const unsigned off = (unsigned)((((size_t)jz * a.rows + grow) * D + 8 * c8) * 4);
+    const f32x4 p0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rso, off, 0, 16));
+    const f32x4 p1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rso, off + 16, 0, 16));
+    const float wj = lj == -INFINITY ? 0.f : exp2f(lj - mu);
+    den += wj;
+    acc0 += p0 * wj;
+    acc1 += p1 * wj;
+  }
+  if (merge_pre) {
+    const float wp = exp2f(lp - mu);
+    den += wp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc0[i] += (float)pa[i] * wp;
+      acc1[i] += (float)pa[4 + i] * wp;
+    }
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  bf16x8 ov;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ov[i] = (bf16)(acc0[i] * inv);
+    ov[4 + i] = (bf16)(acc1[i] * inv);
+  }
+  *reinterpret_cast<bf16x8*>(a.out + grow * D + 8 * c8) = ov;
+}
+
+}  // namespace
+
+int* attn_split_counters();   // attention.hip
+
+// tiles per wave for a block-table width: <= 64 blocks per (item, kv head)
+int attn_decode_tpw(int max_blocks) {
+  const int per_pass = NWV * 64;
+  return max_blocks <= per_pass ? 1 : (max_blocks + per_pass - 1) / per_pass;
+}
+int attn_decode_blocks(int max_blocks) {
+  const int C = NWV * attn_decode_tpw(max_blocks);
+  return (max_blocks + C - 1) / C;
+}
+
+// nonzero: not launched (the caller uses the work-list split path)
+int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, void* out,
+                       const int* q_start, const int* q_len, const int* ctx_len,
+                       const int* block_table, int max_blocks, const int* work_seq4,
+                       const int* work_q04, int nwork4, const int* work_seq1, const int* work_q01,
+                       int nwork1, int Hq, int Hkv, int head_dim, float scale, const int* kv_begin,
+                       const void* pre_o, const float* pre_lse, float* split_o, float* split_lse,
+                       int rows, int nz, hipStream_t s) {
+  if (head_dim != D) return 1;
+  const int nitems = 4 * nwork4 + nwork1;            // 4-wave items: one block per row tile
+  if (nitems <= 0) return 0;
+  if (max_blocks <= 0) return 2;
+  const int tpw = attn_decode_tpw(max_blocks);
+  if (nz != attn_decode_blocks(max_blocks)) return 3;
+  int* cnt = attn_split_counters();
+  if (!cnt || (long long)nitems * Hkv > (1 << 16)) return 5;
+  if (nz > 1 && (!split_o || !split_lse || (long long)nz * rows * D * 4 >= (1ll << 31))) return 6;
+  DecArgs a{};
+  a.q = (const bf16*)q;
+  a.kc = (const bf16*)k_cache;
+  a.vc = (const bf16*)v_cache;
+  a.out = (bf16*)out;
+  a.q_start = q_start;
+  a.q_len = q_len;
+  a.ctx_len = ctx_len;
+  a.block_table = block_table;
+  a.max_blocks = max_blocks;
+  a.work_seq4 = work_seq4;
+  a.work_q04 = work_q04;
+  a.nwork4 = nwork4;
+  a.work_seq1 = work_seq1;
+  a.work_q01 = work_q01;
+  a.Hq = Hq;
+  a.Hkv = Hkv;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.kv_begin = kv_begin;
+  a.pre_o = (const bf16*)pre_o;
+  a.pre_lse = pre_lse;
+  a.split_o = split_o;
+  a.split_lse = split_lse;
+  a.rows = rows;
+  a.split_cnt = cnt;
+  a.tpw = tpw;
+  const dim3 grid(nitems, Hkv, nz);
+  switch (Hq / Hkv) {
+    case 1: attn_decode_kernel<1><<<grid, 256, 0, s>>>(a); break;
+    case 2: attn_decode_kernel<2><<<grid, 256, 0, s>>>(a); break;
+    case 4: attn_decode_kernel<4><<<grid, 256, 0, s>>>(a); break;
+    case 8: attn_decode_kernel<8><<<grid, 256, 0, s>>>(a); break;
+    case 16: attn_decode_kernel<16><<<grid, 256, 0, s>>>(a); break;
+    default: return 4;
+  }
+  return 0;
+}

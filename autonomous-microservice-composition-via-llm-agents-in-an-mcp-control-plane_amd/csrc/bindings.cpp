@@ -389,6 +389,61 @@ bool paged_attention_mixed(const at::Tensor& q, const at::Tensor& k_cache, const
   return true;
 }
 
+// decode-sized split-KV step (attention_decode.hip); false = not launched
+// (the caller takes the work-list split path)
+bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                            at::Tensor& out, const at::Tensor& q_start, const at::Tensor& q_len,
+                            const at::Tensor& ctx_len, const at::Tensor& block_table,
+                            const at::Tensor& work_seq4, const at::Tensor& work_q04,
+                            const at::Tensor& work_seq1, const at::Tensor& work_q01, double scale,
+                            int64_t nz, at::Tensor& split_o, at::Tensor& split_lse,
+                            const c10::optional<at::Tensor>& kv_begin,
+                            const c10::optional<at::Tensor>& pre_o,
+                            const c10::optional<at::Tensor>& pre_lse) {
+  CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
+  CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
+  CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq4); CHECK_I32_TENSOR(work_q04);
+  CHECK_I32_TENSOR(work_seq1); CHECK_I32_TENSOR(work_q01);
+  TORCH_CHECK(q.dim() == 3, "q must be [T, Hq, D]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64, "cache block size must be 64");
+  const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
+  TORCH_CHECK(block_table.dim() == 2 && block_table.size(0) == q_len.numel(), "block_table [S, max_blocks]");
+  TORCH_CHECK(work_seq4.numel() == work_q04.numel() && work_seq1.numel() == work_q01.numel(),
+              "work lists");
+  TORCH_CHECK(nz == attn_decode_blocks(block_table.size(1)), "nz must be attn_decode_blocks(max_blocks)");
+  TORCH_CHECK(split_o.scalar_type() == at::kFloat && split_o.is_contiguous() &&
+              (nz == 1 || split_o.numel() >= nz * q.numel()), "split_o [nz, T, Hq, D] f32");
+  TORCH_CHECK(split_lse.scalar_type() == at::kFloat && split_lse.is_contiguous() &&
+              (nz == 1 || split_lse.numel() >= nz * q.size(0) * Hq), "split_lse [nz, T, Hq] f32");
+  const int* kb = nullptr;
+  const void* po = nullptr;
+  const float* pl = nullptr;
+  if (kv_begin.has_value()) {
+    CHECK_I32_TENSOR((*kv_begin));
+    TORCH_CHECK(kv_begin->numel() == q_len.numel(), "kv_begin [S]");
+    TORCH_CHECK(pre_o.has_value() && pre_lse.has_value(), "kv_begin needs pre_o / pre_lse");
+    CHECK_BF16_TENSOR((*pre_o));
+    TORCH_CHECK(pre_o->sizes() == q.sizes(), "pre_o shape");
+    TORCH_CHECK(pre_lse->scalar_type() == at::kFloat && pre_lse->numel() == q.size(0) * Hq, "pre_lse [T, Hq]");
+    kb = kv_begin->data_ptr<int>();
+    po = pre_o->data_ptr();
+    pl = pre_lse->data_ptr<float>();
+  }
+  const int rc = launch_attn_decode(
+      q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
+      q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
+      block_table.size(1), work_seq4.data_ptr<int>(), work_q04.data_ptr<int>(), work_seq4.numel(),
+      work_seq1.data_ptr<int>(), work_q01.data_ptr<int>(), work_seq1.numel(), Hq, Hkv, D,
+      (float)scale, kb, po, pl, split_o.data_ptr<float>(), split_lse.data_ptr<float>(),
+      (int)(q.size(0) * Hq), (int)nz, stream());
+  TORCH_CHECK(rc != 1 && rc != 3 && rc != 4, "paged_attention_decode: unsupported config (code ", rc, ")");
+  if (rc != 0) return false;
+  check_launch("paged_attention_decode");
+  return true;
+}
+
 void cascade_merge(at::Tensor& out, const at::Tensor& own_lse, const at::Tensor& pre_o,
                    const at::Tensor& pre_lse, int64_t pre_tokens,
                    const c10::optional<at::Tensor>& pre_dims) {
@@ -494,18 +549,6 @@ void add_inplace(at::Tensor& y, const at::Tensor& x) {
   TORCH_CHECK(y.numel() == x.numel() && y.numel() % 8 == 0, "add_inplace shapes");
   launch_add_inplace(y.data_ptr(), x.data_ptr(), y.numel(), stream());
   check_launch("add_inplace");
-}
-
-// read a tensor's bytes [offset, offset + nbytes) into the Infinity Cache
-// (elementwise.hip prefetch_kernel); sink: any int32 CUDA tensor
-void prefetch(const at::Tensor& t, int64_t offset, int64_t nbytes, int64_t blocks, at::Tensor& sink) {
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && sink.is_cuda(), "prefetch: CUDA tensors");
-  const int64_t total = t.numel() * t.element_size();
-  TORCH_CHECK(offset >= 0 && nbytes >= 0 && offset + nbytes <= total && offset % 16 == 0,
-              "prefetch: byte range");
-  launch_prefetch((const char*)t.data_ptr() + offset, (size_t)nbytes, (int)blocks, sink.data_ptr(),
-                  stream());
-  check_launch("prefetch");
 }
 
 // ---- K12 custom all-reduce: the state is an opaque int64 handle on the Python side
@@ -662,8 +705,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_tok"), py::arg("out_logit") = py::none());
   m.def("sample_dense", &sample_dense);
   m.def("add_inplace", &add_inplace);
-  m.def("prefetch", &prefetch, "read a byte range into the Infinity Cache", py::arg("t"),
-        py::arg("offset"), py::arg("nbytes"), py::arg("blocks") = 512, py::arg("sink"));
+  m.def("attn_decode_blocks", &attn_decode_blocks, "grid z of paged_attention_decode for a table width");
+  m.def("paged_attention_decode", &paged_attention_decode, py::arg("q"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("out"), py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"),
+        py::arg("block_table"), py::arg("work_seq4"), py::arg("work_q04"), py::arg("work_seq1"),
+        py::arg("work_q01"), py::arg("scale"), py::arg("nz"), py::arg("split_o"),
+        py::arg("split_lse"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
+        py::arg("pre_lse") = py::none());
   m.def("copy_blocks", &copy_blocks);
   m.def("car_handle_bytes", []() { return (int64_t)car_handle_bytes(); });
   m.def("car_init", &car_init);

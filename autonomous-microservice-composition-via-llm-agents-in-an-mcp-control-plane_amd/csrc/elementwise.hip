@@ -280,32 +280,3 @@ void launch_copy_blocks(void* data, const int* src, const int* dst, int npairs, 
                                                       block_elems / 8);
 }
 
-// ------------------------------------------- weight prefetch (Infinity Cache)
-// Reads [p, p + bytes) and discards it: the lines land in the 256 MiB
-// Infinity Cache (MI355X_MICROARCH.md "Infinity Cache": reads allocate, a line
-// stays resident while < ~256 MiB of other traffic passes).  Run on a side
-// stream ahead of a weight-streaming decode GEMM, it keeps HBM busy while the
-// main stream is latency-bound (attention, launch gaps, ramp / tail) and the
-// GEMM then reads those weights on-die.  Four 16-B loads in flight per lane;
-// the xor of everything loaded goes to `sink` only if it equals a value it
-// practically never equals (a dead store the compiler cannot remove).
-__global__ __launch_bounds__(256) void prefetch_kernel(const u32x4* __restrict__ p, size_t nvec,
-                                                       unsigned* __restrict__ sink) {
-  u32x4 acc = {0u, 0u, 0u, 0u};
-  const size_t stride = (size_t)gridDim.x * 256;
-  size_t i = blockIdx.x * 256ull + threadIdx.x;
-  for (; i + 3 * stride < nvec; i += 4 * stride) {
-    const u32x4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-    acc ^= a ^ b ^ c ^ d;
-  }
-  for (; i < nvec; i += stride) acc ^= p[i];
-  if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9E3779B9u && acc[0] == 0x7F4A7C15u) sink[0] = acc[1];
-}
-
-void launch_prefetch(const void* p, size_t bytes, int blocks, void* sink, hipStream_t s) {
-  const size_t nvec = bytes / 16;
-  if (!nvec) return;
-  const size_t need = (nvec + 1023) / 1024;
-  const int grid = (int)(need < (size_t)blocks ? need : (size_t)blocks);
-  prefetch_kernel<<<grid, 256, 0, s>>>((const u32x4*)p, nvec, (unsigned*)sink);
-}

@@ -38,7 +38,6 @@ void launch_rope_kv(const void* qkv, const int* pos, const int* slots, const voi
                     void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int D,
                     int BS, hipStream_t s);
 void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
-void launch_prefetch(const void* p, size_t bytes, int blocks, void* sink, hipStream_t s);
 
 // QKV projection + RoPE + paged K/V write fused in the GEMM epilogue (K1+K4+K10)
 // serving-size M: tile shape per (M, N) filling one wave of workgroups (gemm_flex.hip)
@@ -135,6 +134,16 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            float* split_o = nullptr, float* split_lse = nullptr, int rows = 0,
                            float* own_lse = nullptr);
 int attn_split_init();
+// decode-sized split-KV steps (attention_decode.hip): grid (items, Hkv, nz),
+// nz = attn_decode_blocks(max_blocks); nonzero = not launched
+int attn_decode_blocks(int max_blocks);
+int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, void* out,
+                       const int* q_start, const int* q_len, const int* ctx_len,
+                       const int* block_table, int max_blocks, const int* work_seq4,
+                       const int* work_q04, int nwork4, const int* work_seq1, const int* work_q01,
+                       int nwork1, int Hq, int Hkv, int head_dim, float scale, const int* kv_begin,
+                       const void* pre_o, const float* pre_lse, float* split_o, float* split_lse,
+                       int rows, int nz, hipStream_t s);
 int launch_paged_attention_mixed(const void* q, const void* k_cache, const void* v_cache,
                                  void* out, const int* q_start, const int* q_len,
                                  const int* ctx_len, const int* block_table, int max_blocks,

@@ -225,6 +225,22 @@ _SIDE = {}
 # split-KV steps as one launch with the combine fused (attention.hip MIXED);
 # MCP_ATTN_MIXED=0 keeps a launch + combine per work list
 _MIXED_SPLIT = os.environ.get("MCP_ATTN_MIXED", "1") == "1"
+# split-KV steps on the decode kernel (csrc/attention_decode.hip: key tiles
+# fixed by the grid position, every tile of a block in flight at once, the
+# waves merged in LDS); MCP_ATTN_DECODE=0 keeps the work-list split launch
+_DECODE_SPLIT = os.environ.get("MCP_ATTN_DECODE", "1") == "1"
+_DECODE_BLOCKS_PER_CU = 2
+
+
+_CUS = {}
+
+
+def _num_cus(device) -> int:
+    key = torch.device(device).index
+    n = _CUS.get(key)
+    if n is None:
+        n = _CUS[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    return n
 
 
 def _side_stream(device):
@@ -304,6 +320,27 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
                                    meta.pre_tokens, scale, pre_dims=pre_dims, **kw_split)
                 kw = {"kv_begin": meta.kv_begin, "pre_o": pre_o, "pre_lse": pre_lse}
         ns = int(getattr(meta, "kv_splits", 1))
+        if ns > 1 and _DECODE_SPLIT and not concurrent and hasattr(L, "paged_attention_decode"):
+            lists = {nw: (ws, wq) for nw, ws, wq in meta.work_lists()}
+            e = torch.empty(0, dtype=torch.int32, device=q.device)
+            ws4, wq4 = lists.get(4, (e, e))
+            ws1, wq1 = lists.get(1, (e, e))
+            nz = L.attn_decode_blocks(int(meta.block_table.shape[1]))
+            # a grid past two blocks per CU (several sequences with long spans
+            # and contexts) runs the work-list split launch below instead
+            # (profiles/attention_decode_r3.jsonl)
+            use_dec = ((4 * ws4.numel() + ws1.numel()) * k_cache.shape[1] * nz
+                       <= _DECODE_BLOCKS_PER_CU * _num_cus(q.device))
+        else:
+            use_dec = False
+        if use_dec:
+            so = torch.empty(nz if nz > 1 else 0, *q.shape, device=q.device, dtype=torch.float32)
+            sl = torch.empty(nz if nz > 1 else 0, q.shape[0], q.shape[1], device=q.device,
+                             dtype=torch.float32)
+            if L.paged_attention_decode(q, k_cache, v_cache, out, meta.q_start, meta.q_len,
+                                        meta.ctx_len, meta.block_table, ws4, wq4, ws1, wq1, scale,
+                                        nz, so, sl, **kw):
+                return out
         if ns > 1 and _MIXED_SPLIT and hasattr(L, "paged_attention_mixed"):
             # split-KV step (few sequences, long own contexts: config 2 / low
             # QPS) in ONE launch: both work lists, the combine fused in

@@ -210,6 +210,7 @@ def test_paged_attention_split_fused_vs_per_list(mixed, monkeypatch):
     ops._MIXED_SPLIT) and as per-list launches + attn_split_combine: both match
     fp32, and repeated launches re-arm the arrival tickets (same output)."""
     monkeypatch.setattr(ops, "_MIXED_SPLIT", mixed)
+    monkeypatch.setattr(ops, "_DECODE_SPLIT", False)
     q_lens, ctx_lens = [1, 3, 9, 70, 2], [5000, 65, 900, 700, 1200]
     outs = []
     for _ in range(3):
@@ -220,6 +221,29 @@ def test_paged_attention_split_fused_vs_per_list(mixed, monkeypatch):
     for Hq, Hkv in ((8, 1), (64, 8)):             # GQA groups 8 (70B TP=8 / TP=1)
         out, exp = _attn_case([1, 5], [3000, 800], Hq, Hkv, seed=10, kv_splits=4)
         assert rel_err(out, exp) < 2e-2
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (8, 8), (16, 8)])
+def test_paged_attention_decode_kernel(Hq, Hkv, monkeypatch):
+    """Split-KV steps on the decode kernel (csrc/attention_decode.hip: key
+    tiles fixed by the grid position, 4 waves on 4 tiles, LDS merge of the
+    waves, last-arriver merge of the blocks) against fp32: single sequences
+    with 1-16 new tokens over 64-4100 keys (one block / several blocks / one
+    tile past a block edge), narrow and wide items in one launch, a 70-token
+    span (5 wide items), tables wider than 256 blocks (several tiles per
+    wave), and bitwise-equal repeats (the arrival tickets re-arm)."""
+    monkeypatch.setattr(ops, "_DECODE_SPLIT", True)
+    monkeypatch.setattr(ops, "_DECODE_BLOCKS_PER_CU", 1 << 20)   # no fallback by grid size
+    cases = [([1], [64]), ([1], [700]), ([4], [1100]), ([16], [1025]), ([3], [4100]),
+             ([1, 3, 9, 70, 2], [5000, 65, 900, 700, 1200]), ([12, 1], [257, 16500])]
+    for i, (q_lens, ctx_lens) in enumerate(cases):
+        outs = []
+        for _ in range(2):
+            out, exp = _attn_case(q_lens, ctx_lens, Hq, Hkv, seed=20 + i, kv_splits=2)
+            assert rel_err(out, exp) < 2e-2, (q_lens, ctx_lens)
+            assert torch.isfinite(out.float()).all()
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1]), (q_lens, ctx_lens)
 
 
 def test_paged_attention_spike():
