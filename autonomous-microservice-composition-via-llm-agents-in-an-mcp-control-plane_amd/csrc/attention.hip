@@ -114,7 +114,7 @@ DEV void split_fused_epilogue(const AttnArgs& a, f32x4 (&o)[8], float m_run, flo
   if (z == 0 && merge_pre && qvalid) {
     const float lse_a = a.pre_lse[row];
     const float mx = fmaxf(lse_a, lse);
-    const float ea = exp2f(lse_a - mx), eb = lse == -INFINITY ? 0.f : exp2f(lse - mx);
+    const float ea = fexp2(lse_a - mx), eb = lse == -INFINITY ? 0.f : fexp2(lse - mx);
     wa = ea / (ea + eb);
     wb = eb / (ea + eb);
     lse = mx + __log2f(ea + eb);
@@ -177,7 +177,7 @@ DEV void split_fused_epilogue(const AttnArgs& a, f32x4 (&o)[8], float m_run, flo
     for (int dt = 0; dt < 8; ++dt)
       pj[dt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
           rso, (unsigned)((((size_t)j * a.rows + row) * D + 4 * fq + 16 * dt) * 4), 0, 16));
-    const float wj = lj == -INFINITY ? 0.f : exp2f(lj - mu);   // 0 for empty splits
+    const float wj = lj == -INFINITY ? 0.f : fexp2(lj - mu);   // 0 for empty splits
     den += wj;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) acc[dt] += pj[dt] * wj;
@@ -351,7 +351,7 @@ void attn_kernel(const AttnArgs a) {
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    const float alpha = fexp2(m_run - m_use);
     m_run = m_new;
     float psum = 0.f;
     bf16x8 pf[2];
@@ -359,7 +359,7 @@ void attn_kernel(const AttnArgs a) {
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sacc[nt][r] - m_use);
+        const float p = fexp2(sacc[nt][r] - m_use);
         psum += p;
         pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
       }
@@ -405,7 +405,7 @@ void attn_kernel(const AttnArgs a) {
     if (blockIdx.z == 0 && a.pre_o != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
       const float lse_a = a.pre_lse[row];
       const float mx = fmaxf(lse_a, lse);
-      const float ea = exp2f(lse_a - mx), eb = lse == -INFINITY ? 0.f : exp2f(lse - mx);
+      const float ea = fexp2(lse_a - mx), eb = lse == -INFINITY ? 0.f : fexp2(lse - mx);
       wa = ea / (ea + eb);
       wb = eb / (ea + eb);
       lse = mx + __log2f(ea + eb);
@@ -436,8 +436,8 @@ void attn_kernel(const AttnArgs a) {
     const float lse_b = m_run + __log2f(l_tot);
     const float lse_a = a.pre_lse[row];
     const float mx = fmaxf(lse_a, lse_b);
-    wa = exp2f(lse_a - mx);
-    wb = exp2f(lse_b - mx);
+    wa = fexp2(lse_a - mx);
+    wb = fexp2(lse_b - mx);
     const float den = 1.f / (wa + wb);
     wa *= den;
     wb *= den;
@@ -569,14 +569,14 @@ void attn_prefix_kernel(const AttnArgs a) {
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float m_new = fmaxf(m_run[r], tmax);
-      const float alpha = exp2f(m_run[r] - m_new);
+      const float alpha = fexp2(m_run[r] - m_new);
       m_run[r] = m_new;
       float psum = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = exp2f(sacc[r][nt][e] - m_new);
+          const float p = fexp2(sacc[r][nt][e] - m_new);
           psum += p;
           pf[r][nt >> 1][(nt & 1) * 4 + e] = (bf16)p;
         }
@@ -654,7 +654,7 @@ __global__ __launch_bounds__(256) void attn_split_combine(const AttnArgs a, int 
   const float mu = m == -INFINITY ? 0.f : m;
 #pragma unroll 4
   for (int z = wave; z < nsplit; z += CW) {
-    const float w = exp2f(a.split_lse[(size_t)z * a.rows + row] - mu);   // 0 for empty splits
+    const float w = fexp2(a.split_lse[(size_t)z * a.rows + row] - mu);   // 0 for empty splits
     den += w;
     const f32x4* p = reinterpret_cast<const f32x4*>(a.split_o + ((size_t)z * a.rows + row) * D + 32 * dq);
 #pragma unroll
@@ -678,7 +678,7 @@ __global__ __launch_bounds__(256) void attn_split_combine(const AttnArgs a, int 
 #pragma unroll
   for (int w = 0; w < CW; ++w) {
     const float mw = red_m[w][lane];
-    sc[w] = mw == -INFINITY ? 0.f : exp2f(mw - mtu);
+    sc[w] = mw == -INFINITY ? 0.f : fexp2(mw - mtu);
     dt += sc[w] * red_d[w][lane];
   }
   const float inv = dt > 0.f ? 1.f / dt : 0.f;
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(256) void attn_prefix_combine(const AttnArgs a, int
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float den = 0.f;
   for (int z = 0; z < nsplit; ++z) {
-    const float w = exp2f(a.split_lse[(size_t)z * a.rows + row] - mu);   // 0 for empty splits
+    const float w = fexp2(a.split_lse[(size_t)z * a.rows + row] - mu);   // 0 for empty splits
     den += w;
     const f32x4* p = reinterpret_cast<const f32x4*>(a.split_o + ((size_t)z * a.rows + row) * D + d0);
     const f32x4 v0 = p[0], v1 = p[1];
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(256) void attn_cascade_merge(const AttnArgs a) {
   const float la = a.pre_lse[row], lb = a.own_lse[row];
   const float mx = fmaxf(la, lb);
   const float mu = mx == -INFINITY ? 0.f : mx;
-  float wa = la == -INFINITY ? 0.f : exp2f(la - mu), wb = lb == -INFINITY ? 0.f : exp2f(lb - mu);
+  float wa = la == -INFINITY ? 0.f : fexp2(la - mu), wb = lb == -INFINITY ? 0.f : fexp2(lb - mu);
   const float den = wa + wb;
   wa = den > 0.f ? wa / den : 0.f;
   wb = den > 0.f ? wb / den : 0.f;

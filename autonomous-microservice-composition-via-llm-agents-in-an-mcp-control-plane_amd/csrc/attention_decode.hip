@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    const float alpha = fexp2(m_run - m_use);
     m_run = m_new;
     float psum = 0.f;
     bf16x8 pf[2];
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sacc[nt][r] - m_use);
+        const float p = fexp2(sacc[nt][r] - m_use);
         psum += p;
         pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
       }
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int w = 0; w < NWV; ++w) {
-      const float e = mw[w] == -INFINITY ? 0.f : exp2f(mw[w] - mu);
+      const float e = mw[w] == -INFINITY ? 0.f : fexp2(mw[w] - mu);
       den += e * s_ml[w][1][r];
       const float* src = reinterpret_cast<const float*>(smem + w * TILE) + r * D;
       acc0 += e * *reinterpret_cast<const f32x4*>(src + (((2 * c8) ^ r) << 2));
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
       if (merge_pre) {
         const float lp = a.pre_lse[grow];
         const float m2 = fmaxf(lp, lse);
-        const float wa = exp2f(lp - m2), wb = lse == -INFINITY ? 0.f : exp2f(lse - m2);
+        const float wa = fexp2(lp - m2), wb = lse == -INFINITY ? 0.f : fexp2(lse - m2);
         const float dn = 1.f / (wa + wb);
         const bf16x8 pa = *reinterpret_cast<const bf16x8*>(a.pre_o + grow * D + 8 * c8);
 #pragma unroll
@@ -336,13 +336,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
     const unsigned off = (unsigned)((((size_t)jz * a.rows + grow) * D + 8 * c8) * 4);
     const f32x4 p0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rso, off, 0, 16));
     const f32x4 p1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rso, off + 16, 0, 16));
-    const float wj = lj == -INFINITY ? 0.f : exp2f(lj - mu);
+    const float wj = lj == -INFINITY ? 0.f : fexp2(lj - mu);
     den += wj;
     acc0 += p0 * wj;
     acc1 += p1 * wj;
   }
   if (merge_pre) {
-    const float wp = exp2f(lp - mu);
+    const float wp = fexp2(lp - mu);
     den += wp;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -34,6 +34,12 @@ DEV float wave_max(float v) {
   return v;
 }
 
+// 2^x as the bare v_exp_f32: exp2f adds a denormal-range fixup (compare,
+// select, ldexp: ~4 extra VALU ops per call, a third of the softmax VALU of
+// the attention loops); results below 2^-126 flush to 0, which a softmax
+// weight can take
+DEV float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 DEV f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
