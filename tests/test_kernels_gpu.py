@@ -412,11 +412,13 @@ def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, concurrent, 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 8)])
 @pytest.mark.parametrize("T", [1, 77, 300])
-@pytest.mark.parametrize("rt", ["1", "2", "4"])
+@pytest.mark.parametrize("rt", ["1", "2", "4", "32", "3"])
 def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
     """The shared-prefix pass alone (normalised O and its log2-sum-exp over
     the prefix keys) in every row-tile form (1 = MODE 1 of attn_kernel, 2 / 4
-    = attn_prefix_kernel: each LDS fragment feeds 2 / 4 row tiles) against
+    = attn_prefix_kernel: each LDS fragment feeds 2 / 4 row tiles, 32 =
+    attn_prefix32_kernel on 32x32x16 MFMAs with the lazy max, 3 = its
+    ping-pong 8-wave form attn_prefix_pp_kernel) against
     fp32 softmax attention; T covers partial row tiles and blocks."""
     monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
     torch.manual_seed(11)
@@ -438,6 +440,35 @@ def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
     exp_lse = (torch.logsumexp(s, -1) / math.log(2)).reshape(T, Hq)
     assert rel_err(out, exp_o) < 2e-2
     assert torch.allclose(lse, exp_lse, atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("rt", ["2", "32", "3"])
+def test_prefix_pass_growing_max(rt, monkeypatch):
+    """Keys whose scale grows tile by tile (the row max jumps by far more than
+    the 2^8 headroom of the lazy running max of the 32x32 form, and by less
+    in some tiles): O and LSE still match fp32 softmax attention."""
+    monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
+    torch.manual_seed(12)
+    Hq, Hkv, D, P, T = 32, 8, 128, 768, 200
+    n_pre = P // 64
+    kc, vc = _cache(n_pre, Hkv)
+    ramp = torch.tensor([0.5, 4.0, 1.0, 8.0, 8.5, 2.0, 16.0, 3.0, 16.5, 30.0, 1.0, 31.0],
+                        device=DEV)[:n_pre]
+    kc = (kc.float() * ramp.view(-1, 1, 1, 1)).bfloat16()
+    pre_bt = torch.arange(n_pre, dtype=torch.int32, device=DEV)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    out = torch.empty_like(q)
+    lse = torch.empty(T, Hq, device=DEV, dtype=torch.float32)
+    scale = 1 / math.sqrt(D)
+    ops.lib().prefix_attention(q, kc, vc, out, lse, pre_bt, P, T, scale)
+    G = Hq // Hkv
+    k = kc.float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    v = vc.float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    s = torch.einsum("thgd,hpd->thgp", q.float().view(T, Hkv, G, D), k) * scale
+    exp_o = torch.einsum("thgp,hpd->thgd", torch.softmax(s, -1), v).reshape(T, Hq, D)
+    exp_lse = (torch.logsumexp(s, -1) / math.log(2)).reshape(T, Hq)
+    assert rel_err(out, exp_o) < 2e-2
+    assert torch.allclose(lse, exp_lse, atol=5e-2, rtol=1e-3)
 
 
 @pytest.mark.parametrize("M,F,K", [(7, 512, 256), (300, 1792, 4096), (3000, 14336, 4096), (520, 3584, 1024)])

@@ -18,7 +18,9 @@ def _worker(rank, world, port, q):
     idx = ShardedIndex(dist.group.WORLD, "cpu")
     idx.set_corpus(corpus)
     v, i = idx.search(queries, 7)
-    q.put((rank, v, i))
+    # plain lists: a torch tensor in the queue is shared by file descriptor,
+    # which the parent can no longer fetch once this process has exited
+    q.put((rank, v.tolist(), i.tolist()))
     dist.destroy_process_group()
 
 
@@ -43,5 +45,5 @@ def test_sharded_topk_matches_global():
     for p in ps:
         p.join(timeout=30)
     for rank, v, i in out:
-        assert torch.allclose(v, rv, atol=1e-6)
-        assert torch.equal(i, ri)
+        assert torch.allclose(torch.tensor(v), rv, atol=1e-6)
+        assert torch.equal(torch.tensor(i, dtype=ri.dtype), ri)

@@ -20,7 +20,7 @@ Hq, Hkv, D = 32, 8, 128
 # "a:b" alternates requests of a and b new tokens (mixed decode / jump-forward steps)
 qls = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "16").split(":")]
 import os
-S, prefix = int(os.environ.get("ATTN_S", "256")), 704      # ATTN_S: requests in the step
+S, prefix = int(os.environ.get("ATTN_S", "256")), int(os.environ.get("ATTN_PREFIX", "704"))  # ATTN_S: requests in the step
 ql_s = np.array([qls[s % len(qls)] for s in range(S)], np.int32)
 ql = int(ql_s.max())
 own = int(os.environ.get("ATTN_OWN", "200"))
