@@ -840,7 +840,7 @@ void attn_prefix32_kernel(const AttnArgs a) {
 // DMA goes out at the end of phase 2t (its buffer's last reader, tile t - 2,
 // finished in phase 2t - 1) and lands before the barrier that ends 2t + 1.
 // Same LDS image, operand maps and lazy max as attn_prefix32_kernel.
-template <int G, int DBG = 0, int PP_RING = 2>
+template <int G, int PP_RING = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void attn_prefix_pp_kernel(const AttnArgs a) {
   constexpr int NW = 8;
@@ -965,19 +965,12 @@ void attn_prefix_pp_kernel(const AttnArgs a) {
   auto U = [&](int t) {
     Kl = reinterpret_cast<const char*>(smem + (t % 3) * 2 * TILE);
     Vl = reinterpret_cast<const char*>(smem + ((t + 2) % 3) * 2 * TILE + TILE);   // tile t - 1
-    const bool pv = t >= 1 && DBG != 2, sk = t < ntiles;
+    const bool pv = t >= 1, sk = t < ntiles;
     if (pv && sk) groups(std::integral_constant<int, 0>{}, std::integral_constant<int, 8>{});
     else if (pv) groups(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
     else if (sk) groups(std::integral_constant<int, 4>{}, std::integral_constant<int, 8>{});
   };
   auto X = [&]() {                            // softmax of sacc -> pf, lazy max
-    if (DBG == 1) {                           // timing probe: no softmax arithmetic
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) pf[kh][i >> 3][i & 7] = (bf16)sacc[kh][i];
-      return;
-    }
     float tmax = sacc[0][0];
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
@@ -1264,10 +1257,7 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
     return a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
   };
   if (rt == 3) {
-    static const int dbg = getenv("MCP_ATTN_PP_DBG") ? atoi(getenv("MCP_ATTN_PP_DBG")) : 0;
-    if (dbg == 1) attn_prefix_pp_kernel<G, 1><<<grid_for(8 * (32 / G)), 512, 0, s>>>(a);
-    else if (dbg == 2) attn_prefix_pp_kernel<G, 2><<<grid_for(8 * (32 / G)), 512, 0, s>>>(a);
-    else attn_prefix_pp_kernel<G><<<grid_for(8 * (32 / G)), 512, 0, s>>>(a);
+    attn_prefix_pp_kernel<G><<<grid_for(8 * (32 / G)), 512, 0, s>>>(a);
     return;
   }
   if (rt == 32) {
