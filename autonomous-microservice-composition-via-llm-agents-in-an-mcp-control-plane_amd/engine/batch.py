@@ -38,6 +38,9 @@ class AttnMeta:
     pre_keys: int = 0                         # shared prefix keys (multiple of 64)
     pre_tokens: int = 0                       # flat tokens [0, pre_tokens) attend to it
     kv_splits: int = 1                        # split-KV factor of the 1-wave items (K6)
+    # hipGraph static layout: the work lists are padded to the key's capacity
+    # (their lengths are not the step's item counts)
+    padded: bool = False
     # hipGraph steps: device [pre_tokens, pre_keys] (the host ints above are
     # then the bucket's capacities, engine/graphs.py)
     pre_dims: Optional[torch.Tensor] = None
@@ -342,7 +345,8 @@ def views(t: torch.Tensor, layout):
         if ws.numel():
             work_l.append((nw, ws, wq))
     meta = AttnMeta(q_start=vs[4], q_len=vs[5], ctx_len=vs[6], block_table=bt, work=work_l,
-                    kv_splits=int(layout[N_SIZES + 2]) if len(layout) > N_SIZES + 2 else 1)
+                    kv_splits=int(layout[N_SIZES + 2]) if len(layout) > N_SIZES + 2 else 1,
+                    padded=len(layout) > N_SIZES + 3 and bool(layout[N_SIZES + 3]))
     if pre_tokens > 0:
         meta.kv_begin, meta.pre_bt = vs[14], vs[15]
         meta.pre_keys, meta.pre_tokens = int(vs[15].numel()) * BLOCK_SIZE, pre_tokens

@@ -244,7 +244,7 @@ class GraphRunner:
         buf.copy_(torch.from_numpy(self.pack_static(None, b, w, sb=sb)))
         # pre_tokens -1: cascade sizes live on the device (batch.views); the
         # graphs of non-cascade steps launch no prefix pass at all
-        e.dstep, e.csrc, e.cdst = views(buf, sizes + [S_b, -1 if casc else 0, ns])
+        e.dstep, e.csrc, e.cdst = views(buf, sizes + [S_b, -1 if casc else 0, ns, 1])
         self._body(e)                                   # eager warm-up (lazy allocations)
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()

@@ -230,6 +230,7 @@ _MIXED_SPLIT = os.environ.get("MCP_ATTN_MIXED", "1") == "1"
 # waves merged in LDS); MCP_ATTN_DECODE=0 keeps the work-list split launch
 _DECODE_SPLIT = os.environ.get("MCP_ATTN_DECODE", "1") == "1"
 _DECODE_BLOCKS_PER_CU = 2
+_DECODE_FORCE = os.environ.get("MCP_ATTN_DECODE_FORCE", "0") == "1"
 
 
 _CUS = {}
@@ -328,9 +329,16 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
             nz = L.attn_decode_blocks(int(meta.block_table.shape[1]))
             # a grid past two blocks per CU (several sequences with long spans
             # and contexts) runs the work-list split launch below instead
-            # (profiles/attention_decode_r3.jsonl)
-            use_dec = ((4 * ws4.numel() + ws1.numel()) * k_cache.shape[1] * nz
-                       <= _DECODE_BLOCKS_PER_CU * _num_cus(q.device))
+            # (profiles/attention_decode_r3.jsonl).  A hipGraph step's lists are
+            # padded to the key's capacity (52 items at the smallest key), so
+            # the rule would always reject it there; a split key is only chosen
+            # for fewer than num_cus / Hkv real items (batch.choose_kv_splits)
+            # and its padding items exit at once: graph steps take the decode
+            # kernel (config 2 p50 99.1 -> 94.3 ms, config 5 at 20 / 40
+            # intents/s equal, profiles/attention_decode_graph_ab.jsonl)
+            use_dec = _DECODE_FORCE or getattr(meta, "padded", False) or (
+                (4 * ws4.numel() + ws1.numel()) * k_cache.shape[1] * nz
+                <= _DECODE_BLOCKS_PER_CU * _num_cus(q.device))
         else:
             use_dec = False
         if use_dec:
