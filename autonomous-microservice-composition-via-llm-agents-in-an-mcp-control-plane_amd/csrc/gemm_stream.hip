@@ -362,8 +362,10 @@ bool gemm_stream_pick(int M, int N, int K, int epi) {
   if (M > 64) return false;
   // gate|up (N >= 16384): cold-weight sweep (tools/bench_cold_stream.py), the
   // stream kernel beats split-K 128^2 at M = 9-32 (48.9-55.3 vs 51.3-59.7 us);
-  // M <= 8 / 12 go to the skinny kernel first (gemm.hip skinny_first)
-  if (N >= 16384) return M > 8 && M <= 32;
+  // M <= 8 / 12 go to the skinny kernel first (gemm.hip skinny_first).
+  // MCP_STREAM_WIDE_MAXM: upper M for the wide projections (A/B)
+  static const int wide_max = getenv("MCP_STREAM_WIDE_MAXM") ? atoi(getenv("MCP_STREAM_WIDE_MAXM")) : 32;
+  if (N >= 16384) return M > 8 && M <= wide_max;
   if (M <= 32 || epi == 3) return true;
   return (long long)N * K <= 4096LL * 4096LL;
 }
