@@ -28,8 +28,6 @@
 // attn_split_combine merges the splits with LSE weights.
 #include <stdlib.h>
 
-#include <type_traits>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -625,419 +623,6 @@ void attn_prefix_kernel(const AttnArgs a) {
   }
 }
 
-// Shared-prefix pass on 32x32x16 MFMAs: one wave per SIMD, two 32-row tiles
-// per wave (64 query rows = 64 / G tokens x G heads), 4 waves = 256 rows per
-// block.  A 32x32x16 MFMA does twice the work of a 16x16x32 one for the same
-// 8 issue cycles and the same 1 KiB fragment read, so against the two 16-row
-// tiles of attn_prefix_kernel each K / V byte read from LDS feeds twice the
-// MACs and the softmax VALU has twice the issue slots beside the MFMAs - the
-// two bounds of that pass (LDS port and VALU issue, profiles/attention_tuning.md).
-//   S^T[key][row] = K . Q^T: A = K fragment (32 keys x 16 d, ds_read_b128),
-//     B = Q^T held in registers; lane (r = l & 31, h = l >> 5) owns query row
-//     r and keys 8 (i >> 2) + 4 h + (i & 3) of each 32-key half (reg i);
-//   O^T[d][row] += V^T . P^T: P^T is the S^T accumulator itself (registers
-//     8 s .. 8 s + 7 are the B fragment of k-step s, cdna_hip_programming.md
-//     §3), V^T read with ds_read_b64_tr_b16 in the same permuted key order.
-// LDS image: 256-B rows, chunk c of row r at c ^ ((r & 3) << 2 | (r >> 2) & 3)
-// - conflict-free for both the 32-row b128 reads and the 32x32x16 transposed
-// reads (tools/lds_banks.py; the ^ (r & 15) image of the 16-row forms is
-// 4-way on these transposed reads).
-// Softmax with a lazy running max (rescale O and the sum only when a row's
-// max grows by more than 2^8, wave-uniform branch): P <= 256 in bf16 and the
-// fp32 sums are exact either way; the final normalisation divides it out.
-template <int G>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
-void attn_prefix32_kernel(const AttnArgs a) {
-  constexpr int NW = 4, RT = 2;                 // (the P fence below names RT = 2 tiles)
-  constexpr int TPT = 32 / G;                 // tokens per 32-row tile
-  constexpr int QT = NW * RT * TPT;           // tokens per block
-  constexpr float LAZY = 8.f;                 // log2 headroom of the stale max
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];   // [buf][K|V][64][128]
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kvh = a.head_major ? blockIdx.x : blockIdx.y;
-  const int qblk = a.head_major ? blockIdx.y : blockIdx.x;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int head = kvh * G + r32 % G;
-  const int Hq = a.Hq, Hkv = a.Hkv;
-  const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
-  const int pre_keys = a.pre_dims ? a.pre_dims[1] : a.pre_keys;
-  if (qblk * QT >= pre_tokens) return;        // whole block idle (before any barrier)
-  const int ntiles = pre_keys / KT;
-  auto swz = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
-
-  int tok[RT];
-  bf16x8 qf[RT][8];                           // B operand of k-step ks: Q[row r32][d = 16 ks + 8 h + j]
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-    tok[r] = qblk * QT + (wave * RT + r) * TPT + r32 / G;
-    const bool v = tok[r] < pre_tokens;
-    const bf16* qp = a.q + ((size_t)(v ? tok[r] : 0) * Hq + head) * D + 8 * h;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      qf[r][ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-      if (!v) qf[r][ks] = bf16x8{};
-    }
-  }
-
-  // staging: 1 KiB piece p = 4 rows of the K (p < 16) or V tile, lane-linear
-  // in LDS (row 4 pr + lane / 16, stored chunk lane & 15)
-  auto stage = [&](int kt, int buf) {
-    const size_t blk = (size_t)a.pre_bt[kt];
-    const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
-    const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
-    bf16* base = smem + buf * 2 * TILE;
-#pragma unroll
-    for (int i = 0; i < 32 / NW; ++i) {
-      const int p = wave * (32 / NW) + i;
-      const int tile = p >> 4, pr = p & 15;
-      const int row = pr * 4 + (lane >> 4);
-      const int chunk = (lane & 15) ^ swz(row);
-      glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
-    }
-  };
-
-  // O^T[d = 32 db + (i & 3) + 8 (i >> 2) + 4 h][row r32], in AGPRs: the P.V
-  // MFMAs are inline asm with "+a" accumulators (hipcc otherwise shuttles the
-  // 128 registers between AGPRs and VGPRs every iteration around the rescale
-  // branch); the pads the compiler does not insert for asm are explicit:
-  // VALU write -> MFMA operand 2 states, MFMA result -> VALU 18 states
-  f32x16 o[RT][4];
-  float m_run[RT], l_part[RT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-#pragma unroll
-    for (int db = 0; db < 4; ++db) o[r][db] = f32x16{};
-    m_run[r] = -INFINITY;
-    l_part[r] = 0.f;
-  }
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-    asm volatile("s_nop 4" : "+a"(o[r][0]), "+a"(o[r][1]), "+a"(o[r][2]), "+a"(o[r][3]));
-  const float sl2 = a.scale_log2;
-
-  // per-lane LDS byte offsets: K fragment (kh, ks) reads row 32 kh + r32,
-  // chunk 2 ks + h; V^T fragment (db, kh, s, second) is a transposed read of
-  // rows 32 kh + 16 s + 8 second + 4 h + q, columns 32 db + 16 (g & 1) + 4 p
-  // (group g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3)
-  const int tq = (lane & 15) >> 2, tp = lane & 3, g1 = (lane >> 4) & 1;
-
-  if (ntiles > 0) stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
-    const char* Kl = reinterpret_cast<const char*>(smem + cur * 2 * TILE);
-    const char* Vl = Kl + TILE * 2;
-
-    // each 32-key half is one online-softmax step (32 S^T registers live per
-    // row tile instead of 64: with the Q fragments and both row tiles that
-    // keeps the loop inside 256 VGPRs next to the 128 AGPRs of O)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      // ---- S^T = K Q^T: each K fragment feeds both row tiles
-      f32x16 sacc[RT];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) sacc[r] = f32x16{};
-      const int row = 32 * kh + r32;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * 256 + 16 * ((2 * ks + h) ^ swz(row)));
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          sacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[r][ks], sacc[r], 0, 0, 0);
-      }
-      // ---- online softmax, lazy max (log2 domain: score x scale_log2)
-      bf16x8 pf[RT][2];                       // [row tile][k-step]
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        float tmax = sacc[r][0];
-#pragma unroll
-        for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, sacc[r][i]);
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * sl2;
-        if (__builtin_amdgcn_ballot_w64(tmax > m_run[r] + LAZY)) {   // wave-uniform
-          const float m_new = fmaxf(m_run[r], tmax);
-          const float alpha = fexp2(m_run[r] - m_new);
-          m_run[r] = m_new;
-          l_part[r] *= alpha;
-          asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 2"
-                       : "+a"(o[r][0]), "+a"(o[r][1]), "+a"(o[r][2]), "+a"(o[r][3]));
-#pragma unroll
-          for (int db = 0; db < 4; ++db) o[r][db] *= alpha;
-          asm volatile("s_nop 1" : "+a"(o[r][0]), "+a"(o[r][1]), "+a"(o[r][2]), "+a"(o[r][3]));
-        }
-        const float mneg = -m_run[r];
-        float psum = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fexp2(__builtin_fmaf(sacc[r][i], sl2, mneg));
-          psum += p;
-          pf[r][i >> 3][i & 7] = (bf16)p;
-        }
-        l_part[r] += psum;
-      }
-      // P (VALU-written) -> MFMA operand: 2 states, once for all of them
-      asm volatile("s_nop 1" : "+v"(pf[0][0]), "+v"(pf[0][1]), "+v"(pf[1][0]), "+v"(pf[1][1]));
-      // ---- O^T += V^T P^T: each transposed V fragment feeds both row tiles
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const int col = 32 * db + 16 * g1 + 4 * tp;        // bf16 column of this lane's address
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const int key0 = 32 * kh + 16 * st + 4 * h + tq, key1 = key0 + 8;
-          const bf16x4 v0 = tr_read(reinterpret_cast<const bf16*>(
-              Vl + key0 * 256 + 16 * ((col >> 3) ^ swz(key0)) + 2 * (col & 7)));
-          const bf16x4 v1 = tr_read(reinterpret_cast<const bf16*>(
-              Vl + key1 * 256 + 16 * ((col >> 3) ^ swz(key1)) + 2 * (col & 7)));
-          const bf16x8 vf = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-          for (int r = 0; r < RT; ++r)
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
-                         : "+a"(o[r][db]) : "v"(vf), "v"(pf[r][st]));
-        }
-      }
-    }
-    __syncthreads();             // its fence also drains the next tile's LDS-DMA
-  }
-
-  // ---- normalise and store: lane holds O[row r32][d = 32 db + 8 b + 4 h + (0..3)]
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 2"
-                 : "+a"(o[r][0]), "+a"(o[r][1]), "+a"(o[r][2]), "+a"(o[r][3]));
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-    const float l_tot = l_part[r] + __shfl_xor(l_part[r], 32, 64);
-    if (tok[r] >= pre_tokens) continue;
-    const size_t row = (size_t)tok[r] * Hq + head;
-    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-    if (h == 0) a.lse_out[row] = m_run[r] + __log2f(l_tot);
-    bf16* op = a.out + row * D + 4 * h;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        bf16x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[r][db][4 * b + e] * inv);
-        *reinterpret_cast<bf16x4*>(op + 32 * db + 8 * b) = w;
-      }
-  }
-}
-
-// Shared-prefix pass, ping-pong form: 8 waves = two per SIMD, one 32-row tile
-// (32 / G tokens x G heads) each on 32x32x16 MFMAs, and the two waves of a
-// SIMD half a step apart, so one runs its MFMA segment while the other runs
-// its softmax (the regime of MI355X_MICROARCH.md "Two waves per SIMD").  The
-// lock-step forms above put both waves of a SIMD in the same segment: every
-// MFMA segment then waits out a VALU-only one (measured ~25-30 % of the MFMA
-// peak for both).  Per key tile t and wave:
-//   U(t): O^T += V(t-1)^T P(t-1)^T  and  S^T(t) = K(t) Q^T    (32 MFMAs)
-//   X(t): lazy-max online softmax of S(t) -> P(t), rescale    (VALU)
-// Phase p (one barrier after each): waves 0-3 run U(p / 2) on even p and
-// X(p / 2) on odd p, waves 4-7 one phase later.  K / V tiles rotate through
-// 3 LDS buffers (96 KiB): tile t is read in phases 2t .. 2t + 3, tile t + 1's
-// DMA goes out at the end of phase 2t (its buffer's last reader, tile t - 2,
-// finished in phase 2t - 1) and lands before the barrier that ends 2t + 1.
-// Same LDS image, operand maps and lazy max as attn_prefix32_kernel.
-template <int G, int PP_RING = 2>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void attn_prefix_pp_kernel(const AttnArgs a) {
-  constexpr int NW = 8;
-  constexpr int TPT = 32 / G;                 // tokens per 32-row tile
-  constexpr int QT = NW * TPT;                // tokens per block
-  constexpr float LAZY = 8.f;
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * 2 * TILE];   // [buf][K|V][64][128]
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int half = wave >> 2;
-  const int kvh = a.head_major ? blockIdx.x : blockIdx.y;
-  const int qblk = a.head_major ? blockIdx.y : blockIdx.x;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int head = kvh * G + r32 % G;
-  const int Hq = a.Hq, Hkv = a.Hkv;
-  const int pre_tokens = a.pre_dims ? a.pre_dims[0] : a.pre_tokens;
-  const int pre_keys = a.pre_dims ? a.pre_dims[1] : a.pre_keys;
-  if (qblk * QT >= pre_tokens) return;        // whole block idle (before any barrier)
-  const int ntiles = pre_keys / KT;
-  auto swz = [](int row) { return ((row & 3) << 2) | ((row >> 2) & 3); };
-
-  const int tok = qblk * QT + wave * TPT + r32 / G;
-  const bool qvalid = tok < pre_tokens;
-  bf16x8 qf[8];                               // B operand of k-step ks: Q[row r32][d = 16 ks + 8 h + j]
-  {
-    const bf16* qp = a.q + ((size_t)(qvalid ? tok : 0) * Hq + head) * D + 8 * h;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      qf[ks] = *reinterpret_cast<const bf16x8*>(qp + 16 * ks);
-      if (!qvalid) qf[ks] = bf16x8{};
-    }
-  }
-
-  // the tile's 32 DMA pieces, 8 per wave of waves 0-3 (pieces 16 wave ..
-  // + 7 of K | V), issued at the END of their U segment: hipcc puts a
-  // vmcnt(0) in front of every ds_read_b64_tr_b16 that follows an LDS-DMA of
-  // the same wave (the transposed-read builtin carries no alias info), so a
-  // DMA issued ahead of a U segment would wait out its own latency there.
-  // Issued after it, the DMA is in flight through the wave's X segment (no
-  // transposed reads) and lands before the barrier that ends it.
-  // the prefix block table, one entry per lane (read once; a per-tile load
-  // would put an L2 round trip in front of every DMA issue)
-  const int bt_lane = lane < ntiles ? a.pre_bt[lane] : 0;
-  auto stage = [&](int kt) {
-    const size_t blk = (size_t)(kt < 64 ? __builtin_amdgcn_readlane(bt_lane, kt) : a.pre_bt[kt]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int p = wave * 8 + i;
-      const int tile = p >> 4, pr = p & 15;
-      const int row = pr * 4 + (lane >> 4);
-      const int chunk = (lane & 15) ^ swz(row);
-      glds16((tile ? a.vc : a.kc) + (blk * Hkv + kvh) * (size_t)TILE + row * D + chunk * 8,
-             smem + (kt % 3) * 2 * TILE + tile * TILE + pr * 512);
-    }
-  };
-
-  f32x16 o[4];                                // O^T[d = 32 db + (i & 3) + 8 (i >> 2) + 4 h][row r32]
-#pragma unroll
-  for (int db = 0; db < 4; ++db) o[db] = f32x16{};
-  f32x16 sacc[2];                             // S^T of the current tile, per 32-key half
-  bf16x8 pf[2][2];                            // P^T of the previous tile [key half][k-step]
-  float m_run = -INFINITY, l_part = 0.f;
-  const float sl2 = a.scale_log2;
-  const int tq = (lane & 15) >> 2, tp = lane & 3, g1 = (lane >> 4) & 1;
-
-  // U(t) as 8 groups of 4 MFMAs - groups 0-3: P.V for d-block g; groups 4-7:
-  // S for key half (g - 4) / 2, d-steps 4 ((g - 4) & 1) .. + 3 - with the LDS
-  // fragments of group g + PP_RING - 1 read while group g's MFMAs run (a
-  // rolling register ring).  Reading each group's fragments right before its
-  // MFMAs exposed the LDS latency on every group: the probe without the P.V
-  // half ran 32 % faster, without the softmax only 7 %.
-  const char* Kl = nullptr;
-  const char* Vl = nullptr;
-  auto load = [&](int g, bf16x8 (&f)[4]) {
-    if (g < 4) {
-      const int col = 32 * g + 16 * g1 + 4 * tp;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kh = j >> 1, st = j & 1;
-        const int key0 = 32 * kh + 16 * st + 4 * h + tq, key1 = key0 + 8;
-        const bf16x4 v0 = tr_read(reinterpret_cast<const bf16*>(
-            Vl + key0 * 256 + 16 * ((col >> 3) ^ swz(key0)) + 2 * (col & 7)));
-        const bf16x4 v1 = tr_read(reinterpret_cast<const bf16*>(
-            Vl + key1 * 256 + 16 * ((col >> 3) ^ swz(key1)) + 2 * (col & 7)));
-        f[j] = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      }
-    } else {
-      const int row = 32 * ((g - 4) >> 1) + r32;
-      const int ks0 = 4 * ((g - 4) & 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        f[j] = *reinterpret_cast<const bf16x8*>(Kl + row * 256 + 16 * ((2 * (ks0 + j) + h) ^ swz(row)));
-    }
-  };
-  auto comp = [&](int g, const bf16x8 (&f)[4]) {
-    if (g < 4) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[j], pf[j >> 1][j & 1], o[g], 0, 0, 0);
-    } else {
-      const int kh = (g - 4) >> 1, ks0 = 4 * ((g - 4) & 1);
-      if (ks0 == 0) sacc[kh] = f32x16{};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        sacc[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[j], qf[ks0 + j], sacc[kh], 0, 0, 0);
-    }
-  };
-  auto groups = [&](auto g0c, auto g1c) {
-    constexpr int G0 = decltype(g0c)::value, G1 = decltype(g1c)::value;
-    constexpr int R = PP_RING;
-    bf16x8 F[R][4];
-#pragma unroll
-    for (int g = G0; g < G0 + R - 1 && g < G1; ++g) load(g, F[g - G0]);
-#pragma unroll
-    for (int g = G0; g < G1; ++g) {
-      if (g + R - 1 < G1) load(g + R - 1, F[(g - G0 + R - 1) % R]);
-      __builtin_amdgcn_sched_barrier(0);
-      comp(g, F[(g - G0) % R]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  auto U = [&](int t) {
-    Kl = reinterpret_cast<const char*>(smem + (t % 3) * 2 * TILE);
-    Vl = reinterpret_cast<const char*>(smem + ((t + 2) % 3) * 2 * TILE + TILE);   // tile t - 1
-    const bool pv = t >= 1, sk = t < ntiles;
-    if (pv && sk) groups(std::integral_constant<int, 0>{}, std::integral_constant<int, 8>{});
-    else if (pv) groups(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
-    else if (sk) groups(std::integral_constant<int, 4>{}, std::integral_constant<int, 8>{});
-  };
-  auto X = [&]() {                            // softmax of sacc -> pf, lazy max
-    float tmax = sacc[0][0];
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, sacc[kh][i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * sl2;
-    if (__builtin_amdgcn_ballot_w64(tmax > m_run + LAZY)) {   // wave-uniform
-      const float m_new = fmaxf(m_run, tmax);
-      const float alpha = fexp2(m_run - m_new);
-      m_run = m_new;
-      l_part *= alpha;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) o[db] *= alpha;
-    }
-    const float mneg = -m_run;
-    float psum = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fexp2(__builtin_fmaf(sacc[kh][i], sl2, mneg));
-        psum += p;
-        pf[kh][i >> 3][i & 7] = (bf16)p;
-      }
-    l_part += psum;
-  };
-
-  // prologue: tiles 0 and 1 loaded (waves 0-3), landed for every wave
-  if (half == 0) {
-    if (ntiles > 0) stage(0);
-    if (ntiles > 1) stage(1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int nphase = 2 * ntiles + 2;
-  for (int p = 0; p < nphase; ++p) {
-    const int t = p >> 1;
-    const int q = p - half;                   // this wave's own phase index
-    if (q >= 0) {
-      if ((q & 1) == 0) U(q >> 1);
-      else if ((q >> 1) < ntiles) X();
-    }
-    // waves 0-3, after U(t) in phase 2t: tile t + 1 (its buffer's last
-    // reader, tile t - 2's P.V, finished in phase 2t - 1)
-    if (half == 0 && (p & 1) == 0 && t >= 1 && t + 1 < ntiles) stage(t + 1);
-    if (p & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t + 1 landed
-    __syncthreads();
-  }
-
-  // ---- normalise and store: lane holds O[row r32][d = 32 db + 8 b + 4 h + (0..3)]
-  const float l_tot = l_part + __shfl_xor(l_part, 32, 64);
-  if (!qvalid) return;
-  const size_t row = (size_t)tok * Hq + head;
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  if (h == 0) a.lse_out[row] = m_run + __log2f(l_tot);
-  bf16* op = a.out + row * D + 4 * h;
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      bf16x4 w;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = (bf16)(o[db][4 * b + e] * inv);
-      *reinterpret_cast<bf16x4*>(op + 32 * db + 8 * b) = w;
-    }
-}
-
 // Merge of the split-KV partials of 1-wave items: one workgroup per (item,
 // kv head) = 16 rows (TPW tokens x G heads).  Wave w takes splits w, w + 4,
 // ...; lane = (row l & 15, 32-wide d slice).  Each wave keeps its own running
@@ -1250,21 +835,12 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
   // 1 = the attn_kernel MODE 1 forms below, A/B)
   // (read per launch: the GPU tests compare the forms in one process)
   const char* rt_env = getenv("MCP_ATTN_PREFIX_RT");
-  // (3 = ping-pong 32x32x16 form; 32 = its one-wave-per-SIMD form)
   const int rt = rt_env ? atoi(rt_env) : 2;
-  auto grid_for = [&](int qt) {
-    const int nblk = (a.pre_tokens + qt - 1) / qt;
-    return a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
-  };
-  if (rt == 3) {
-    attn_prefix_pp_kernel<G><<<grid_for(8 * (32 / G)), 512, 0, s>>>(a);
-    return;
-  }
-  if (rt == 32) {
-    attn_prefix32_kernel<G><<<grid_for(4 * 2 * (32 / G)), 256, 0, s>>>(a);
-    return;
-  }
   if (rt == 2 || rt == 4) {
+    auto grid_for = [&](int qt) {
+      const int nblk = (a.pre_tokens + qt - 1) / qt;
+      return a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
+    };
     if (rt == 4)
       attn_prefix_kernel<4, G, 4><<<grid_for(4 * 4 * (16 / G)), 256, 0, s>>>(a);
     else if (prefix_nw() == 4)

@@ -412,13 +412,11 @@ def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, concurrent, 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 8)])
 @pytest.mark.parametrize("T", [1, 77, 300])
-@pytest.mark.parametrize("rt", ["1", "2", "4", "32", "3"])
+@pytest.mark.parametrize("rt", ["1", "2", "4"])
 def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
     """The shared-prefix pass alone (normalised O and its log2-sum-exp over
     the prefix keys) in every row-tile form (1 = MODE 1 of attn_kernel, 2 / 4
-    = attn_prefix_kernel: each LDS fragment feeds 2 / 4 row tiles, 32 =
-    attn_prefix32_kernel on 32x32x16 MFMAs with the lazy max, 3 = its
-    ping-pong 8-wave form attn_prefix_pp_kernel) against
+    = attn_prefix_kernel: each LDS fragment feeds 2 / 4 row tiles) against
     fp32 softmax attention; T covers partial row tiles and blocks."""
     monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
     torch.manual_seed(11)
@@ -442,11 +440,11 @@ def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
     assert torch.allclose(lse, exp_lse, atol=2e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("rt", ["2", "32", "3"])
+@pytest.mark.parametrize("rt", ["1", "2"])
 def test_prefix_pass_growing_max(rt, monkeypatch):
-    """Keys whose scale grows tile by tile (the row max jumps by far more than
-    the 2^8 headroom of the lazy running max of the 32x32 form, and by less
-    in some tiles): O and LSE still match fp32 softmax attention."""
+    """Keys whose scale grows tile by tile (the online-softmax max jumps by
+    large and small amounts between tiles): O and LSE still match fp32
+    softmax attention."""
     monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
     torch.manual_seed(12)
     Hq, Hkv, D, P, T = 32, 8, 128, 768, 200
