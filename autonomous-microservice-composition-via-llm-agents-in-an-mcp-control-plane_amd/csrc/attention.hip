@@ -806,14 +806,23 @@ int* split_counters() {
   return g_split_cnt[d & 63];
 }
 
-int prefix_nw() {
-  static int nw = 0;
-  if (!nw) {
+// waves per block of the shared-prefix pass: MCP_ATTN_PREFIX_NW = 4 / 8
+// forces one; by default 4-wave blocks (half the tokens per block) when the
+// 8-wave grid would not give every CU a block.  tools/bench_attention.py,
+// 704-key prefix, 16 new tokens per request (prefix pass us, 8 / 4 waves):
+// 8 requests 31.0 / 23.5, 36 32.6 / 25.3, 64 34.4 / 27.1, 128 39.0 / 41.6,
+// 256 78.1 / 76.3; 8 tokens each: 36 31.6 / 24.0, 128 33.9 / 27.1
+// (profiles/attention_tuning.md, round 3)
+int prefix_nw(int tokens, int tok_per_block8, int hkv) {
+  static int forced = -1;
+  if (forced < 0) {
     const char* e = getenv("MCP_ATTN_PREFIX_NW");
-    nw = e ? atoi(e) : 8;
-    if (nw != 4 && nw != 8) nw = 8;
+    forced = e ? atoi(e) : 0;
+    if (forced != 4 && forced != 8) forced = 0;
   }
-  return nw;
+  if (forced) return forced;
+  const long long blocks8 = (long long)((tokens + tok_per_block8 - 1) / tok_per_block8) * hkv;
+  return blocks8 < gemm256_num_cus() ? 4 : 8;
 }
 
 // Shared-prefix pass: 8 waves per block (32 tokens x G heads) -> half the K/V
@@ -843,13 +852,13 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
     };
     if (rt == 4)
       attn_prefix_kernel<4, G, 4><<<grid_for(4 * 4 * (16 / G)), 256, 0, s>>>(a);
-    else if (prefix_nw() == 4)
+    else if (prefix_nw(a.pre_tokens, 8 * 2 * (16 / G), a.Hkv) == 4)
       attn_prefix_kernel<4, G, 2><<<grid_for(4 * 2 * (16 / G)), 256, 0, s>>>(a);
     else
       attn_prefix_kernel<8, G, 2><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     return;
   }
-  if (prefix_nw() == 4) {
+  if (prefix_nw(a.pre_tokens, 8 * (16 / G), a.Hkv) == 4) {
     constexpr int QT = 4 * (16 / G);
     const int nblk = (a.pre_tokens + QT - 1) / QT;
     const dim3 grid = a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
