@@ -50,6 +50,12 @@ class AttnMeta:
 
 
 _XCD_ORDER = os.environ.get("MCP_ATTN_XCD_ORDER", "1") == "1"
+# fewest own key tiles (of the longest sequence) for a split-KV step.  4
+# (was 8): serving steps of a few requests with 4-7 own key tiles each split
+# too - config 5 at 40 intents/s p50 172-178 -> 147-150 ms, 80/s 213-221 ->
+# 202-213 ms, 20/s 123 -> 119-121 ms (same box; 2 measured equal to 4,
+# profiles/attention_splitkv_min_tiles_ab.jsonl).  MCP_KV_SPLIT_MIN_TILES overrides
+_SPLIT_MIN_TILES = int(os.environ.get("MCP_KV_SPLIT_MIN_TILES", "4"))
 N_SIZES = 19            # packed segments of pack_host (the layout's leading entries)
 
 
@@ -82,7 +88,7 @@ def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
     if forced > 1:
         return forced
     work = items * hkv
-    if work >= num_cus or tiles < 8:
+    if work >= num_cus or tiles < _SPLIT_MIN_TILES:
         return 1
     # ~2 workgroups per CU (measured best at batch 1 / 4 and 8k-128k contexts,
     # profiles/attention_splitkv.jsonl); >= 4 key tiles per split there, >= 2

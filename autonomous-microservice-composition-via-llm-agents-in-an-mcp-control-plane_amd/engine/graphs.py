@@ -262,7 +262,8 @@ class GraphRunner:
     # such steps; any other split key runs eagerly (no lazy capture on the
     # request path)
     WARM_SPLITS = (2, 4, 8)
-    WARM_SPLIT_MAX_TOKENS = 64
+    WARM_SPLIT_MAX_TOKENS = int(os.environ.get("MCP_WARM_SPLIT_MAX_TOKENS", "64"))
+    WARM_SPLIT_SEQ_CLASSES = int(os.environ.get("MCP_WARM_SPLIT_SEQ_CLASSES", "1"))
 
     def warm(self, max_tokens: Optional[int] = None, contexts: Sequence[int] = (2048,),
              kv_splits: Sequence[int] = (1,)) -> int:
@@ -290,13 +291,13 @@ class GraphRunner:
                         for casc in (0, 1):
                             cap((b, sb, w, int(ns), casc), b, w, sb)
             if b <= self.WARM_SPLIT_MAX_TOKENS and self.device.type == "cuda":
-                sb = self.seq_classes(b)[0]
-                for w in widths:
-                    for ns in self.WARM_SPLITS:
-                        if ns in kv_splits:
-                            continue
-                        for casc in (0, 1):
-                            cap((b, sb, w, int(ns), casc), b, w, sb)
+                for sb in self.seq_classes(b)[:self.WARM_SPLIT_SEQ_CLASSES]:
+                    for w in widths:
+                        for ns in self.WARM_SPLITS:
+                            if ns in kv_splits:
+                                continue
+                            for casc in (0, 1):
+                                cap((b, sb, w, int(ns), casc), b, w, sb)
         self.warmed = True
         return self.captures - n0
 

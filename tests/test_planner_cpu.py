@@ -353,7 +353,8 @@ def test_kv_split_rule():
     assert choose_kv_splits([1], [32768], 4, 8) == 64          # batch-1 decode, 32k keys
     assert choose_kv_splits([1] * 4, [32768] * 4, 4, 8) == 16
     assert choose_kv_splits([1], [700], 4, 8) == 4               # single intent: 11 tiles / 2 -> 5 -> power of two
-    assert choose_kv_splits([1], [400], 4, 8) == 1               # < 8 tiles: unsplit
+    assert choose_kv_splits([1], [400], 4, 8) == 2               # 7 tiles: 2 splits (serving-size steps)
+    assert choose_kv_splits([1], [150], 4, 8) == 1               # < 4 tiles: unsplit
     assert choose_kv_splits([1] * 64, [8192] * 64, 4, 8) == 1    # 512 items already fill it
     assert choose_kv_splits([300], [32768], 4, 8) == 4           # 19 4-wave items: underfilled
     assert choose_kv_splits([3000], [32768], 4, 8) == 1          # a big prefill fills the chip
