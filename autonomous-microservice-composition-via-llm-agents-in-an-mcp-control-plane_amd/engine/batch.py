@@ -56,6 +56,10 @@ _XCD_ORDER = os.environ.get("MCP_ATTN_XCD_ORDER", "1") == "1"
 # 202-213 ms, 20/s 123 -> 119-121 ms (same box; 2 measured equal to 4,
 # profiles/attention_splitkv_min_tiles_ab.jsonl).  MCP_KV_SPLIT_MIN_TILES overrides
 _SPLIT_MIN_TILES = int(os.environ.get("MCP_KV_SPLIT_MIN_TILES", "4"))
+# split only while the step has fewer than this many x num_cus work items:
+# 2 (was 1) - config 5 at 80 intents/s p50 195-196 -> 188-190 ms, p99 244 ->
+# 230, 120/s 321-333 -> 316-321 (profiles/attention_splitkv_min_tiles_ab.jsonl)
+_SPLIT_WORK_FACTOR = float(os.environ.get("MCP_KV_SPLIT_WORK_FACTOR", "2"))
 N_SIZES = 19            # packed segments of pack_host (the layout's leading entries)
 
 
@@ -88,7 +92,7 @@ def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
     if forced > 1:
         return forced
     work = items * hkv
-    if work >= num_cus or tiles < _SPLIT_MIN_TILES:
+    if work >= _SPLIT_WORK_FACTOR * num_cus or tiles < _SPLIT_MIN_TILES:
         return 1
     # ~2 workgroups per CU (measured best at batch 1 / 4 and 8k-128k contexts,
     # profiles/attention_splitkv.jsonl); >= 4 key tiles per split there, >= 2

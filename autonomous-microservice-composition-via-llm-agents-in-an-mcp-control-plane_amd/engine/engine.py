@@ -36,6 +36,14 @@ from ..utils.tracing import span
 from .batch import BLOCK_SIZE, HostStager, choose_kv_splits, pack_step, step_from_host, views
 from .kv_cache import KVCache
 
+# steps above this many tokens run eagerly even when a graph bucket fits.  At
+# serving loads the bigger steps (tens of requests) ran slower replayed than
+# eager - the padded token bucket, work lists and block table of the graph key
+# cost more than the launches they save: config 5 at 120 intents/s p50 328 ->
+# 304 ms, 20/s 124 -> 122, 80/s 188 -> 187, config 2 96.4 -> 95.8 with 128
+# (profiles/graph_max_tokens_ab.jsonl).  MCP_GRAPH_MAX_TOKENS overrides
+_GRAPH_MAX_T = int(os.environ.get("MCP_GRAPH_MAX_TOKENS", "128"))
+
 _uid = itertools.count(1)
 
 
@@ -586,7 +594,7 @@ class LLMEngine:
             ctr = [(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF for q in sample_seqs]
         # a step that fits a captured bucket replays its hipGraph (prefix
         # copy-on-write, cascade and split-KV attention included)
-        use_graph = (self.graphs is not None and T <= self.graphs.buckets[-1]
+        use_graph = (self.graphs is not None and T <= self.graphs.buckets[-1] and T <= _GRAPH_MAX_T
                      and self.temperature == self.graphs.temperature)
         cascade = pre_tokens > 0
         # split-KV for few long-context decode sequences (K6), over the keys
@@ -727,6 +735,7 @@ class LLMEngine:
         0 when graphs are off."""
         if self.graphs is None:
             return 0
+        max_tokens = _GRAPH_MAX_T if max_tokens is None else min(max_tokens, _GRAPH_MAX_T)
         return self.graphs.warm(max_tokens, contexts)
 
     # -------------------------------------------------------------- driver

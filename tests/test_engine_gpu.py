@@ -14,6 +14,17 @@ from mcp_amd.registry import MemoryRegistry, synthetic_registry
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _graph_every_bucket(monkeypatch):
+    """These tests check the graph machinery on every bucket (copy-on-write,
+    cascade and split-KV keys included): lift the serving default that runs
+    steps above 128 tokens eagerly (engine._GRAPH_MAX_T); spawned ranks read
+    the environment."""
+    import mcp_amd.engine.engine as eng_mod
+    monkeypatch.setenv("MCP_GRAPH_MAX_TOKENS", "1000000")
+    monkeypatch.setattr(eng_mod, "_GRAPH_MAX_T", 1000000)
+
+
 def _plans(model, reg, intents, **kw):
     eng = LLMEngine(model, num_blocks=512, max_batch=32, temperature=0.0, **kw)
     planner = LocalPlanner(eng, reg, max_nodes=4, min_nodes=2)

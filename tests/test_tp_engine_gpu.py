@@ -18,6 +18,17 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _graph_every_bucket(monkeypatch):
+    """These tests check the graph machinery on every bucket (copy-on-write,
+    cascade and split-KV keys included): lift the serving default that runs
+    steps above 128 tokens eagerly (engine._GRAPH_MAX_T); spawned ranks read
+    the environment."""
+    import mcp_amd.engine.engine as eng_mod
+    monkeypatch.setenv("MCP_GRAPH_MAX_TOKENS", "1000000")
+    monkeypatch.setattr(eng_mod, "_GRAPH_MAX_T", 1000000)
+
+
 @pytest.mark.timeout(600)
 def test_tp2_two_processes_one_gpu_matches_tp1(monkeypatch):
     if not torch.cuda.is_available():
