@@ -170,6 +170,7 @@ class LLMEngine:
         self.seed = seed
         self.running: List[Sequence] = []
         self.waiting: List[Sequence] = []
+        self._deferred_free: List[int] = []              # released after the step's copies are queued
         self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
         self._last_prefix = None                         # (token list object, entry)
         self.max_prefixes = 64
@@ -220,12 +221,26 @@ class LLMEngine:
 
     def _evict_prefixes(self, need: int) -> bool:
         """Drop cached prefix entries, least recently used first, until
-        ``need`` blocks are free (requests still using a prefix keep its
-        blocks alive).  Returns whether they are."""
+        ``need`` blocks are free.  Entries no request uses go first (every
+        block returns to the pool); then entries that free at least one block
+        (a prefix whose full blocks running requests still share gives back
+        its tail); an entry whose blocks are all still shared frees nothing
+        and stays cached - dropping it would only make later requests
+        recompute a hot prefix.  Returns whether ``need`` blocks are free."""
         a = self.alloc
-        while a.num_free < need and self.prefixes:
-            old = next(iter(self.prefixes))
-            a.free(self.prefixes.pop(old).blocks)
+        if a.num_free >= need:
+            return True
+        for only_unused in (True, False):
+            for key in list(self.prefixes):
+                if a.num_free >= need:
+                    return True
+                blocks = self.prefixes[key].blocks
+                held = sum(1 for b in blocks if a.refcount(b) == 1)
+                if held == 0 or (only_unused and held < len(blocks)):
+                    continue
+                if self._last_prefix is not None and self._last_prefix[1] is self.prefixes[key]:
+                    self._last_prefix = None
+                a.free(self.prefixes.pop(key).blocks)
         return a.num_free >= need
 
     def _alloc_pressure(self, need: int, protect: set) -> Optional[List[int]]:
@@ -237,7 +252,7 @@ class LLMEngine:
             busy = set(protect)
             for L in self.inflight.values():
                 busy.update(id(q) for q, _ in L.batch_seqs)
-            for seq in reversed(self.running):
+            for seq in list(reversed(self.running)):    # _preempt edits running
                 if self.alloc.num_free >= need:
                     break
                 if seq.is_prefix_job or seq.evicted or not seq.blocks or id(seq) in busy:
@@ -255,6 +270,8 @@ class LLMEngine:
         counter carry on."""
         keep = seq.base // BLOCK_SIZE
         head = list(seq.prefix.tokens[keep * BLOCK_SIZE:seq.base]) if seq.base % BLOCK_SIZE else []
+        if keep and seq.prefix is not None:
+            seq.kept_prefix = seq.prefix       # its first ``keep`` blocks stay shared
         self.alloc.free(seq.blocks[keep:])
         del seq.blocks[keep:]
         seq.pending = head + seq.tokens
@@ -265,6 +282,42 @@ class LLMEngine:
         self.running.remove(seq)
         self.waiting.insert(0, seq)
         self.stats["preemptions"] += 1
+
+    def _release_idle(self, need: int, skip) -> None:
+        """Last resort before failing a request for memory: requests that are
+        not in this step hold shared-prefix blocks too - preempted ones keep
+        their prefix's full blocks, not-yet-materialised ones a reference to
+        their whole prefix.  Fully release them (most recently queued first)
+        until ``need`` blocks are free; each then carries its whole prompt as
+        pending tokens."""
+        a = self.alloc
+        for seq in list(reversed(self.waiting)) + list(reversed(self.running)):
+            if a.num_free >= need:
+                return
+            if seq is skip or seq.is_prefix_job or seq.done:
+                continue
+            if not seq.materialized:
+                e = seq.prefix
+                a.free(e.blocks)
+                seq.pending = list(e.tokens) + seq.pending
+                seq.tokens = list(e.tokens) + seq.tokens
+                seq.prefix, seq.materialized = None, True
+            elif seq.evicted or seq in self.waiting:
+                if not seq.blocks:
+                    continue
+                kept = getattr(seq, "kept_prefix", None)
+                if kept is None or seq.num_cached != seq.base:
+                    continue                   # holds KV of its own: not a prefix-only holder
+                a.free(seq.blocks)
+                seq.blocks = []
+                head = list(kept.tokens[:seq.base])
+                seq.pending = head + seq.pending
+                seq.tokens = head + seq.tokens
+                seq.base = seq.num_cached = 0
+                seq.kept_prefix = None
+            else:
+                continue
+            self.stats["released"] = self.stats.get("released", 0) + 1
 
     def _blocks_to_admit(self, seq: Sequence) -> int:
         """Blocks a waiting request needs for the tokens it already has."""
@@ -295,7 +348,13 @@ class LLMEngine:
         if tail:
             copies.append((e.blocks[-1], nb))
             seq.blocks.append(nb)
-            self.alloc.free([e.blocks[-1]])    # the reference taken at submit
+            # the reference taken at submit is released only after this
+            # step's copies are queued: freed now (an already evicted prefix
+            # drops the block's last reference), the LIFO pool could hand the
+            # block to another request's tail copy in the same step - copy
+            # pairs (t_a -> n_a), (t_b -> t_a) run in parallel and a's tail
+            # would take b's KV
+            self._deferred_free.append(e.blocks[-1])
         seq.num_cached = seq.base = e.length
         seq.materialized = True
         return True
@@ -490,15 +549,25 @@ class LLMEngine:
         return False
 
     def _schedule_launch(self, cohort: Optional[int]) -> Optional[_Launch]:
+        try:
+            return self._schedule_launch_inner(cohort)
+        finally:
+            if self._deferred_free:            # this step's copy list is queued on the stream
+                self.alloc.free(self._deferred_free)
+                self._deferred_free = []
+
+    def _schedule_launch_inner(self, cohort: Optional[int]) -> Optional[_Launch]:
         t_sched = time.perf_counter()
         self._admit()
         if not self.running:
             return None
         pool = self.running if cohort is None else [q for q in self.running if q.cohort == cohort]
         copies = []
+        unplaced = None                       # a computed-prefix request the pool could not take
         for seq in pool:
             if not seq.materialized and seq.prefix.computed:
-                self._materialize(seq, copies)
+                if not self._materialize(seq, copies):
+                    unplaced = unplaced or seq
         if any(q.evicted for q in pool):     # preempted while materialising
             pool = [q for q in pool if not q.evicted]
         budget = self.max_step_tokens
@@ -525,7 +594,7 @@ class LLMEngine:
                 # 113 ms, profiles/config2_attention_ab.jsonl)
                 if (casc.length >= 16 * BLOCK_SIZE and n_share < 16) or n_share < self.CASCADE_MIN_SHARERS:
                     casc = None
-        order = pool
+        order = list(pool)                     # _alloc_pressure may preempt (edit running)
         if casc is not None:
             first, rest = [], []
             for q in pool:
@@ -578,14 +647,28 @@ class LLMEngine:
         if T == 0:
             if copies:     # copy-on-write blocks still have to land before later steps
                 self._launch(*pack_step([], BLOCK_SIZE, group, copies))
+            if unplaced is not None and blocked is None and not self.inflight:
+                # its tail block is held by idle requests' prefixes: release them
+                self._release_idle(1, unplaced)
+                self._evict_prefixes(1)
             if blocked is not None and not self.inflight:
-                # nothing else holds blocks that could be reclaimed: the
-                # request does not fit the pool at all
-                blocked.error = (f"KV cache exhausted: the request needs "
-                                 f"{self._blocks_to_admit(blocked) + len(blocked.blocks)} blocks, "
-                                 f"the pool has {self.kv.num_blocks}")
-                self._finish(blocked)
-                self.running = [q for q in self.running if not q.done]
+                own = (blocked.num_cached + len(blocked.pending) + BLOCK_SIZE - 1) // BLOCK_SIZE
+                if own > self.kv.num_blocks:
+                    # the request alone does not fit the whole pool
+                    blocked.error = (f"KV cache exhausted: the request needs {own} blocks, "
+                                     f"the pool has {self.kv.num_blocks}")
+                    self._finish(blocked)
+                    self.running = [q for q in self.running if not q.done]
+                else:
+                    # it fits once the blocks idle requests hold are released
+                    # (the next step schedules it)
+                    want = own - len(blocked.blocks)
+                    self._release_idle(want, blocked)
+                    if not self._evict_prefixes(want):
+                        blocked.error = (f"KV cache exhausted: the request needs {own} blocks, "
+                                         f"{self.alloc.num_free} of {self.kv.num_blocks} can be freed")
+                        self._finish(blocked)
+                        self.running = [q for q in self.running if not q.done]
             return None
         allowed = ctr = None
         if sample_seqs:            # grammar masks go in the same single H2D copy
@@ -740,12 +823,22 @@ class LLMEngine:
 
     # -------------------------------------------------------------- driver
     def run(self, max_steps: int = 1_000_000):
-        n = 0
+        n = idle = 0
         while self.has_work() and n < max_steps:
-            if self.step() == 0 and not self.waiting and not self.inflight:
-                # nothing runnable: sequences blocked on nothing -> bug guard
-                stuck = [s for s in self.running if not s.pending]
-                if stuck:
-                    raise RuntimeError("engine stalled with sequences that have no pending tokens")
+            if self.step() == 0 and not self.inflight:
+                if not self.waiting:
+                    # nothing runnable: sequences blocked on nothing -> bug guard
+                    stuck = [s for s in self.running if not s.pending]
+                    if stuck:
+                        raise RuntimeError("engine stalled with sequences that have no pending tokens")
+                # a step without progress may release blocks for the next one;
+                # several in a row with nothing in flight can never progress
+                idle += 1
+                if idle > 8:
+                    raise RuntimeError(f"engine stalled: {len(self.running)} running and "
+                                       f"{len(self.waiting)} waiting requests cannot be scheduled "
+                                       f"({self.alloc.num_free} of {self.kv.num_blocks} KV blocks free)")
+            else:
+                idle = 0
             n += 1
         return n

@@ -46,7 +46,7 @@ def deinterleave_gate_up(w: torch.Tensor):
     return v[:, 0].reshape(F2 // 2, H), v[:, 1].reshape(F2 // 2, H)
 
 
-SS_FIX = float(1 << 28)         # fixed-point unit of the fused-norm row statistics (csrc/common.h)
+SS_FIX = float(1 << 20)         # fixed-point unit of the fused-norm row statistics (csrc/common.h)
 
 
 def row_sumsq(x: torch.Tensor) -> torch.Tensor:

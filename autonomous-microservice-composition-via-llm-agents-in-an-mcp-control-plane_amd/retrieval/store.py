@@ -106,8 +106,18 @@ class SchemaIndex:
         self._rows: Dict[str, Tuple[int, int]] = {}
         self._shadow_names: List[str] = []
         self._seen: Dict[str, object] = {}               # name -> the record object indexed
-        self._lock = threading.Lock()                   # pending updates / shadow
+        # two locks: ``_diff_lock`` serialises the shadow diffs and their
+        # embedding (refresher thread or a synchronous catch-up), ``_lock``
+        # only guards the hand-over of finished updates - the engine thread's
+        # ``sync`` never waits behind an embedding
+        self._lock = threading.Lock()
+        self._diff_lock = threading.Lock()
+        self._shadow_version = None                     # registry version the shadow reflects
         self._pending: List[_Update] = []
+        # a search that finds the registry ahead of the index by at most this
+        # many changed records diffs them itself (a service registered just
+        # before a /plan is visible to it); larger backlogs stay on the refresher
+        self.sync_max_changes = 64
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self.stats = {"embedded": 0, "applied": 0, "full_builds": 0}
@@ -124,7 +134,7 @@ class SchemaIndex:
             v = torch.cat([v, v.new_zeros(4 - n % 4, v.shape[1])])
         v = v.contiguous()
         ops.l2norm_rows(v)
-        with self._lock:
+        with self._diff_lock, self._lock:
             self._pending.clear()
             self.names, self.vectors, self.n = list(names), v, n
             self._shadow_names = list(names)
@@ -135,7 +145,7 @@ class SchemaIndex:
     def _diff(self, services: Sequence[dict], version) -> Optional[_Update]:
         """CPU side of a refresh (any thread): embed the new / changed records,
         swap-remove the vanished ones; the shadow state moves to the result.
-        Caller holds ``self._lock``."""
+        Caller holds ``self._diff_lock``."""
         want = {}
         for s in services:
             want[s["name"]] = s
@@ -185,7 +195,7 @@ class SchemaIndex:
     def _diff_changes(self, changed: Sequence[str], version) -> Optional[_Update]:
         """O(changes) diff from a registry change log (``changes_since``):
         the named records are re-read (``registry.get``) and upserted, or
-        swap-removed when gone.  Caller holds ``self._lock``."""
+        swap-removed when gone.  Caller holds ``self._diff_lock``."""
         rows, names = self._rows, self._shadow_names
         writes: Dict[int, str] = {}
         recs: Dict[str, object] = {}
@@ -256,11 +266,13 @@ class SchemaIndex:
             if self.vectors is not None and ver == self._version and not self._pending:
                 return
             services = self.registry.list_services()
-        with self._lock:
+        with self._diff_lock:
             if self.vectors is None:
                 self.stats["full_builds"] += 1
             u = self._diff(services, ver)
-            pend, self._pending = self._pending, []
+            self._shadow_version = ver
+            with self._lock:
+                pend, self._pending = self._pending, []
         for p in pend:
             self._apply(p)
         if u is not None:
@@ -279,34 +291,49 @@ class SchemaIndex:
             self._apply(p)
         return len(pend)
 
+    def _catch_up(self, max_changes: Optional[int] = None) -> bool:
+        """Bring the shadow up to the registry's current version (diff + embed
+        under ``_diff_lock``, then queue the update).  With ``max_changes``
+        only a change-log backlog of at most that many records is taken;
+        returns whether the shadow is now current."""
+        ver = getattr(self.registry, "version", None)
+        if ver is None or ver == self._shadow_version:
+            return True
+        with self._diff_lock:
+            seen = self._shadow_version
+            ver = getattr(self.registry, "version", None)
+            if ver == seen:
+                return True
+            # a registry with a change log: O(changes); else a full diff
+            ch = self.registry.changes_since(seen) \
+                if seen is not None and hasattr(self.registry, "changes_since") else None
+            if ch is not None:
+                if max_changes is not None and len(ch[1]) > max_changes:
+                    return False
+                ver, names = ch
+                u = self._diff_changes(names, ver)
+            elif max_changes is not None:
+                return False
+            else:
+                u = self._diff(self.registry.list_services(), ver)
+            self._shadow_version = ver
+            if u is not None:
+                with self._lock:
+                    self._pending.append(u)
+        return True
+
     def start_background(self, poll_s: float = 0.05) -> None:
         """Refresher thread: watches ``registry.version`` and prepares the
         incremental updates off the engine thread (``sync`` applies them)."""
         if self._thread is not None or self.registry is None:
             return
+        if self._shadow_version is None:
+            self._shadow_version = self._version
 
         def loop():
-            seen = self._version
             while not self._stop.wait(poll_s):
                 try:
-                    ver = getattr(self.registry, "version", None)
-                    if ver == seen:
-                        continue
-                    # a registry with a change log: O(changes); else a full diff
-                    ch = self.registry.changes_since(seen) \
-                        if seen is not None and hasattr(self.registry, "changes_since") else None
-                    if ch is not None:
-                        ver, names = ch
-                        with self._lock:
-                            u = self._diff_changes(names, ver)
-                            self._pending.append(u)
-                    else:
-                        services = self.registry.list_services()
-                        with self._lock:
-                            u = self._diff(services, ver)
-                            if u is not None:
-                                self._pending.append(u)
-                    seen = ver
+                    self._catch_up()
                 except Exception:      # noqa: BLE001 - a registry hiccup: retry next poll
                     time.sleep(poll_s)
 
@@ -333,7 +360,11 @@ class SchemaIndex:
 
     def search(self, intent: str, k: int, services: Sequence[dict]) -> List[dict]:
         if self._thread is not None and self.vectors is not None:
-            self.sync()                                 # background mode: never re-embed here
+            # background mode: a short change-log backlog (a registration
+            # just before this request) is diffed here so the request sees
+            # it; a large one stays on the refresher thread
+            self._catch_up(self.sync_max_changes)
+            self.sync()
         elif self.vectors is None or getattr(self.registry, "version", None) != self._version \
                 or self.n != len(services):
             self.refresh(services)

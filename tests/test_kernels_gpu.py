@@ -816,6 +816,31 @@ def test_fused_norm_residual_statistic(M, N, K):
         assert rel_err(y, ref.gemm(X, W, R)) < 1e-2
 
 
+@pytest.mark.parametrize("M", [3, 300, 2600])
+def test_fused_norm_statistic_large_rows(M):
+    """rows of |x| ~ 3e3 at H = 8192 (70B width).  At the old
+    2^-28 unit such a row's sum of squares overflowed int64 and wrapped; the
+    2^-20 unit with a clamped add keeps it exact to 1e-5 and positive, both in
+    the residual GEMM epilogue and in the stand-alone norm kernel."""
+    torch.manual_seed(23)
+    N, K = 8192, 1024
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    R = (torch.randn(M, N, device=DEV) * 3e3).bfloat16()
+    y = R.clone()
+    ss = torch.zeros(M, dtype=torch.int64, device=DEV)
+    ops.gemm(X, W, R=y, out=y, ss_out=ss)
+    exp = y.double().pow(2).sum(-1) * ref.SS_FIX
+    assert (ss > 0).all()
+    assert ((ss.double() - exp).abs() / exp).max().item() < 1e-5
+    ss2 = torch.zeros(M, dtype=torch.int64, device=DEV)
+    ops.row_sumsq(y, ss2)
+    assert (ss2 > 0).all() and ((ss2.double() - exp).abs() / exp).max().item() < 1e-5
+    sc = ref.norm_row_scale(ss.cpu(), N, 1e-5)
+    exp_sc = torch.rsqrt(y.cpu().double().pow(2).mean(-1) + 1e-5).float().unsqueeze(-1)
+    assert torch.allclose(sc, exp_sc, rtol=1e-5)
+
+
 @pytest.mark.parametrize("M", [1, 6, 20, 48, 200, 700, 2600])
 def test_fused_norm_swiglu_and_qkv(M):
     """SwiGLU and QKV + RoPE with ``ss_in``: the accumulators of row m scaled

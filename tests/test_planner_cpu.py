@@ -487,3 +487,89 @@ def test_preemption_by_recompute_under_a_small_kv_pool():
     err, eng = run(9)
     assert isinstance(err, RuntimeError) and "KV cache exhausted" in str(err)
     assert eng.alloc.num_free == 9 and not eng.running and not eng.waiting
+
+
+def _distinct_prefix_requests(eng, n):
+    """n requests whose registry prefixes differ (own registries), each prefix
+    longer than one block with a partial tail."""
+    out = []
+    for i in range(n):
+        reg = MemoryRegistry(synthetic_registry(4 + i, seed=20 + i))
+        pl = LocalPlanner(eng, reg, max_nodes=2)
+        dec, ptoks, stoks = pl.prepare(synthetic_intent(300 + i))
+        assert len(ptoks) > 64 and len(ptoks) % 64
+        out.append((dec, ptoks, stoks))
+    return out
+
+
+def test_tail_copies_never_alias_when_evicted_prefixes_materialise_together():
+    """two requests whose cached prefixes were evicted before
+    they materialise in the same step.  Freeing a tail source right away let
+    the LIFO pool hand it to the next request's tail copy, so the step's copy
+    list held (t_a -> n_a) and (t_b -> t_a), which run in parallel on the GPU.
+    No block may be both a source and a destination in one step, and the
+    plans must equal those of an engine that never evicted."""
+    import mcp_amd.engine.engine as engmod
+    results = []
+    for evict in (False, True):
+        eng = LLMEngine(LlamaModel.random("tiny", "cpu", seed=1), num_blocks=128, max_batch=8,
+                        temperature=0.0, graphs=False)
+        reqs = _distinct_prefix_requests(eng, 3)
+        seqs = [eng.submit(d, s, prefix_tokens=p) for d, p, s in reqs]
+        pairs = []
+        real = engmod.ops.copy_blocks
+
+        def spy(kv, src, dst):
+            pairs.append((src.tolist(), dst.tolist()))
+            return real(kv, src, dst)
+        engmod.ops.copy_blocks = spy
+        try:
+            while any(not e.computed for e in eng.prefixes.values()):
+                eng.step()
+            if evict:
+                eng.drop_prefixes()                # entries gone: requests hold the last refs
+            eng.run()
+        finally:
+            engmod.ops.copy_blocks = real
+        assert pairs, "the tail blocks were never copied"
+        for src, dst in pairs:
+            assert not set(src) & set(dst), (src, dst)
+            assert len(set(dst)) == len(dst)
+        assert all(q.error is None for q in seqs)
+        eng.drop_prefixes()
+        assert eng.alloc.num_free == eng.kv.num_blocks
+        results.append([q.result for q in seqs])
+    assert results[0] == results[1]
+
+
+def test_evict_prefixes_keeps_entries_that_free_nothing():
+    """an entry whose blocks running requests still share
+    frees nothing; evicting it would only make later requests recompute it."""
+    eng = LLMEngine(LlamaModel.random("tiny", "cpu", seed=1), num_blocks=64, max_batch=8,
+                    temperature=0.0, graphs=False)
+    (d, p, s), = _distinct_prefix_requests(eng, 1)
+    q = eng.submit(d, s, prefix_tokens=p)
+    e = eng.prefixes[tuple(p)]
+    assert not eng._evict_prefixes(eng.alloc.num_free + 1)   # job + request hold every block
+    assert tuple(p) in eng.prefixes
+    eng.run()
+    assert q.error is None and tuple(p) in eng.prefixes and e.computed
+    assert eng._evict_prefixes(eng.alloc.num_free + 1)       # unused now: its blocks come back
+    assert tuple(p) not in eng.prefixes and eng.alloc.num_free == eng.kv.num_blocks
+
+
+def test_pool_pressure_releases_idle_prefix_holders_instead_of_failing():
+    """a request that fits the pool on its own must not fail
+    with 'KV cache exhausted' because waiting requests hold references to
+    their (distinct) prefixes; those are released and recomputed later."""
+    eng = LLMEngine(LlamaModel.random("tiny", "cpu", seed=1), num_blocks=40, max_batch=1,
+                    temperature=0.0, graphs=False)
+    reqs = _distinct_prefix_requests(eng, 6)
+    need = max((len(p) + len(s)) // 64 + 4 for _, p, s in reqs)
+    assert sum(len(p) // 64 + 1 for _, p, _ in reqs) + need > eng.kv.num_blocks
+    seqs = [eng.submit(d, s, prefix_tokens=p) for d, p, s in reqs]
+    eng.run()
+    assert all(q.done and q.error is None for q in seqs), [q.error for q in seqs]
+    assert eng.stats.get("released", 0) > 0
+    eng.drop_prefixes()
+    assert eng.alloc.num_free == eng.kv.num_blocks

@@ -145,3 +145,24 @@ def test_background_refresh_never_stalls_engine_loop():
     assert float(np.median(retr)) < max(0.020, full_s / 5), (float(np.median(retr)), full_s)
     assert idx.n == 10_100 and "late-99" in idx.names
     assert idx.stats["full_builds"] == 1 and idx.stats["applied"] >= 2
+
+
+def test_background_index_sees_a_registration_made_just_before_the_search():
+    """in background mode a service registered right before
+    a /plan call must be retrievable by that call, not one poll interval
+    later; large backlogs stay on the refresher thread."""
+    reg = MemoryRegistry(synthetic_registry(300, seed=4))
+    idx = SchemaIndex(reg, dim=256)
+    idx.refresh()
+    idx.start_background(poll_s=60.0)              # the refresher never runs in this test
+    try:
+        reg.register(make_service("zebra-quota-ledger", {"zebra_quota": "number"}, {"ok": "string"}))
+        got = idx.search("zebra quota ledger", 3, reg.list_services())
+        assert got and got[0]["name"] == "zebra-quota-ledger"
+        for i in range(idx.sync_max_changes + 1):  # a backlog over the limit is not diffed inline
+            reg.register(make_service(f"bulk-{i}", {"x": "string"}, {"y": "string"}))
+        idx.search("bulk", 3, reg.list_services())
+        assert "bulk-0" not in idx.names
+        assert idx._catch_up() and idx.sync() == 1 and "bulk-0" in idx.names
+    finally:
+        idx.stop_background()
