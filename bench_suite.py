@@ -21,11 +21,70 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-REF_PLAN_MS = {3: 1.42, 10: 1.53, 50: 1.81, 1000: 8.79}          # SURVEY §6 (reference plumbing)
+REF_PLAN_MS = {3: 1.42, 10: 1.53, 50: 1.81, 1000: 8.79}          # SURVEY §6 (another host)
 REF_EXEC_MS = {3: 1.89, 10: 3.16, 50: 10.08}
 
 
-def plumbing(runs: int = 30):
+def load_reference(path: str = "/root/reference/control_plane.py", canned=None):
+    """The reference app on THIS host for same-host comparisons:
+    a scratch copy of ``control_plane.py`` in a temp dir with only its
+    escaped-docstring SyntaxError fixed (D1), imported against stub ``redis`` /
+    ``psycopg2`` / ``pgvector`` / ``openai`` modules (an instant LLM returning
+    ``canned``).  Nothing of the reference is stored in this repo; returns the
+    module (``.app``, ``.orch``) or None when the file is absent."""
+    import importlib.util
+    import tempfile
+    import types
+    if not os.path.exists(path):
+        return None
+    src = open(path, encoding="utf-8").read().replace('\\"\\"\\"', '"""')
+    store = {}
+
+    class _Redis:
+        def scan_iter(self, pattern):
+            pre = pattern.rstrip("*")
+            return [k for k in list(store) if k.startswith(pre)]
+
+        def get(self, k):
+            return store.get(k)
+
+    reply = json.dumps(canned or {"nodes": [], "edges": []})
+
+    class _Completion:
+        @staticmethod
+        def create(**kw):
+            msg = types.SimpleNamespace(content=reply)
+            return types.SimpleNamespace(choices=[types.SimpleNamespace(message=msg)])
+    stubs = {"redis": types.SimpleNamespace(from_url=lambda url: _Redis()),
+             "psycopg2": types.SimpleNamespace(connect=lambda dsn: object()),
+             "pgvector": types.ModuleType("pgvector"),
+             "pgvector.psycopg2": types.SimpleNamespace(register_vector=lambda conn: None),
+             "openai": types.SimpleNamespace(ChatCompletion=_Completion, api_key=None)}
+    saved = {k: sys.modules.get(k) for k in stubs}
+    sys.modules.update(stubs)
+    try:
+        d = tempfile.mkdtemp(prefix="refcp_")
+        f = os.path.join(d, "control_plane_scratch.py")
+        with open(f, "w", encoding="utf-8") as fh:
+            fh.write(src)
+        spec = importlib.util.spec_from_file_location("control_plane_scratch", f)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    mod._store = store
+    return mod
+
+
+def plumbing(runs: int = 30, rounds: int = 3, out=None):
+    """Config 1 on this host: ours and the reference (``load_reference``)
+    alternate ``rounds`` times per case, ``runs`` requests each; the p50 of
+    every round is reported, and the speedup from the medians of the rounds."""
+    import asyncio
     import httpx
     from fastapi.testclient import TestClient
     from mcp_amd.api.server import create_app
@@ -36,22 +95,59 @@ def plumbing(runs: int = 30):
     def handler(request):
         return httpx.Response(200, json={"ok": True})
     canned = {"nodes": [{"name": "a", "endpoint": "http://a/api", "inputs": {"x": "uid"}}], "edges": []}
+    ref = load_reference(canned=canned)
+
+    def time_posts(c, route, body_fn, k):
+        for i in range(5):
+            c.post(route, json=body_fn(i))
+        ts = []
+        for i in range(k):
+            t = time.perf_counter()
+            r = c.post(route, json=body_fn(i))
+            ts.append(time.perf_counter() - t)
+            assert r.status_code == 200, r.text
+        return statistics.median(ts) * 1e3
+
+    def emit(rec):
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if out:
+            with open(out, "a") as fh:
+                fh.write(line + "\n")
+
+    def ref_client(mod, services):
+        mod._store.clear()
+        for s in services:
+            mod._store["mcp:service:" + s["name"]] = json.dumps(dict(s))
+        mod.orch.client = httpx.AsyncClient(transport=httpx.MockTransport(handler))
+        return TestClient(mod.app)
+
+    def compare(kind, n, ours_fn, ref_fn):
+        o, r = [], []
+        for _ in range(rounds):
+            o.append(ours_fn())
+            if ref is not None:
+                r.append(ref_fn())
+        rec = {"config": f"plumbing/{kind}", ("services" if kind == "plan" else "nodes"): n,
+               "p50_ms": round(statistics.median(o), 3), "rounds_ms": [round(x, 3) for x in o]}
+        if r:
+            rec.update(reference_same_host_ms=round(statistics.median(r), 3),
+                       reference_rounds_ms=[round(x, 3) for x in r],
+                       speedup=round(statistics.median(r) / statistics.median(o), 2))
+        else:
+            rec.update(reference_other_host_ms=(REF_PLAN_MS if kind == "plan" else REF_EXEC_MS)[n])
+        emit(rec)
+
     for n in (3, 10, 50, 1000):
-        reg = MemoryRegistry(synthetic_registry(n, seed=1))
+        services = synthetic_registry(n, seed=1)
+        reg = MemoryRegistry(services)
         app = create_app(Settings(), registry=reg, planner=StubPlanner(reg, canned=canned),
                          transport=httpx.MockTransport(handler))
+        body = lambda i: {"intent": f"charge order {i}"}
         with TestClient(app) as c:
-            for _ in range(5):
-                c.post("/plan", json={"intent": "warm"})
-            ts = []
-            for i in range(runs):
-                t = time.perf_counter()
-                r = c.post("/plan", json={"intent": f"charge order {i}"})
-                ts.append(time.perf_counter() - t)
-                assert r.status_code == 200
-        p50 = statistics.median(ts) * 1e3
-        print(json.dumps({"config": "plumbing/plan", "services": n, "p50_ms": round(p50, 3),
-                          "reference_ms": REF_PLAN_MS[n], "speedup": round(REF_PLAN_MS[n] / p50, 2)}))
+            rc = ref_client(ref, services) if ref is not None else None
+            compare("plan", n, lambda: time_posts(c, "/plan", body, runs),
+                    lambda: time_posts(rc, "/plan", body, runs))
     for n in (3, 10, 50):
         nodes = [{"name": f"n{i}", "endpoint": f"http://n{i}/api",
                   "inputs": {"x": f"n{i - 1}" if i else "uid"}} for i in range(n)]
@@ -59,19 +155,11 @@ def plumbing(runs: int = 30):
         reg = MemoryRegistry(synthetic_registry(3))
         app = create_app(Settings(), registry=reg, planner=StubPlanner(reg),
                          transport=httpx.MockTransport(handler))
+        body = lambda i: {"graph": {"nodes": nodes, "edges": edges}, "payload": {"uid": 1}}
         with TestClient(app) as c:
-            body = {"graph": {"nodes": nodes, "edges": edges}, "payload": {"uid": 1}}
-            for _ in range(5):
-                c.post("/execute", json=body)
-            ts = []
-            for _ in range(runs):
-                t = time.perf_counter()
-                r = c.post("/execute", json=body)
-                ts.append(time.perf_counter() - t)
-                assert r.status_code == 200
-        p50 = statistics.median(ts) * 1e3
-        print(json.dumps({"config": "plumbing/execute", "nodes": n, "p50_ms": round(p50, 3),
-                          "reference_ms": REF_EXEC_MS[n], "speedup": round(REF_EXEC_MS[n] / p50, 2)}))
+            rc = ref_client(ref, synthetic_registry(3)) if ref is not None else None
+            compare("execute", n, lambda: time_posts(c, "/execute", body, runs),
+                    lambda: time_posts(rc, "/execute", body, runs))
 
 
 def topk(n: int, dim: int, k: int, batches=(1, 16, 32, 64), iters: int = 50):
@@ -229,9 +317,10 @@ if __name__ == "__main__":
     ap.add_argument("--churn", type=int, default=100, help="e2e: services registered during a phase")
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--out", default=None, help="plumbing: also append the JSON lines here")
     a = ap.parse_args()
     if a.which == "plumbing":
-        plumbing()
+        plumbing(out=a.out)
     elif a.which == "e2e":
         e2e(a.n, a.model, a.runs, a.clients, a.churn)
     else:

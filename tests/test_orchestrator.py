@@ -211,3 +211,53 @@ def test_validate_and_normalize():
                         {"service_name": "b", "endpoint": "http://b/api", "input_keys": []}])
     validate_dag(t2)
     assert t2["edges"] == [{"from": "a", "to": "b", "fallback": "http://fb"}]
+
+
+def test_fast_post_path_matches_client_post(caplog):
+    """The orchestrator's fast POST path (client transport, no auth/redirect
+    plumbing) gives the same request bytes and headers, the same results,
+    the same error strings (HTTP status, redirect, non-JSON body, connection
+    error, timeout) and the same httpx INFO line as ``client.post``."""
+    seen = {}
+
+    def handler(request: httpx.Request):
+        key = request.url.host
+        seen.setdefault(key, []).append((request.method, str(request.url),
+                                         sorted(request.headers.multi_items()), request.content))
+        if key == "err":
+            return httpx.Response(500, text="boom")
+        if key == "moved":
+            return httpx.Response(301, headers={"Location": "http://elsewhere/"})
+        if key == "text":
+            return httpx.Response(200, text="not json")
+        if key == "down":
+            raise httpx.ConnectError("All connection attempts failed")
+        if key == "slow":
+            raise httpx.ReadTimeout("timed out")
+        return httpx.Response(200, json={"got": json.loads(request.content), "uni": "é"})
+
+    def outcome(fast):
+        o = make_orch(handler)
+        if not fast:
+            o._fast_ok = lambda: False
+        out = []
+        for host in ("ok", "err", "moved", "text", "down", "slow"):
+            try:
+                out.append(("ok", run(o._post(f"http://{host}/api", {"x": 1, "s": "ünï", "n": None}))))
+            except Exception as e:  # noqa: BLE001 - compared as text
+                out.append((type(e).__name__, str(e)))
+        return out
+
+    with caplog.at_level(logging.INFO, logger="httpx"):
+        slow = outcome(False)
+        n = len(caplog.records)
+        fast = outcome(True)
+    assert fast == slow
+    logs = [r.getMessage() for r in caplog.records if r.name == "httpx"]
+    assert logs[:n] == logs[n:] and any('"HTTP/1.1 500 Internal Server Error"' in m for m in logs)
+    for host, reqs in seen.items():
+        assert reqs[0] == reqs[1], host
+    o = make_orch(handler)
+    assert o._fast_ok()
+    o.client.cookies.set("sid", "1")                 # cookie jars take client.post
+    assert not o._fast_ok()
