@@ -73,20 +73,24 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
                transport: Optional[httpx.AsyncBaseTransport] = None,
                planner_transport: Optional[httpx.AsyncBaseTransport] = None) -> FastAPI:
     settings = settings or Settings.from_env()
-    registry = registry if registry is not None else make_registry(settings.redis_url,
-                                                                   settings.services_prefix)
+    if registry is None:
+        registry = make_registry(settings.redis_url, settings.services_prefix)
+        if settings.synthetic_services > 0 and not settings.redis_url:
+            from ..registry import synthetic_registry
+            registry.register_many(synthetic_registry(settings.synthetic_services, seed=1))
     state = {}
 
     def _make_planner() -> Planner:
         if planner is not None:
             return planner
         if settings.planner_backend == "local":
-            if settings.replicas > 1:
+            if settings.replicas > 1 or settings.router:
                 # request-level DP over replicas, each a TP group of
                 # settings.tp ranks (MCP_REPLICAS=2 MCP_TP=4: two TP=4 planners)
                 from ..parallel.router import ReplicaConfig, ReplicaRouter, group_devices
                 cfg = ReplicaConfig(model=settings.model, max_batch=settings.max_batch,
-                                    max_nodes=settings.max_nodes, seed=settings.seed,
+                                    max_nodes=settings.max_nodes, min_nodes=settings.min_nodes,
+                                    seed=settings.seed,
                                     num_blocks=settings.kv_blocks or None,
                                     max_step_tokens=settings.max_step_tokens,
                                     temperature=settings.temperature,
@@ -214,8 +218,10 @@ def main():  # pragma: no cover - CLI entry (reference :155-157)
     ap = argparse.ArgumentParser(description="MI355X MCP control plane")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--no-access-log", action="store_true",
+                    help="skip uvicorn's per-request access log line")
     args = ap.parse_args()
-    uvicorn.run(create_app(), host=args.host, port=args.port)
+    uvicorn.run(create_app(), host=args.host, port=args.port, access_log=not args.no_access_log)
 
 
 if __name__ == "__main__":  # pragma: no cover

@@ -31,6 +31,7 @@ class Settings:
     redis_url: Optional[str] = None          # None -> in-memory registry
     postgres_dsn: Optional[str] = None       # accepted for parity, unused
     services_prefix: str = SERVICES_PREFIX
+    synthetic_services: int = 0              # >0 and no Redis: seed the in-memory registry (benches, demos)
     # planner
     planner_backend: str = "stub"            # stub | local | openai
     openai_base_url: str = "https://api.openai.com/v1"   # openai backend (reference parity)
@@ -40,11 +41,13 @@ class Settings:
     model: str = "llama3-8b"                 # llama3-8b | llama3-70b | tiny
     tp: int = 1                              # >1: this process is TP rank 0, workers spawned (parallel.tp_serve)
     replicas: int = 1
+    router: bool = False                     # DP router + replica processes even at replicas == 1
     max_batch: int = 256
     max_step_tokens: int = 8192
     kv_blocks: int = 0                       # 0 -> size from free HBM
     temperature: float = 0.2                 # control_plane.py:72
     max_nodes: int = 6
+    min_nodes: int = 1
     topk: int = 32                           # schema retrieval: services kept in prompt
     retrieval_threshold: int = 48            # prune only when registry is larger
     embed_dim: int = 1024
@@ -66,6 +69,7 @@ class Settings:
         return cls(
             redis_url=_env("REDIS_URL", None),
             postgres_dsn=_env("POSTGRES_DSN", None),
+            synthetic_services=_env("MCP_SYNTHETIC_SERVICES", 0, int),
             planner_backend=_env("MCP_PLANNER_BACKEND", "stub"),
             openai_base_url=_env("OPENAI_BASE_URL", "https://api.openai.com/v1"),
             openai_api_key=_env("OPENAI_API_KEY", None),
@@ -74,11 +78,13 @@ class Settings:
             model=_env("MCP_MODEL", "llama3-8b"),
             tp=_env("MCP_TP", 1, int),
             replicas=_env("MCP_REPLICAS", 1, int),
+            router=_env("MCP_ROUTER", False, bool),
             max_batch=_env("MCP_MAX_BATCH", 256, int),
             max_step_tokens=_env("MCP_MAX_STEP_TOKENS", 8192, int),
             kv_blocks=_env("MCP_KV_BLOCKS", 0, int),
             temperature=_env("MCP_TEMPERATURE", 0.2, float),
             max_nodes=_env("MCP_MAX_NODES", 6, int),
+            min_nodes=_env("MCP_MIN_NODES", 1, int),
             topk=_env("MCP_TOPK", 32, int),
             retrieval_threshold=_env("MCP_RETRIEVAL_THRESHOLD", 48, int),
             embed_dim=_env("MCP_EMBED_DIM", 1024, int),

@@ -83,9 +83,10 @@ DEV float uniform01(uint64_t seed, uint64_t a, uint64_t b) {
 // back correctly as torch's signed int64; a row of |x| ~ 3e3 at H = 8192 is
 // 2^36 units.  Precision: 2^-21 per add, ~1e-6 of a row of |x| ~ 1e-2.
 constexpr float SS_FIX = 1048576.f;                   // 2^20
-constexpr float SS_ADD_MAX = 72057594037927936.f;     // 2^56
-DEV unsigned long long ss_fixed(float v) {
-  return (unsigned long long)__float2ull_rn(fminf(v * SS_FIX, SS_ADD_MAX));
+constexpr float SS_ADD_MAX = 72057594037927936.f;     // 2^56: one add of a partial
+constexpr float SS_ROW_MAX = 4611686018427387904.f;   // 2^62: a whole row stored at once
+DEV unsigned long long ss_fixed(float v, float cap = SS_ADD_MAX) {
+  return (unsigned long long)__float2ull_rn(fminf(v * SS_FIX, cap));
 }
 DEV void ss_atomic_add(unsigned long long* p, float v) {
   __hip_atomic_fetch_add(p, ss_fixed(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void row_sumsq_kernel(const bf16* __restrict__
   float acc = 0.f;
   for (int c = lane; c < (H >> 3); c += 64) acc += sumsq_bf16x8(xr[c]);
   acc = wave_sum(acc);
-  if (lane == 0) ss[row] = ss_fixed(acc);
+  if (lane == 0) ss[row] = ss_fixed(acc, SS_ROW_MAX);
 }
 
 void launch_row_sumsq(const void* x, unsigned long long* ss, int T, int H, hipStream_t s) {

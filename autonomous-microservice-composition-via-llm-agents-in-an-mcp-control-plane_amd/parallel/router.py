@@ -58,6 +58,7 @@ class ReplicaConfig:
     model: str
     max_batch: int = 256
     max_nodes: int = 6
+    min_nodes: int = 1
     seed: int = 0
     num_blocks: Optional[int] = None
     max_step_tokens: int = 8192
@@ -71,6 +72,9 @@ class ReplicaConfig:
     tp: int = 1                         # ranks per replica (TP group size)
     tp_backend: Optional[str] = None    # default: nccl (RCCL) on GPUs, gloo on CPU
     full_weights_seed: Optional[int] = None   # tests: shard one full init (tp_serve.build_rank)
+    # model == "stub": the replica answers every intent with this canned DAG
+    # and runs no engine - measures the router / queue path alone
+    stub_plan: Optional[dict] = None
 
 
 def _backend(cfg: ReplicaConfig, device: str) -> str:
@@ -82,6 +86,9 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     """Replica process: owns one engine; plans batches of whatever is queued.
     With ``cfg.tp > 1`` it is rank 0 (the driver) of its group's process
     group at ``port``; the router has spawned the other ranks."""
+    if cfg.model == "stub":
+        _stub_replica_main(idx, cfg, inq, outq)
+        return
     import torch
     from ..engine.engine import LLMEngine
     from ..models.llama import LlamaModel
@@ -128,14 +135,15 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     retriever.start_background()
     from ..planner.tokenizer import tokenizer_for
     planner = LocalPlanner(eng, registry, tokenizer=tokenizer_for(cfg.model),
-                           max_nodes=cfg.max_nodes, retriever=retriever,
+                           max_nodes=cfg.max_nodes, min_nodes=cfg.min_nodes, retriever=retriever,
                            retrieval_threshold=cfg.retrieval_threshold, topk=cfg.topk)
     outq.put(("ready", idx, None))
     pending = {}
     last_hb = time.monotonic()
     while True:
         try:
-            item = inq.get(timeout=0.01 if eng.has_work() else cfg.heartbeat_s)
+            # never wait on the queue while the engine has a step to run
+            item = inq.get_nowait() if eng.has_work() else inq.get(timeout=cfg.heartbeat_s)
         except queue.Empty:
             item = None
         while item is not None:
@@ -154,18 +162,54 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
                     dec, ptoks, stoks = planner.prepare(intent)
                     pending[rid] = eng.submit(dec, stoks, prefix_tokens=ptoks)
                 except Exception as e:  # noqa: BLE001
-                    outq.put(("err", rid, repr(e)))
+                    outq.put(("batch", idx, [("err", rid, repr(e))]))
             try:
                 item = inq.get_nowait()
             except queue.Empty:
                 item = None
         if eng.has_work():
             eng.step()
-        for rid in [r for r, s in pending.items() if s.done]:
-            s = pending.pop(rid)
-            outq.put(("err", rid, s.error) if s.error else ("ok", rid, s.result))
+        done = [r for r, s in pending.items() if s.done]
+        if done:                                       # one message per step, not per request
+            out = []
+            for rid in done:
+                s = pending.pop(rid)
+                out.append(("err", rid, s.error) if s.error else ("ok", rid, s.result))
+            outq.put(("batch", idx, out))
         now = time.monotonic()
         if now - last_hb >= cfg.heartbeat_s:          # liveness for the router's watchdog
+            outq.put(("hb", idx, None))
+            last_hb = now
+
+
+def _stub_replica_main(idx: int, cfg: ReplicaConfig, inq, outq):
+    """``model="stub"``: the replica's queue protocol with an instant planner
+    (every intent gets ``cfg.stub_plan``), so tests and benches time the
+    router, the queues and the API process alone."""
+    plan = cfg.stub_plan or {"nodes": [], "edges": []}
+    outq.put(("ready", idx, None))
+    last_hb = time.monotonic()
+    while True:
+        try:
+            item = inq.get(timeout=cfg.heartbeat_s)
+        except queue.Empty:
+            item = None
+        out = []
+        while item is not None:
+            if item == "stop":
+                if out:
+                    outq.put(("batch", idx, out))
+                return
+            if item[0] != "registry":
+                out.append(("ok", item[0], plan))
+            try:
+                item = inq.get_nowait() if len(out) < 256 else None
+            except queue.Empty:
+                item = None
+        if out:
+            outq.put(("batch", idx, out))
+        now = time.monotonic()
+        if now - last_hb >= cfg.heartbeat_s:
             outq.put(("hb", idx, None))
             last_hb = now
 
@@ -325,6 +369,7 @@ class ReplicaRouter(Planner):
             self._inqs[i].put((rid, intent))
 
     def _pump(self):
+        last_health = 0.0
         while not self._stop.is_set():
             try:
                 kind, rid, val = self._outq.get(timeout=0.2)
@@ -336,19 +381,29 @@ class ReplicaRouter(Planner):
                     self._last_msg[idx] = time.monotonic()
                     if kind == "ready" and self._procs[idx].is_alive():
                         self.alive[idx] = True
-            elif kind in ("ok", "err"):
+            elif kind == "batch":                      # results of one replica step
+                idx, done = rid, val
+                resolve = []
                 with self._lock:
-                    for i, d in self.inflight.items():
-                        if d.pop(rid, None) is not None:
-                            self._last_msg[i] = time.monotonic()
-                    entry = self._futs.pop(rid, None)
-                if entry is not None:
-                    loop, fut = entry
-                    if kind == "ok":
-                        loop.call_soon_threadsafe(_resolve, fut, val, None)
-                    else:
-                        loop.call_soon_threadsafe(_resolve, fut, None, RuntimeError(val))
-            self._check_health()
+                    self._last_msg[idx] = time.monotonic()
+                    for k, r, v in done:
+                        for d in self.inflight.values():
+                            if d.pop(r, None) is not None:
+                                break
+                        entry = self._futs.pop(r, None)
+                        if entry is not None:
+                            resolve.append((entry, k, v))
+                by_loop = {}
+                for (loop, fut), k, v in resolve:
+                    by_loop.setdefault(loop, []).append(
+                        (fut, v, None) if k == "ok" else (fut, None, RuntimeError(v)))
+                for loop, items in by_loop.items():     # one wake-up per event loop
+                    loop.call_soon_threadsafe(_resolve_many, items)
+            # liveness (process table syscalls) at most every 50 ms, not per message
+            now = time.monotonic()
+            if kind is None or now - last_health >= 0.05:
+                last_health = now
+                self._check_health()
 
     def _check_health(self):
         now = time.monotonic()
@@ -389,9 +444,15 @@ class ReplicaRouter(Planner):
         rid = next(self._ids)
         self._futs[rid] = (loop, fut)
         self._dispatch(rid, intent)
+        # a timer on the future instead of asyncio.wait_for (which wraps every
+        # request in an extra task: ~20 % of the API process's time per plan
+        # at thousands of plans/s)
+        timer = loop.call_later(self.request_timeout, _resolve, fut, None,
+                                TimeoutError(f"plan not done in {self.request_timeout:.0f}s"))
         try:
-            return await asyncio.wait_for(fut, self.request_timeout)
+            return await fut
         finally:
+            timer.cancel()
             self._futs.pop(rid, None)
 
     def kill_replica(self, i: int):        # fault injection (tests)
@@ -410,6 +471,11 @@ class ReplicaRouter(Planner):
                 proc.join(timeout=30)
                 if proc.is_alive():
                     proc.kill()
+
+
+def _resolve_many(items):
+    for fut, val, exc in items:
+        _resolve(fut, val, exc)
 
 
 def _resolve(fut, val, exc):

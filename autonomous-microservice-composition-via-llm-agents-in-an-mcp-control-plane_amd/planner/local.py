@@ -97,7 +97,8 @@ class LocalPlanner(Planner):
         if tok.vocab_size > model.cfg.vocab_size:
             raise ValueError(f"tokenizer vocabulary {tok.vocab_size} exceeds the model's "
                              f"{model.cfg.vocab_size}")
-        return cls(eng, registry, tokenizer=tok, max_nodes=settings.max_nodes, retriever=retr,
+        return cls(eng, registry, tokenizer=tok, max_nodes=settings.max_nodes,
+                   min_nodes=getattr(settings, "min_nodes", 1), retriever=retr,
                    retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
 
     # ----------------------------------------------------------- prepare

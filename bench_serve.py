@@ -89,6 +89,108 @@ def run_qps(planner, engine, qps, duration, seed, rank):
     return lat, dags, elapsed, n, batch_sizes
 
 
+def run_via_api(args):
+    """Config 5 through the deployment path: ``python -m mcp_amd.api.server``
+    (uvicorn + FastAPI, ``create_app`` from the environment) in a child
+    process with the local planner - ``--replicas N`` DP replica processes
+    behind the router (``MCP_REPLICAS`` / ``MCP_ROUTER``), or with
+    ``--replicas 0`` the in-process engine thread of a one-GPU server - and
+    this process as the load generator: Poisson arrivals of ``--qps`` per
+    replica over HTTP (httpx, 127.0.0.1), each request's arrival -> DAG time.
+    Same model, registry, DAG size and engine limits as the direct ``qps``
+    mode, so the two lines compare the engine with and without the front end."""
+    import asyncio
+    import logging
+    import subprocess
+    import httpx
+    from mcp_amd.parallel.launch import free_port
+    logging.getLogger("httpx").setLevel(logging.WARNING)
+    port = free_port()
+    nrep = max(0, args.replicas)
+    env = dict(os.environ, MCP_PLANNER_BACKEND="local", MCP_MODEL=args.model,
+               MCP_MAX_BATCH="512", MCP_MAX_STEP_TOKENS="16384", MCP_TEMPERATURE="0.2",
+               MCP_MAX_NODES=str(args.max_nodes), MCP_MIN_NODES=str(args.min_nodes),
+               MCP_SEED=str(args.seed), MCP_REPLICAS=str(max(1, nrep)),
+               MCP_ROUTER="1" if nrep >= 1 else "0", MCP_SYNTHETIC_SERVICES=str(args.services))
+    if args.no_graphs:
+        env["MCP_GRAPHS"] = "0"
+    log_path = os.environ.get("MCP_SERVER_LOG", "/tmp/mcp_api_server.log")
+    srv = subprocess.Popen([sys.executable, "-m", "mcp_amd.api.server", "--host", "127.0.0.1",
+                            "--port", str(port), "--no-access-log"],
+                           env=env, stdout=open(log_path, "w"), stderr=subprocess.STDOUT,
+                           cwd=os.path.dirname(os.path.abspath(__file__)))
+    base = f"http://127.0.0.1:{port}"
+    reg = MemoryRegistry(synthetic_registry(args.services, seed=1))
+    names = [s.name for s in reg.list_services()]
+
+    async def drive():
+        limits = httpx.Limits(max_connections=4096, max_keepalive_connections=1024)
+        async with httpx.AsyncClient(base_url=base, timeout=600.0, limits=limits) as c:
+            t0 = time.time()
+            while True:                                  # start-up: model init + graph capture
+                if srv.poll() is not None:
+                    raise RuntimeError(f"server exited ({srv.returncode}); see {log_path}")
+                try:
+                    if (await c.get("/healthz")).status_code == 200:
+                        break
+                except httpx.TransportError:
+                    pass
+                if time.time() - t0 > 900:
+                    raise TimeoutError("server did not start")
+                await asyncio.sleep(1.0)
+            log(f"server ready after {time.time() - t0:.1f}s")
+            # the server's in-memory registry holds the same synthetic services
+            # (MCP_SYNTHETIC_SERVICES, seed 1)
+            await asyncio.gather(*[c.post("/plan", json={"intent": synthetic_intent(-1 - i)})
+                                   for i in range(max(1, args.warmup))])
+            qps = args.qps * max(1, nrep)
+            rng = np.random.default_rng(args.seed)
+            n = max(1, int(qps * args.duration))
+            arrivals = np.cumsum(rng.exponential(1.0 / qps, n))
+            lat, dags, errs = [], [], []
+
+            async def one(i):
+                r = await c.post("/plan", json={"intent": synthetic_intent(i)})
+                if r.status_code != 200:
+                    errs.append(r.text)
+                    return
+                dags.append(r.json()["graph"])
+                lat.append(time.perf_counter() - (t_start + arrivals[i]))
+            tasks = []
+            t_start = time.perf_counter()
+            for i in range(n):
+                delay = t_start + arrivals[i] - time.perf_counter()
+                if delay > 0:
+                    await asyncio.sleep(delay)
+                tasks.append(asyncio.create_task(one(i)))
+            await asyncio.gather(*tasks)
+            elapsed = time.perf_counter() - t_start
+            metrics = (await c.get("/metrics")).text
+            return lat, dags, errs, elapsed, n, metrics
+
+    try:
+        lat, dags, errs, elapsed, n, metrics = asyncio.run(drive())
+    finally:
+        srv.terminate()
+        try:
+            srv.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            srv.kill()
+    if errs:
+        raise RuntimeError(f"{len(errs)} requests failed: {errs[0][:300]}")
+    for d in dags:
+        validate_dag(d, names)
+    out = {"metric": "plans/sec at fixed QPS through the API (config 5, deployment path)",
+           "path": f"uvicorn + FastAPI + {'router -> %d replica process(es)' % nrep if nrep else 'in-process engine thread'}",
+           "model": args.model, "services": args.services, "dtype": "bf16",
+           "data": "synthetic intents, random-init weights", "replicas": nrep,
+           "nodes_per_plan": [args.min_nodes, args.max_nodes], "offered_qps": args.qps * max(1, nrep),
+           "value": round(len(lat) / elapsed, 2), "unit": "plans/s",
+           "p50_latency_ms": round(statistics.median(lat) * 1e3, 1),
+           "p99_latency_ms": round(pct(lat, 99) * 1e3, 1), "requests": n, "duration_s": args.duration}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=["single", "qps"])
@@ -103,7 +205,13 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); N > 1 self-launches")
+    ap.add_argument("--via-api", action="store_true",
+                    help="qps: drive the HTTP API server (child process) instead of the engine")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="--via-api: DP replica processes behind the router (0: in-process engine)")
     args = ap.parse_args()
+    if args.via_api:
+        return run_via_api(args)
     from mcp_amd.parallel.launch import check_devices, self_launch
     rc = self_launch(args.gpus)
     if rc is not None:

@@ -8,6 +8,8 @@ import time
 
 import pytest
 
+from mcp_amd.api.server import create_app
+from mcp_amd.config import Settings
 from mcp_amd.orchestrator import validate_dag
 from mcp_amd.parallel.router import ReplicaConfig, ReplicaRouter
 from mcp_amd.planner.prompt import synthetic_intent
@@ -148,3 +150,77 @@ def test_router_replicas_of_tp_groups_match_local_planner(monkeypatch):
     ref = LocalPlanner(eng, reg, max_nodes=3).plan_many(intents)
     assert dags == ref
     assert again == ref[0]
+
+
+def test_router_and_api_dispatch_rate_with_stub_replicas():
+    """the API process must not be the ceiling for a node of 8
+    replicas at ~211 plans/s each (~1.7k plans/s).  Four replica processes
+    with an instant planner (``model="stub"``): the router alone and the
+    FastAPI app in front of it (raw ASGI calls, no HTTP client in the loop)
+    each complete >= 2000 requests/s, every reply the canned DAG."""
+    import json as _json
+    import time as _time
+    plan = {"nodes": [{"name": f"s{i}", "endpoint": f"http://s{i}/api", "inputs": {"x": "uid"}}
+                      for i in range(5)],
+            "edges": [{"from": f"s{i - 1}", "to": f"s{i}"} for i in range(1, 5)]}
+    reg = MemoryRegistry(synthetic_registry(10, seed=1))
+    router = ReplicaRouter(["cpu"] * 4, "stub", reg, config=ReplicaConfig(model="stub", stub_plan=plan))
+    try:
+        async def direct(n):
+            sem = asyncio.Semaphore(512)
+
+            async def one(i):
+                async with sem:
+                    return await router.plan(f"intent {i}")
+            await asyncio.gather(*[one(i) for i in range(500)])       # warm
+            t = _time.perf_counter()
+            out = await asyncio.gather(*[one(i) for i in range(n)])
+            return n / (_time.perf_counter() - t), out
+        rate, out = asyncio.run(direct(8000))
+        assert all(o == plan for o in out)
+        assert rate >= 2000, rate
+        assert sum(router.respawns) == 0 and all(not d for d in router.inflight.values())
+
+        app = create_app(Settings(), registry=reg, planner=router)
+        body = _json.dumps({"intent": "charge the order"}).encode()
+
+        async def call():
+            scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1",
+                     "method": "POST", "scheme": "http", "path": "/plan", "raw_path": b"/plan",
+                     "query_string": b"", "root_path": "", "client": ("127.0.0.1", 1),
+                     "server": ("127.0.0.1", 80),
+                     "headers": [(b"content-type", b"application/json"),
+                                 (b"content-length", str(len(body)).encode())]}
+            state = {"sent": False}
+            msgs = []
+
+            async def receive():
+                if not state["sent"]:
+                    state["sent"] = True
+                    return {"type": "http.request", "body": body, "more_body": False}
+                await asyncio.sleep(3600)
+
+            async def send(m):
+                msgs.append(m)
+            await app(scope, receive, send)
+            assert msgs[0]["status"] == 200
+            return _json.loads(msgs[1]["body"])
+
+        async def via_app(n):
+            # the lifespan would wrap ``router`` in nothing here (no cache /
+            # adaptive) and close it on exit: fill the state by hand instead
+            app.state.components["planner"] = router
+            sem = asyncio.Semaphore(64)
+
+            async def one():
+                async with sem:
+                    return await call()
+            await asyncio.gather(*[one() for _ in range(500)])
+            t = _time.perf_counter()
+            out = await asyncio.gather(*[one() for _ in range(n)])
+            return n / (_time.perf_counter() - t), out
+        rate, out = asyncio.run(via_app(6000))
+        assert all(o == {"graph": plan} for o in out)
+        assert rate >= 2000, rate
+    finally:
+        router.close()
