@@ -97,13 +97,24 @@ class AllReduce:
 
     ``check()`` raises when a K12 barrier timed out (a peer never arrived): the
     engine calls it after every step, so a lost peer is a hard failure instead
-    of activations summed from stale staging buffers."""
+    of activations summed from stale staging buffers.
+
+    Start-up self-check (``MCP_CAR_SELFCHECK=1``, default): K12's peers read
+    each other's staging buffers over xGMI (coarse-grained ``hipMalloc``
+    memory, system-scope flags, ``csrc/custom_allreduce.hip``).  Before the
+    first real message every rank sums probe tensors of known integer values
+    through K12 in both modes (one-shot and two-shot) and through the RCCL
+    path, and checks both against the exact sum; the ranks agree on the
+    outcome (``all_gather_object``), and a K12 mismatch on any rank disables
+    K12 on every rank (all messages then take RCCL) with a logged reason
+    (``custom_disabled``).  An RCCL mismatch is a hard error."""
 
     def __init__(self, group, device):
         self.group = group
         self.device = torch.device(device)
         self.custom = None
         self.native = None
+        self.custom_disabled: Optional[str] = None
         if self.device.type != "cuda":
             return
         world = dist.get_world_size(group)
@@ -115,6 +126,37 @@ class AllReduce:
                                                                        str(8 << 20))))
         if os.environ.get("MCP_COMM", "native") == "native":
             self.native = NativeComm(group, self.device)
+        if self.custom is not None and os.environ.get("MCP_CAR_SELFCHECK", "1") == "1":
+            self._selfcheck()
+
+    def _reference_sum(self, t: torch.Tensor) -> None:
+        if self.native is not None:
+            self.native.all_reduce(t)
+        else:
+            dist.all_reduce(t, group=self.group)
+
+    def _selfcheck(self) -> None:
+        rank, world = dist.get_rank(self.group), dist.get_world_size(self.group)
+        inject = os.environ.get("MCP_CAR_SELFCHECK_INJECT")   # tests: this rank's K12 result is wrong
+        sizes = [n for n in (8 << 10, min(self.custom.max_bytes, 2 << 20) // 2)
+                 if 0 < n * 2 <= self.custom.max_bytes]
+        with torch.cuda.device(self.device):
+            verdict = selfcheck_decision(
+                rank, world, sizes,
+                probe=lambda n, r: probe_values(n, r, self.device),
+                custom=lambda t, mode: self.custom(t, mode=mode),
+                reference=self._reference_sum,
+                agree=lambda mine: _gather_objects(mine, self.group),
+                inject=inject is not None and int(inject) == rank)
+        if verdict.get("reference_error"):
+            raise RuntimeError(f"all-reduce self-check: the RCCL path is wrong: {verdict}")
+        if not verdict["custom_ok"]:
+            import logging
+            logging.getLogger("mcp.comm").warning(
+                "custom all-reduce (K12) disabled: start-up self-check mismatch %s", verdict["why"])
+            self.custom.close()
+            self.custom = None
+            self.custom_disabled = verdict["why"]
 
     def __call__(self, t: torch.Tensor) -> None:
         if self.device.type != "cuda":
@@ -141,6 +183,50 @@ class AllReduce:
         if self.custom is not None and nbytes <= self.custom.max_bytes:
             return True
         return self.native is not None or not _is_gloo(self.group)
+
+
+def probe_values(n: int, rank: int, device) -> torch.Tensor:
+    """Self-check probe: small integers (exact in bf16, and so is their sum
+    over <= 8 ranks) that differ per rank and per element."""
+    i = torch.arange(n, device=device, dtype=torch.int32)
+    return ((i * 7 + rank * 3) % 11 + (i % 5 == rank % 5).int() * 2).to(torch.bfloat16)
+
+
+def selfcheck_decision(rank: int, world: int, sizes, probe, custom, reference, agree,
+                       inject: bool = False) -> dict:
+    """One rank's part of the K12 start-up self-check.  For every probe size,
+    K12 one-shot (mode 1) and two-shot (mode 2) and the reference collective
+    each sum ``probe(n, rank)`` over the group and are compared with the exact
+    sum (computed locally from ``probe(n, r)`` of every rank).  ``agree``
+    exchanges every rank's findings; K12 stays on only if no rank saw a
+    mismatch.  Returns {"custom_ok", "reference_error", "why"}."""
+    bad, ref_bad = [], []
+    for n in sizes:
+        exact = sum(probe(n, r).float() for r in range(world))
+        for mode in (1, 2):
+            t = probe(n, rank)
+            out = custom(t, mode)
+            if inject:
+                out = out.clone()
+                out[n // 2] += 1
+            if not torch.equal(out.float(), exact):
+                bad.append(f"rank {rank}: K12 mode {mode}, {n * 2} B: "
+                           f"{int((out.float() != exact).sum())} wrong elements")
+        t = probe(n, rank)
+        reference(t)
+        if not torch.equal(t.float(), exact):
+            ref_bad.append(f"rank {rank}: reference all-reduce, {n * 2} B")
+    every = agree({"bad": bad, "ref_bad": ref_bad})
+    bad_all = [b for e in every for b in e["bad"]]
+    ref_all = [b for e in every for b in e["ref_bad"]]
+    return {"custom_ok": not bad_all, "reference_error": bool(ref_all),
+            "why": "; ".join(bad_all + ref_all) or None}
+
+
+def _gather_objects(obj, group):
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
 
 
 def make_allreduce(group, device) -> AllReduce:

@@ -179,3 +179,66 @@ def test_custom_allreduce_missing_peer_is_a_hard_error():
                 p.kill()
     assert results[0] is True, results
     assert results[1] is None, results
+
+
+def _selfcheck_worker(rank, world, port, inject, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MCP_COMM="torch",
+                          MCP_CUSTOM_ALLREDUCE="1", MCP_CAR_MAX_BYTES=str(4 << 20))
+        if inject is not None:
+            os.environ["MCP_CAR_SELFCHECK_INJECT"] = str(inject)
+        import torch.distributed as dist
+        import mcp_amd  # noqa: F401
+        from mcp_amd.parallel.comm import AllReduce
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        ar = AllReduce(dist.group.WORLD, "cuda:0")
+        x = _data(rank, 8192, 5).cuda()
+        ar(x)                                   # K12 if it survived the check, else gloo
+        torch.cuda.synchronize()
+        ref = sum(_data(r, 8192, 5).float() for r in range(world))
+        err = (x.float().cpu() - ref).abs().max().item()
+        ar.check()
+        on = ar.custom is not None
+        if on:
+            ar.custom.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, on, ar.custom_disabled, err))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e), None))
+
+
+@pytest.mark.parametrize("inject", [None, 1])
+def test_allreduce_startup_selfcheck(inject):
+    """at AllReduce start-up every rank sums known probes
+    through K12 (one- and two-shot) and the reference path; a healthy K12
+    stays on, an injected mismatch on rank 1 turns K12 off on BOTH ranks with
+    the reason, and the all-reduce stays correct either way."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_selfcheck_worker, args=(r, world, port, inject, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, on, why, err = q.get(timeout=240)
+            out[rank] = (on, why, err)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, (on, why, err) in out.items():
+        assert on is not None, why
+        assert err is not None and err < 0.05, (rank, err)
+        if inject is None:
+            assert on and why is None, (rank, why)
+        else:
+            assert not on and "rank 1: K12 mode" in why, (rank, why)

@@ -22,10 +22,11 @@ streams the whole model, nothing stays in the 256 MB Infinity Cache).
 hipBLASLt (``torch.matmul`` / ``addmm_``) is timed beside them as a yardstick
 only ("ref_us": [ours, hipBLASLt] per bucket); nothing dispatches to it.
 
-    python tools/tune_gemm_plan.py [out.json] [m_max] [8b|70b]
+    python tools/tune_gemm_plan.py [out.json] [m_max] [8b|70b|70b-tp8|8b-tp2+8b-tp4...]
 
 ``70b``: the Llama-3-70B TP=1 projections (config 4) instead of the 8B ones;
-tools/merge_gemm_plan.py folds such a file into the shipped plan.
+``<model>-tp<t>``: one rank's shards of a TP=t group (qkv / o / gate|up / down
+divided by t); tools/merge_gemm_plan.py folds such a file into the shipped plan.
 """
 import json
 import os
@@ -42,11 +43,29 @@ L = ops.lib()
 L.gemm_plan_clear()
 out_path = sys.argv[1] if len(sys.argv) > 1 else ops.GEMM_PLAN_FILE
 m_max = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
-# Llama-3-8B (TP=1): qkv, o, gate|up (SwiGLU, interleaved), down; 70B (TP=1) on request
+# per-rank projections of Llama-3 8B / 70B at TP = t (Megatron 1-D shards):
+# qkv [(Hq + 2 Hkv) D / t, H], o [H, Hq D / t], gate|up (SwiGLU, interleaved)
+# [2 F / t, H], down [H, F / t].  "8b" / "70b" = TP 1; "70b-tp8" etc. the shards
+# one rank of a TP group runs (o / down with the residual epilogue, as rank 0
+# does); several specs joined by "+" tune together
+ARCH = {"8b": (4096, 32, 8, 14336), "70b": (8192, 64, 8, 28672)}
+
+
+def shard_shapes(spec):
+    name, _, tp = spec.partition("-tp")
+    H, hq, hkv, F = ARCH[name]
+    t = int(tp or 1)
+    return [((hq + 2 * hkv) * 128 // t, H), (H, hq * 128 // t), (2 * F // t, H), (H, F // t)]
+
+
 MODEL = sys.argv[3] if len(sys.argv) > 3 else "8b"
-SHAPES = {"8b": [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)],
-          "70b": [(10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672)]}[MODEL]
-SWIGLU_N = {28672, 57344}
+SHAPES, SWIGLU_N = [], set()
+for spec in MODEL.split("+"):
+    for i, sh in enumerate(shard_shapes(spec)):
+        if sh not in SHAPES:
+            SHAPES.append(sh)
+        if i == 2:
+            SWIGLU_N.add(sh[0])
 MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
@@ -96,7 +115,7 @@ result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
           "flex": "measured flex tile per bucket (gemm_flex.hip candidate, +32 = 4-stage; -1 = none)",
           "ref_us": "[ours, hipBLASLt] us per bucket, yardstick only",
           "generated": time.strftime("%Y-%m-%d"), "shapes": []}
-RESIDUAL.update({(4096, 4096), (4096, 14336), (8192, 8192), (8192, 28672)})
+RESIDUAL.update(sh for spec in MODEL.split("+") for i, sh in enumerate(shard_shapes(spec)) if i in (1, 3))
 t0 = time.time()
 for (N, K) in SHAPES:
     Xf = torch.randn(m_max, K, device=dev).bfloat16()
