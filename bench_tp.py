@@ -38,6 +38,205 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# xGMI / RCCL assumptions of the TP prediction (--simulate-rank), not
+# measurements: 7 links x ~153 GB/s per MI355X (one direction), RCCL
+# all-reduce bus bandwidth for large messages, and a per-call launch +
+# hand-off latency for RCCL; K12's latency floor IS measured (two processes
+# on this GPU), its xGMI read time is added from the link model
+XGMI_LINK_GBS = float(os.environ.get("MCP_SIM_XGMI_GBS", "153"))
+RCCL_BUSBW_GBS = float(os.environ.get("MCP_SIM_RCCL_BUSBW_GBS", "300"))
+RCCL_LAT_US = float(os.environ.get("MCP_SIM_RCCL_LAT_US", "25"))
+
+
+class _SimAllReduce:
+    """Stands in for the TP group's all-reduce on a simulated rank: no data
+    moves (the rank's partial sums flow on unreduced - the arithmetic per
+    rank is unchanged), capturable in hipGraphs like K12."""
+
+    def __call__(self, t):
+        return None
+
+    def check(self):
+        return None
+
+    def graph_safe(self, nbytes):
+        return True
+
+
+def _k12_timer(rank, world, port, sizes, q):
+    """Two K12 ranks on this GPU: us per all-reduce of each size (eager,
+    both ranks calling together; the flag barriers and kernel launches are
+    the real ones, the peer reads hit local HBM instead of xGMI)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        from mcp_amd.parallel.custom_allreduce import CustomAllReduce
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        car = CustomAllReduce(dist.group.WORLD, "cuda:0", max_bytes=max(sizes))
+        out = {}
+        for nb in sizes:
+            x = torch.randn(nb // 2, device="cuda").bfloat16()
+            for _ in range(5):
+                car(x)
+            torch.cuda.synchronize()
+            dist.barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(40):
+                car(x)
+            e1.record()
+            torch.cuda.synchronize()
+            out[nb] = e0.elapsed_time(e1) / 40 * 1e3
+        car.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e)))
+
+
+def simulate_rank(args):
+    """config 4 at TP = ``--simulate-rank`` predicted on ONE
+    GPU.  Rank 0 of the TP group runs alone: its real weight shards (qkv / o /
+    gate|up / down divided by tp, random init), its KV heads, the driver's
+    scheduler, grammar and sampling, hipGraphs as a TP driver captures them -
+    with the all-reduces replaced by no-ops, so the timed batches give the
+    rank's compute time.  Every all-reduce the steps would issue (2 per layer
+    of [T, H] bf16, the last layer on the sampled rows) is then priced: K12
+    sizes (<= MCP_CAR_MAX_BYTES) at max(measured two-process K12 call on this
+    GPU, link-model xGMI read time), larger ones at the RCCL model
+    (assumptions above, reported in the JSON).  No overlap of communication
+    with compute is assumed."""
+    import torch.multiprocessing as mp
+    from mcp_amd.engine.engine import LLMEngine
+    from mcp_amd.engine.kv_cache import KVCache
+    from mcp_amd.models.llama import LlamaModel, get_config, random_weights
+    from mcp_amd.orchestrator import validate_dag
+    from mcp_amd.parallel.launch import free_port
+    from mcp_amd.planner.local import LocalPlanner
+    from mcp_amd.planner.prompt import synthetic_intent
+    from mcp_amd.registry import MemoryRegistry, synthetic_registry
+
+    tp = args.simulate_rank
+    cuda = torch.cuda.is_available()
+    dev = torch.device("cuda", 0) if cuda else torch.device("cpu")
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    cfg = get_config(args.model)
+    H = cfg.hidden
+    t0 = time.time()
+    model = LlamaModel(cfg, random_weights(cfg, dev, seed=args.seed, tp_rank=0, tp=tp), dev,
+                       0, tp, None, allreduce=_SimAllReduce())
+    sync()
+    log(f"[sim rank 0 of TP={tp}] {args.model} shard ready in {time.time() - t0:.1f}s")
+    per_block = KVCache.bytes_per_block(cfg.layers, model.hkv, cfg.head_dim)
+    if cuda:
+        free, total = torch.cuda.mem_get_info(dev)
+        nb = int(min(65536, (free - 0.1 * total) // per_block))
+    else:
+        nb = 64 + 8 * args.batch
+    eng = LLMEngine(model, num_blocks=nb, max_batch=args.batch + 8, max_step_tokens=16384,
+                    temperature=0.2, seed=args.seed, graphs=cuda)
+    reg = MemoryRegistry(synthetic_registry(args.services, seed=4))
+    planner = LocalPlanner(eng, reg, max_nodes=args.max_nodes, retrieval_threshold=10 ** 9)
+    names = [s.name for s in reg.list_services()]
+    ncap = eng.warm_graphs(contexts=(8192,))
+    steps = []
+    real = eng._schedule_launch
+
+    def rec(cohort):
+        L = real(cohort)
+        if L is not None:
+            steps.append((L.T, len(L.sample_seqs)))
+        return L
+    eng._schedule_launch = rec
+
+    def one_step(base):
+        seqs = planner.submit_many([synthetic_intent(base + i) for i in range(args.batch)])
+        eng.run()
+        return seqs
+    for w in range(args.warmup):
+        one_step(10_000 + w * args.batch)
+    sync()
+    steps.clear()
+    t = time.perf_counter()
+    seqs_all = []
+    for s in range(args.steps):
+        seqs_all += one_step(s * args.batch)
+    sync()
+    compute_s = time.perf_counter() - t
+    for q in seqs_all:
+        if q.error:
+            raise RuntimeError(q.error)
+        validate_dag(q.result, names)
+    lats = sorted(q.t_done - q.t_submit for q in seqs_all)
+
+    # ---- every all-reduce of the timed steps
+    msgs = []
+    for T, ns in steps:
+        msgs += [T * H * 2] * (2 * (cfg.layers - 1)) + ([ns * H * 2] * 2 if ns else [])
+    car_max = int(os.environ.get("MCP_CAR_MAX_BYTES", str(8 << 20)))
+    # K12 sizes measured on a grid (64-token steps of [T, H] bf16, up to the K12 limit)
+    grid = sorted({min(car_max, -(-m // (64 * H * 2)) * 64 * H * 2) for m in msgs if m <= car_max})
+    k12 = {b: 0.0 for b in grid}              # CPU dry run: the link model alone
+    if grid and cuda:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = free_port()
+        procs = [ctx.Process(target=_k12_timer, args=(r, 2, port, grid, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        got = {}
+        try:
+            for _ in range(2):
+                r, out = q.get(timeout=300)
+                got[r] = out
+        finally:
+            for p in procs:
+                p.join(timeout=30)
+                if p.is_alive():
+                    p.kill()
+        if any(isinstance(v, str) for v in got.values()):
+            raise RuntimeError(f"K12 timing failed: {got}")
+        k12 = {nbytes: max(got[0][nbytes], got[1][nbytes]) for nbytes in grid}
+    one_shot_max = int(os.environ.get("MCP_CAR_ONE_SHOT_MAX", str(256 * 1024)))
+
+    def price_us(m):
+        if m <= car_max:
+            b = min(car_max, -(-m // (64 * H * 2)) * 64 * H * 2)
+            # xGMI reads: one-shot pulls every peer's whole buffer (7 links in
+            # parallel), two-shot a 1/tp slice twice
+            read = m / (XGMI_LINK_GBS * 1e3) if m <= one_shot_max else 2 * m / tp / (XGMI_LINK_GBS * 1e3)
+            return max(k12[b], read + k12[b] * 0.5), "k12"
+        return RCCL_LAT_US + m * 2 * (tp - 1) / tp / (RCCL_BUSBW_GBS * 1e3), "rccl"
+    comm = {"k12": 0.0, "rccl": 0.0}
+    ncalls = {"k12": 0, "rccl": 0}
+    for m in msgs:
+        us, kind = price_us(m)
+        comm[kind] += us * 1e-6
+        ncalls[kind] += 1
+    comm_s = comm["k12"] + comm["rccl"]
+    plans = len(seqs_all)
+    pred_s = compute_s + comm_s
+    print(json.dumps({
+        "config": "llama3-70b TP planner, 50-service registry (config 4), one rank simulated on one GPU",
+        "model": args.model, "tp": tp, "services": args.services, "batch": args.batch,
+        "steps": args.steps, "engine_steps": len(steps), "tokens": sum(T for T, _ in steps),
+        "plans": plans, "graphs_captured": ncap,
+        "rank_compute_s": round(compute_s, 3),
+        "rank_compute_plans_per_s": round(plans / compute_s, 2),
+        "allreduce_calls": ncalls, "allreduce_s": {k: round(v, 3) for k, v in comm.items()},
+        "k12_measured_us": {str(k): round(v, 1) for k, v in k12.items()},
+        "predicted_step_s": round(pred_s / args.steps, 3),
+        "predicted_plans_per_s": round(plans / pred_s, 2),
+        "predicted_p50_latency_ms_upper": round(lats[len(lats) // 2] * pred_s / compute_s * 1e3, 1),
+        "measured": "rank-0 compute (GEMM shards, attention on its KV heads, norms, sampling, "
+                    "scheduler, hipGraphs) and K12 call time (two processes on one GPU)",
+        "modelled": {"xgmi_link_GBps": XGMI_LINK_GBS, "rccl_busbw_GBps": RCCL_BUSBW_GBS,
+                     "rccl_latency_us": RCCL_LAT_US, "overlap": "none"},
+        "data": "synthetic intents, random-init weights",
+    }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-70b")
@@ -50,7 +249,11 @@ def main():
     ap.add_argument("--seq-parallel", action="store_true",
                     help="Megatron sequence parallelism (reduce-scatter / all-gather) for TP > 1")
     ap.add_argument("--gpus", type=int, default=1, help="TP degree = ranks (one per GPU); N > 1 self-launches")
+    ap.add_argument("--simulate-rank", type=int, default=0, metavar="TP",
+                    help="predict config 4 at TP=N from one rank's shards on one GPU (simulate_rank)")
     args = ap.parse_args()
+    if args.simulate_rank > 1:
+        return simulate_rank(args)
     from mcp_amd.parallel.launch import check_devices, self_launch
     rc = self_launch(args.gpus)
     if rc is not None:
