@@ -53,6 +53,18 @@ class PrefixEntry:
     blocks: List[int]          # ceil(length / 64) blocks; the last may be partial
     length: int                # prefix tokens
     computed: bool = False
+    hashes: tuple = ()         # chained hashes of the full 64-token blocks
+    shared: int = 0            # leading blocks taken from other cached prefixes
+
+
+def block_hashes(tokens: Seq[int]) -> tuple:
+    """Chained hash of every full 64-token block: block i's hash covers
+    tokens [0, 64 (i + 1)), so equal hashes mean equal KV for that block."""
+    out, h = [], 0
+    for b in range(len(tokens) // BLOCK_SIZE):
+        h = hash((h, tuple(tokens[b * BLOCK_SIZE:(b + 1) * BLOCK_SIZE])))
+        out.append(h)
+    return tuple(out)
 
 
 class Sequence:
@@ -174,6 +186,13 @@ class LLMEngine:
         self.prefixes: Dict[tuple, PrefixEntry] = {}     # insertion order = LRU order
         self._last_prefix = None                         # (token list object, entry)
         self.max_prefixes = 64
+        # block-level prefix reuse: chained block hash -> keys of cached
+        # entries holding that block (a new prefix shares the leading full
+        # blocks it has in common with any computed entry, e.g. retrieved
+        # service lists that start with the same services; MCP_BLOCK_REUSE=0
+        # disables)
+        self._block_index: Dict[int, Dict[tuple, int]] = {}
+        self.block_reuse = os.environ.get("MCP_BLOCK_REUSE", "1") == "1"
         self.steps = 0
         if self._graphs_wanted:
             from .graphs import GraphRunner
@@ -201,23 +220,69 @@ class LLMEngine:
             self.prefixes[tokens] = e                  # refresh LRU position
         else:
             while len(self.prefixes) >= self.max_prefixes:   # evict the LRU entry
-                old = next(iter(self.prefixes))
-                self.alloc.free(self.prefixes.pop(old).blocks)
+                self._drop_entry(next(iter(self.prefixes)))
             need = (len(tokens) + BLOCK_SIZE - 1) // BLOCK_SIZE
+            hashes = block_hashes(tokens) if self.block_reuse else ()
+            shared = self._shared_blocks(tokens, hashes)
+            self.alloc.incref(shared)          # held before eviction can drop their entries
             # a full pool: drop cached prefixes before giving up sharing -
             # with retrieval every request may bring its own prefix
-            if not self._evict_prefixes(need):
+            if not self._evict_prefixes(need - len(shared)):
+                if shared:
+                    self.alloc.free(shared)
                 return None             # the request carries its whole prompt instead
-            blocks = self.alloc.alloc(need)
-            e = PrefixEntry(tokens=tokens, blocks=blocks, length=len(tokens))
+            blocks = shared + self.alloc.alloc(need - len(shared))
+            e = PrefixEntry(tokens=tokens, blocks=blocks, length=len(tokens), hashes=hashes,
+                            shared=len(shared))
             self.prefixes[tokens] = e
-            job = Sequence(None, list(tokens))
+            for i, h in enumerate(hashes):
+                self._block_index.setdefault(h, {})[tokens] = i
+            n_sh = len(shared) * BLOCK_SIZE
+            job = Sequence(None, list(tokens[n_sh:]))
             job.blocks = list(blocks)
+            job.num_cached = n_sh               # the shared blocks' keys are computed
             job.prefix_entry = e
             self.alloc.incref(blocks)          # the job's own reference
             self.waiting.insert(0, job)
+            self.stats["prefix_blocks"] = self.stats.get("prefix_blocks", 0) + need
+            self.stats["prefix_blocks_reused"] = self.stats.get("prefix_blocks_reused", 0) + len(shared)
         self._last_prefix = (src, e)
         return e
+
+    def _shared_blocks(self, tokens: tuple, hashes: tuple) -> List[int]:
+        """The leading full blocks of ``tokens`` that computed cached entries
+        already hold (longest run of matching chained hashes, tokens checked)."""
+        out = []
+        for i, h in enumerate(hashes):
+            holders = self._block_index.get(h)
+            src = None
+            for key in holders or ():
+                ent = self.prefixes.get(key)
+                if ent is not None and ent.computed and ent.tokens[:(i + 1) * BLOCK_SIZE] == \
+                        tokens[:(i + 1) * BLOCK_SIZE]:
+                    src = ent
+                    break
+            if src is None:
+                break
+            out.append(src.blocks[i])
+        # keep at least one token to compute: the prefix job must run a step
+        if out and len(out) * BLOCK_SIZE >= len(tokens):
+            out.pop()
+        return out
+
+    def _drop_entry(self, key: tuple) -> None:
+        """Forget one cached prefix: release its blocks (requests and other
+        entries sharing them keep theirs) and its block-index entries."""
+        e = self.prefixes.pop(key)
+        for h in e.hashes:
+            holders = self._block_index.get(h)
+            if holders is not None:
+                holders.pop(key, None)
+                if not holders:
+                    del self._block_index[h]
+        if self._last_prefix is not None and self._last_prefix[1] is e:
+            self._last_prefix = None
+        self.alloc.free(e.blocks)
 
     def _evict_prefixes(self, need: int) -> bool:
         """Drop cached prefix entries, least recently used first, until
@@ -238,9 +303,7 @@ class LLMEngine:
                 held = sum(1 for b in blocks if a.refcount(b) == 1)
                 if held == 0 or (only_unused and held < len(blocks)):
                     continue
-                if self._last_prefix is not None and self._last_prefix[1] is self.prefixes[key]:
-                    self._last_prefix = None
-                a.free(self.prefixes.pop(key).blocks)
+                self._drop_entry(key)
         return a.num_free >= need
 
     def _alloc_pressure(self, need: int, protect: set) -> Optional[List[int]]:
@@ -331,6 +394,7 @@ class LLMEngine:
         for e in self.prefixes.values():
             self.alloc.free(e.blocks)
         self.prefixes.clear()
+        self._block_index.clear()
         self._last_prefix = None
 
     def _materialize(self, seq: Sequence, copies: list):

@@ -573,3 +573,37 @@ def test_pool_pressure_releases_idle_prefix_holders_instead_of_failing():
     assert eng.stats.get("released", 0) > 0
     eng.drop_prefixes()
     assert eng.alloc.num_free == eng.kv.num_blocks
+
+
+def test_block_level_prefix_reuse_across_different_prefixes():
+    """prompts whose retrieved service lists start alike share
+    their leading full KV blocks.  A second prefix that extends the first one's
+    services reuses every full block of the first (its prefix job computes
+    only the rest, from the shared keys on), and greedy plans equal those of
+    an engine that recomputes every prefix (MCP_BLOCK_REUSE=0 semantics)."""
+    svc = sorted(synthetic_registry(12, seed=9), key=lambda r: r.name)   # registries list by name
+    lists = [svc[:6], svc[:6] + svc[8:11], svc[:4] + svc[6:9]]
+    out = []
+    for reuse in (False, True):
+        eng = LLMEngine(LlamaModel.random("tiny", "cpu", seed=1), num_blocks=256, max_batch=8,
+                        temperature=0.0, graphs=False)
+        eng.block_reuse = reuse
+        seqs = []
+        for i, cands in enumerate(lists):
+            reg = MemoryRegistry(cands)
+            pl = LocalPlanner(eng, reg, max_nodes=3)
+            dec, ptoks, stoks = pl.prepare(synthetic_intent(40 + i))
+            seqs.append(eng.submit(dec, stoks, prefix_tokens=ptoks))
+            eng.run()                         # each prefix computed before the next arrives
+        assert all(q.error is None for q in seqs)
+        out.append([q.result for q in seqs])
+        if reuse:
+            e0, e1, e2 = (eng.prefixes[k] for k in list(eng.prefixes)[:3])
+            assert e1.shared == e0.length // 64 and e1.blocks[:e1.shared] == e0.blocks[:e1.shared]
+            assert 0 < e2.shared < e0.length // 64
+            assert eng.stats["prefix_blocks_reused"] == e1.shared + e2.shared
+        else:
+            assert eng.stats.get("prefix_blocks_reused", 0) == 0
+        eng.drop_prefixes()
+        assert eng.alloc.num_free == eng.kv.num_blocks
+    assert out[0] == out[1]
