@@ -199,6 +199,8 @@ def qkv_rope(h, wqkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, 
     the shape (``qkv`` is then untouched scratch); otherwise GEMM + rope_kv.
     ``ss_in``: fused RMSNorm of the rows of ``h`` (see ``gemm_silu``)."""
     if h.is_cuda:
+        if _TRACE is not None:
+            _trace(h, wqkv, "qkv_rope")
         T = h.numel() // h.shape[-1]
         qkv = h.new_empty(T, wqkv.shape[0]) if qkv is None else qkv
         lib().qkv_rope(h, wqkv, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D,
