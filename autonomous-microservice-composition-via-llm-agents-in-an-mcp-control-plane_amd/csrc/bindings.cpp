@@ -217,6 +217,12 @@ void gemm_plan_set_flex_py(int64_t N, int64_t K, const std::vector<int64_t>& fle
   gemm_plan_set_flex((int)N, (int)K, c.data(), (int)c.size());
 }
 
+void gemm_plan_set_group_py(int64_t N, int64_t K, const std::vector<int64_t>& group) {
+  std::vector<int> c(group.begin(), group.end());
+  for (int v : c) TORCH_CHECK(v >= 0 && v <= 64, "gemm plan group must be 0..64");
+  gemm_plan_set_group((int)N, (int)K, c.data(), (int)c.size());
+}
+
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
   TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
@@ -660,6 +666,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_set_flex", &gemm_plan_set_flex_py,
         "measured flex tile per 64-row M bucket for one (N, K) (-1 = none; +32 = 4-stage form)");
   m.def("gemm_plan_flex", &gemm_plan_flex);
+  m.def("gemm_plan_set_group", &gemm_plan_set_group_py,
+        "measured tile group of the AGPR kernel per 64-row M bucket for one (N, K) (0 = default)");
+  m.def("gemm_plan_group", &gemm_plan_group);
+  m.def("gemm_group_force", &gemm_group_force, "AGPR kernel tile group: 0 = plan / default 4");
+  m.def("gemm256d_group", &gemm256d_group);
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_flex_count", &gemm_flex_count, "flex tile candidates (gemm(..., algo=16 + i))");
   m.def("gemm_flex_tiles", &gemm_flex_tiles, py::arg("cand"), py::arg("M"), py::arg("N"));

@@ -68,13 +68,13 @@ struct Frags {
   bf16x8 b[8];
 };
 
-// grouped tile order: GROUP M-tiles share each W column panel in L2
-DEV void tile_coords(int t, int nm, int nn, int bm, int& m0, int& n0) {
-  constexpr int GROUP = 4;
-  const int per_group = GROUP * nn;
+// grouped tile order: ``group`` M-tiles share each W column panel (a launch
+// argument: gemm256d_group picks it per shape)
+DEV void tile_coords(int t, int nm, int nn, int bm, int group, int& m0, int& n0) {
+  const int per_group = group * nn;
   const int g = t / per_group;
-  const int first_m = g * GROUP;
-  const int gsz = min(nm - first_m, GROUP);
+  const int first_m = g * group;
+  const int gsz = min(nm - first_m, group);
   m0 = (first_m + (t % per_group) % gsz) * bm;
   n0 = ((t % per_group) / gsz) * BN;
 }
@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
-                                                       int K, const RopeArgs ra, const NormEpi ne) {
+                                                       int K, int group, const RopeArgs ra,
+                                                       const NormEpi ne) {
   static_assert(BMT % 32 == 0 && BMT >= 128 && BMT <= 256, "tile height");
   constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (4..8)
   constexpr int WROWS = BMT / 2;                    // rows per wave (64..128)
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   int m0, n0;
   // grid = the first gridDim.x tiles of the grouped order (all of them, or the
   // full waves of a hybrid launch whose tail runs stream-K, gemm256sk.hip)
-  tile_coords(xcd_remap(blockIdx.x, gridDim.x), nm, nn, BMT, m0, n0);
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), nm, nn, BMT, group, m0, n0);
 
   // ---- LDS-DMA: instruction q of an operand fills rows 8q..8q+7,
   //      lane-linearly (row 8q + lane/8, LDS chunk lane%8, swizzled source
@@ -495,18 +496,37 @@ static int hybrid_tile0(int M, int N, int bm, int epi) {
   return (full > 0 && tail > 0 && 4 * tail <= g_cus) ? full : 0;
 }
 
+// Tile group (M-tiles per W panel in the grouped order).  4 was fixed from
+// warm-weight timings; a serving step streams cold weights, where sharing a
+// W panel across more M-tiles in one pass can read it from HBM fewer times.
+// gemm_group_force (tools) / MCP_GEMM_GROUP override; the plan's "group"
+// entry per M bucket otherwise, default 4.
+static int g_group_force = 0;
+void gemm_group_force(int g) { g_group_force = g; }
+int gemm256d_group(int M, int N, int K) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("MCP_GEMM_GROUP");
+    env = e ? atoi(e) : 0;
+  }
+  if (g_group_force > 0) return g_group_force;
+  if (env > 0) return env;
+  const int g = gemm_plan_group(M, N, K);
+  return g > 0 ? g : 4;
+}
+
 template <int BMT>
 static int launch_height(const void* X, const void* W, void* Y, const void* R, int M, int N,
-                         int K, int epi, dim3 grid, const RopeArgs& ra, hipStream_t s) {
+                         int K, int epi, dim3 grid, int group, const RopeArgs& ra, hipStream_t s) {
   auto x = (const bf16*)X;
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
   switch (epi) {
-    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra, norm_epi()); return 0;
-    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, ra, norm_epi()); return 0;
-    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra, norm_epi()); return 0;
-    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, ra, norm_epi()); return 0;
+    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;
+    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
     default: return 2;
   }
 }
@@ -524,19 +544,21 @@ static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R
     if (!g_cus) gemm256d_waves_bm(M, N, K, 256);
     if (2 * nm * nn <= g_cus) return launch_gemm_tn_256sk_tail(X, W, Y, R, M, N, K, epi, 0, s);
   }
-  const int tile0 = hybrid_tile0(M, N, bm, epi);
+  const int group = gemm256d_group(M, N, K);
+  // the stream-K tail kernel walks the tiles in the group-4 order
+  const int tile0 = group == 4 ? hybrid_tile0(M, N, bm, epi) : 0;
   const dim3 grid(tile0 > 0 ? tile0 : nm * nn);
   if (tile0 > 0) {
     // full waves first (same stream: the tail starts when they are done)
-    if (const int rc = launch_height<256>(X, W, Y, R, M, N, K, epi, grid, ra, s)) return rc;
+    if (const int rc = launch_height<256>(X, W, Y, R, M, N, K, epi, grid, group, ra, s)) return rc;
     return launch_gemm_tn_256sk_tail(X, W, Y, R, M, N, K, epi, tile0, s);
   }
   switch (bm) {
-    case 256: return launch_height<256>(X, W, Y, R, M, N, K, epi, grid, ra, s);
-    case 224: return launch_height<224>(X, W, Y, R, M, N, K, epi, grid, ra, s);
-    case 192: return launch_height<192>(X, W, Y, R, M, N, K, epi, grid, ra, s);
-    case 160: return launch_height<160>(X, W, Y, R, M, N, K, epi, grid, ra, s);
-    case 128: return launch_height<128>(X, W, Y, R, M, N, K, epi, grid, ra, s);
+    case 256: return launch_height<256>(X, W, Y, R, M, N, K, epi, grid, group, ra, s);
+    case 224: return launch_height<224>(X, W, Y, R, M, N, K, epi, grid, group, ra, s);
+    case 192: return launch_height<192>(X, W, Y, R, M, N, K, epi, grid, group, ra, s);
+    case 160: return launch_height<160>(X, W, Y, R, M, N, K, epi, grid, group, ra, s);
+    case 128: return launch_height<128>(X, W, Y, R, M, N, K, epi, grid, group, ra, s);
     default: return 4;
   }
 }

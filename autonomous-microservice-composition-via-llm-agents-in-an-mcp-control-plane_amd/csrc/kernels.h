@@ -46,6 +46,10 @@ int launch_gemm_flex(const void* X, const void* W, void* Y, const void* R, int M
 int gemm_flex_count();
 void gemm_plan_set_flex(int N, int K, const int* flex, int n);
 int gemm_plan_flex(int M, int N, int K);
+void gemm_plan_set_group(int N, int K, const int* group, int n);
+int gemm_plan_group(int M, int N, int K);   // 0 = none recorded
+void gemm_group_force(int g);               // AGPR kernel tile group: 0 = plan / default
+int gemm256d_group(int M, int N, int K);
 int gemm_flex_tiles(int cand, int M, int N);
 struct RopeArgs {
   const int* pos;          // [T] positions
