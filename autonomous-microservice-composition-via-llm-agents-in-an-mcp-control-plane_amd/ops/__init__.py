@@ -335,11 +335,13 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
             # and contexts) runs the work-list split launch below instead
             # (profiles/attention_decode_r3.jsonl).  A hipGraph step's lists are
             # padded to the key's capacity (52 items at the smallest key), so
-            # the rule would always reject it there; a split key is only chosen
-            # for fewer than num_cus / Hkv real items (batch.choose_kv_splits)
-            # and its padding items exit at once: graph steps take the decode
-            # kernel (config 2 p50 99.1 -> 94.3 ms, config 5 at 20 / 40
-            # intents/s equal, profiles/attention_decode_graph_ab.jsonl)
+            # the rule would always reject it there; a split key is chosen only
+            # while the real items stay under 2 x CUs of work
+            # (batch.choose_kv_splits, work factor 2) and the padding items
+            # exit at once: graph steps take the decode kernel (config 2 p50
+            # 99.1 -> 94.3 ms, config 5 at 20 / 40 intents/s equal,
+            # profiles/attention_decode_graph_ab.jsonl); its cascade folds are
+            # checked against fp32 (test_decode_kernel_cascade_fold)
             use_dec = _DECODE_FORCE or getattr(meta, "padded", False) or (
                 (4 * ws4.numel() + ws1.numel()) * k_cache.shape[1] * nz
                 <= _DECODE_BLOCKS_PER_CU * _num_cus(q.device))

@@ -410,6 +410,56 @@ def test_cascade_prefix_attention(Hq, Hkv, kv_splits, prefix_split, concurrent, 
     assert rel_err(out, exp) < 2e-2
 
 
+@pytest.mark.parametrize("own_keys,q_lens", [([5], [1]), ([40, 60], [3, 1]),
+                                              ([70], [4]), ([300, 130, 64], [1, 9, 2])])
+def test_decode_kernel_cascade_fold(own_keys, q_lens, monkeypatch):
+    """the decode kernel (attention_decode.hip, forced, as
+    graph-replayed split steps take it) with cascade inputs - every sequence
+    after a 640-key shared prefix (kv_begin), the prefix partial (pre_o /
+    pre_lse) folded in - against fp32 full attention: own key spans of one
+    block (the single-block fold, nact == 1) and of several blocks (the
+    last-arriver fold)."""
+    monkeypatch.setattr(ops, "_DECODE_SPLIT", True)
+    monkeypatch.setattr(ops, "_DECODE_FORCE", True)
+    monkeypatch.setenv("MCP_ATTN_CONCURRENT", "0")
+    torch.manual_seed(31)
+    Hq, Hkv, D, BS, P_full = 32, 8, 128, 64, 640
+    ctx = [P_full + k for k in own_keys]
+    n_pre = P_full // BS
+    own_blocks = [(k + BS - 1) // BS for k in own_keys]
+    nb = n_pre + sum(own_blocks) + 2
+    kc, vc = _cache(nb, Hkv)
+    pre = list(range(n_pre))
+    o = n_pre
+    tables = []
+    for nbk in own_blocks:
+        tables.append(pre + list(range(o, o + nbk)))
+        o += nbk
+    bt = np.zeros((len(q_lens), max(len(t) for t in tables)), np.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = t
+    T = sum(q_lens)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    qs = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    step = StepInputs(token_ids=np.zeros(T, np.int32), positions=np.zeros(T, np.int32),
+                      slots=np.zeros(T, np.int32), q_start=qs,
+                      q_len=np.asarray(q_lens, np.int32), ctx_len=np.asarray(ctx, np.int32),
+                      block_table=bt, logit_rows=np.zeros(0, np.int32),
+                      kv_begin=np.full(len(q_lens), P_full, np.int32),
+                      pre_bt=np.asarray(pre, np.int32), pre_tokens=T)
+    dev = pack(step, Hq // Hkv, DEV)
+    dev.attn.kv_splits = 2
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), torch.from_numpy(qs),
+                              torch.tensor(q_lens), torch.tensor(ctx), torch.from_numpy(bt),
+                              1 / math.sqrt(D))
+    outs = []
+    for _ in range(2):                                  # the arrival tickets re-arm
+        out = ops.paged_attention(q, kc, vc, dev.attn, 1 / math.sqrt(D)).cpu()
+        assert rel_err(out, exp) < 2e-2, (own_keys, q_lens)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 8)])
 @pytest.mark.parametrize("T", [1, 77, 300])
 @pytest.mark.parametrize("rt", ["1", "2", "4"])
