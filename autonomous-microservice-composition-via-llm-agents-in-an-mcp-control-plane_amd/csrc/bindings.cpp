@@ -223,6 +223,12 @@ void gemm_plan_set_group_py(int64_t N, int64_t K, const std::vector<int64_t>& gr
   gemm_plan_set_group((int)N, (int)K, c.data(), (int)c.size());
 }
 
+void gemm_plan_set_persist_py(int64_t N, int64_t K, const std::vector<int64_t>& persist) {
+  std::vector<int> c(persist.begin(), persist.end());
+  for (int v : c) TORCH_CHECK(v == 0 || v == 1, "gemm plan persist must be 0 or 1");
+  gemm_plan_set_persist((int)N, (int)K, c.data(), (int)c.size());
+}
+
 void gemm_f32out(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_DEV(Y); CHECK_CONTIG(Y);
   TORCH_CHECK(Y.scalar_type() == at::kFloat, "Y must be f32");
@@ -671,6 +677,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_group", &gemm_plan_group);
   m.def("gemm_group_force", &gemm_group_force, "AGPR kernel tile group: 0 = plan / default 4");
   m.def("gemm256d_group", &gemm256d_group);
+  m.def("gemm_plan_set_persist", &gemm_plan_set_persist_py,
+        "per 64-row M bucket for one (N, K): 1 = the persistent AGPR kernel measured faster");
+  m.def("gemm_plan_persist", &gemm_plan_persist);
+  m.def("gemm_persist_force", &gemm_persist_force,
+        "persistent AGPR GEMM: -1 plan / MCP_GEMM_PERSIST, 0 off, 1 when tiles > CUs, 2 always");
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_flex_count", &gemm_flex_count, "flex tile candidates (gemm(..., algo=16 + i))");
   m.def("gemm_flex_tiles", &gemm_flex_tiles, py::arg("cand"), py::arg("M"), py::arg("N"));

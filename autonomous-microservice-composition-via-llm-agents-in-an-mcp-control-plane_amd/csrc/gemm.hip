@@ -251,6 +251,7 @@ struct GemmPlan {
   std::vector<signed char> split;    // measured split-K of the 128^2 path (0: the rule)
   std::vector<signed char> flex;     // measured flex tile (gemm_flex.hip) or -1
   std::vector<signed char> group;    // measured tile group of the AGPR kernel (0: default)
+  std::vector<signed char> persist;  // 1: the persistent AGPR kernel (gemm256p.hip) measured faster
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -262,7 +263,7 @@ void gemm_plan_set(int N, int K, const int* codes, int n) {
       p.code = std::move(c);
       return;
     }
-  g_plans.push_back({N, K, std::move(c), {}, {}, {}});
+  g_plans.push_back({N, K, std::move(c), {}, {}, {}, {}});
 }
 
 void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
@@ -271,7 +272,7 @@ void gemm_plan_set_splits(int N, int K, const int* splits, int n) {
       p.split.assign(splits, splits + n);
       return;
     }
-  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n), {}, {}});
+  g_plans.push_back({N, K, {}, std::vector<signed char>(splits, splits + n), {}, {}, {}});
 }
 
 void gemm_plan_set_flex(int N, int K, const int* flex, int n) {
@@ -280,7 +281,7 @@ void gemm_plan_set_flex(int N, int K, const int* flex, int n) {
       p.flex.assign(flex, flex + n);
       return;
     }
-  g_plans.push_back({N, K, {}, {}, std::vector<signed char>(flex, flex + n), {}});
+  g_plans.push_back({N, K, {}, {}, std::vector<signed char>(flex, flex + n), {}, {}});
 }
 
 void gemm_plan_set_group(int N, int K, const int* group, int n) {
@@ -289,7 +290,25 @@ void gemm_plan_set_group(int N, int K, const int* group, int n) {
       p.group.assign(group, group + n);
       return;
     }
-  g_plans.push_back({N, K, {}, {}, {}, std::vector<signed char>(group, group + n)});
+  g_plans.push_back({N, K, {}, {}, {}, std::vector<signed char>(group, group + n), {}});
+}
+
+void gemm_plan_set_persist(int N, int K, const int* persist, int n) {
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.persist.assign(persist, persist + n);
+      return;
+    }
+  g_plans.push_back({N, K, {}, {}, {}, {}, std::vector<signed char>(persist, persist + n)});
+}
+
+int gemm_plan_persist(int M, int N, int K) {
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.persist.size() ? p.persist[b] : 0;
+    }
+  return 0;
 }
 
 // measured tile group of the AGPR kernel for this M bucket (0 = none recorded)

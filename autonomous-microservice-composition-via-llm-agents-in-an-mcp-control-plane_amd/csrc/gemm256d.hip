@@ -531,11 +531,29 @@ static int launch_height(const void* X, const void* W, void* Y, const void* R, i
   }
 }
 
+// Persistent form (gemm256p.hip): -1 = plan / MCP_GEMM_PERSIST, 0 = off,
+// 1 = whenever the tiles exceed one wave of workgroups, 2 = always
+static int g_persist_force = -1;
+void gemm_persist_force(int p) { g_persist_force = p; }
+int gemm256d_persist(int M, int N, int K, int tiles) {
+  static int env = -2;
+  if (env == -2) {
+    const char* e = getenv("MCP_GEMM_PERSIST");
+    env = e ? atoi(e) : -1;
+  }
+  int mode = g_persist_force >= 0 ? g_persist_force : env;
+  if (mode < 0) mode = gemm_plan_persist(M, N, K) ? 1 : 0;
+  if (!g_cus) gemm256d_waves_bm(M, N, K, 256);
+  return mode == 2 || (mode == 1 && tiles > g_cus);
+}
+
 static int launch_256d_impl(const void* X, const void* W, void* Y, const void* R, int M, int N,
                             int K, int epi, int bm, const RopeArgs& ra, hipStream_t s) {
   if (const int rc = gemm256d_ok(M, N, K)) return rc;
   if (bm == 0) bm = gemm256d_height(M, N, K);
   const int nm = (M + bm - 1) / bm, nn = (N + BN - 1) / BN;
+  if (gemm256d_persist(M, N, K, nm * nn))
+    return launch_gemm_tn_256p(X, W, Y, R, M, N, K, epi, bm, g_cus, gemm256d_group(M, N, K), ra, s);
   // at most half the CUs' worth of 256-row tiles: the whole product runs
   // stream-K (every tile over >= 2 workgroups, last arriver sums the slabs)
   // instead of leaving half the chip idle (MCP_GEMM_SK_SMALL=0 disables)

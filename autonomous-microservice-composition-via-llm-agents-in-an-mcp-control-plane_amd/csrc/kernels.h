@@ -50,6 +50,14 @@ void gemm_plan_set_group(int N, int K, const int* group, int n);
 int gemm_plan_group(int M, int N, int K);   // 0 = none recorded
 void gemm_group_force(int g);               // AGPR kernel tile group: 0 = plan / default
 int gemm256d_group(int M, int N, int K);
+void gemm_plan_set_persist(int N, int K, const int* persist, int n);
+int gemm_plan_persist(int M, int N, int K);  // 1 = the persistent AGPR kernel measured faster
+void gemm_persist_force(int p);             // -1 plan / env, 0 off, 1 multi-wave, 2 always
+int gemm256d_persist(int M, int N, int K, int tiles);
+struct RopeArgs;
+// gemm256p.hip: persistent AGPR GEMM (grid = min(tiles, cus))
+int launch_gemm_tn_256p(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                        int epi, int bm, int cus, int group, const RopeArgs& ra, hipStream_t s);
 int gemm_flex_tiles(int cand, int M, int N);
 struct RopeArgs {
   const int* pos;          // [T] positions

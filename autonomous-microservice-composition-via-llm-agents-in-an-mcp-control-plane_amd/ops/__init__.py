@@ -73,6 +73,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
             mod.gemm_plan_set_flex(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["flex"]])
         if "group" in sh and hasattr(mod, "gemm_plan_set_group"):
             mod.gemm_plan_set_group(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["group"]])
+        if "persist" in sh and hasattr(mod, "gemm_plan_set_persist"):
+            mod.gemm_plan_set_persist(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["persist"]])
     return len(plan["shapes"])
 
 
