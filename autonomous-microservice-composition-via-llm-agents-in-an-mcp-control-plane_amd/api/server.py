@@ -29,7 +29,7 @@ from typing import Optional
 
 import httpx
 from fastapi import FastAPI, HTTPException
-from fastapi.responses import JSONResponse, PlainTextResponse
+from fastapi.responses import JSONResponse, PlainTextResponse, Response
 from pydantic import BaseModel
 
 from ..config import Settings
@@ -157,9 +157,12 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
 
     @app.post("/plan", response_model=PlanResponse)
     async def plan_intent(req: PlanRequest):
-        resp = PlanResponse(graph=await _plan(req.intent))
+        resp = PlanResponse(graph=await _plan(req.intent))   # a non-object plan -> 500 (T8)
         if not req.explain:
-            return resp
+            # the validated model serialised once, straight into the response:
+            # FastAPI's response_model pass would validate and encode it again
+            # (~1/4 of the API process's time per plan at thousands of plans/s)
+            return Response(resp.__pydantic_serializer__.to_json(resp), media_type="application/json")
         try:
             text = _explain(resp.graph)
         except Exception as e:     # a plan the orchestrator would reject (T2 / cycle)
