@@ -133,6 +133,8 @@ def _replica_main(idx: int, device: str, cfg: ReplicaConfig, records: list, vers
     retriever = SchemaIndex(registry, dim=cfg.embed_dim, device=device)
     retriever.refresh()
     retriever.start_background()
+    from ..utils.heap import settle as settle_heap
+    settle_heap()                          # start-up heap -> permanent GC generation
     from ..planner.tokenizer import tokenizer_for
     planner = LocalPlanner(eng, registry, tokenizer=tokenizer_for(cfg.model),
                            max_nodes=cfg.max_nodes, min_nodes=cfg.min_nodes, retriever=retriever,

@@ -26,6 +26,7 @@ import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
+from ..utils.heap import settle as settle_heap
 from ..utils.metrics import METRICS
 from .base import Planner
 from .grammar import GrammarSpec
@@ -97,9 +98,11 @@ class LocalPlanner(Planner):
         if tok.vocab_size > model.cfg.vocab_size:
             raise ValueError(f"tokenizer vocabulary {tok.vocab_size} exceeds the model's "
                              f"{model.cfg.vocab_size}")
-        return cls(eng, registry, tokenizer=tok, max_nodes=settings.max_nodes,
-                   min_nodes=getattr(settings, "min_nodes", 1), retriever=retr,
-                   retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
+        planner = cls(eng, registry, tokenizer=tok, max_nodes=settings.max_nodes,
+                      min_nodes=getattr(settings, "min_nodes", 1), retriever=retr,
+                      retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
+        settle_heap()                      # start-up heap -> permanent GC generation
+        return planner
 
     # ----------------------------------------------------------- prepare
     # retrieved services go into the prompt in name order (MCP_RETRIEVAL_ORDER=

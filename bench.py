@@ -119,6 +119,7 @@ def main():
     from mcp_amd.planner.local import LocalPlanner
     from mcp_amd.planner.prompt import synthetic_intent
     from mcp_amd.registry import MemoryRegistry, synthetic_registry
+    from mcp_amd.utils.heap import settle as settle_heap
 
     t0 = time.time()
     model = LlamaModel.random(args.model, dev, seed=args.seed)
@@ -153,6 +154,7 @@ def main():
     for w in range(args.warmup):
         _, dt, toks = one_step(-1 - w)
         log(f"[rank {rank}] warmup {w}: {dt * 1e3:.0f} ms, {toks} tokens")
+    settle_heap()                  # as a server does once it is up (utils/heap.py)
     cap0 = engine.stats.get("graph_captures", 0)
     seqs_all = []
     if world > 1:

@@ -235,6 +235,8 @@ def main():
     ncap = engine.warm_graphs(contexts=(2048,))            # server start-up: capture the buckets
     warm_s = time.perf_counter() - t_w
     planner.plan_many([synthetic_intent(-1 - i) for i in range(max(1, args.warmup))])
+    from mcp_amd.utils.heap import settle as settle_heap
+    settle_heap()                                          # as the server does after start-up
 
     out = {"n_gpus": world, "model": args.model, "services": args.services, "dtype": "bf16",
            "data": "synthetic intents, random-init weights",
