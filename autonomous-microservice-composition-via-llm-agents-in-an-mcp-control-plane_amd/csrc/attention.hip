@@ -44,6 +44,28 @@ DEV bf16x4 tr_read(const bf16* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
+// Block-table entries of a key walk, 64 tiles per VGPR (lane i: tile base + i),
+// read back with v_readlane.  Reading bt[kt + 1] inside the loop put a global
+// load and its vmcnt(0) in front of every tile's DMA: two dependent memory
+// round trips per key tile (table entry, then K / V) instead of one.  One
+// load per 64 tiles, issued before the first DMA.
+struct BtLanes {
+  const int* bt;
+  int end, base, v;
+  DEV BtLanes(const int* bt_, int kt0, int end_) : bt(bt_), end(end_), base(kt0) { fill(); }
+  DEV void fill() {
+    const int i = base + (int)(threadIdx.x & 63);
+    v = i < end ? bt[i] : 0;
+  }
+  DEV int operator()(int kt) {         // kt uniform, non-decreasing, < end
+    if (kt - base >= 64) {
+      base = kt;
+      fill();
+    }
+    return __builtin_amdgcn_readlane(v, kt - base);
+  }
+};
+
 struct AttnArgs {
   const bf16* q;
   const bf16* kc;
@@ -288,8 +310,9 @@ void attn_kernel(const AttnArgs a) {
 
   // staging: piece p covers rows 4p..4p+3 of the K (p<16) or V (p>=16) tile
   const int srow = lane >> 4;
+  BtLanes bt_at(bt, kt0, ntiles);
   auto stage = [&](int kt, int buf) {
-    const size_t blk = (size_t)bt[kt];
+    const size_t blk = (size_t)bt_at(kt);
     const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
     const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
@@ -505,8 +528,9 @@ void attn_prefix_kernel(const AttnArgs a) {
   }
 
   const int srow = lane >> 4;
+  BtLanes bt_at(a.pre_bt, 0, ntiles);
   auto stage = [&](int kt, int buf) {
-    const size_t blk = (size_t)a.pre_bt[kt];
+    const size_t blk = (size_t)bt_at(kt);
     const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
     const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
