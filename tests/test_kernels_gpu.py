@@ -960,3 +960,38 @@ def test_fused_norm_qkv_fallback_rope_kv(monkeypatch):
     ops.qkv_rope(x, W, pos, slots, cs, q, kc, vc, Hq, Hkv, D, ss_in=ss, eps=eps)
     assert rel_err(q.cpu(), qr) < 2e-2
     assert rel_err(kc.cpu(), kr) < 2e-2 and rel_err(vc.cpu(), vr) < 2e-2
+
+
+@pytest.mark.parametrize("ring", ["2", "3"])
+@pytest.mark.parametrize("P", [64, 128, 192, 640, 4096, 4160])
+def test_prefix_pass_dma_ring(P, ring, monkeypatch):
+    """The 8-wave prefix pass in both DMA rings (2 = double buffer through the
+    builtin, 3 = 3-deep ring with hand-counted waits on inline-asm DMAs) at 1,
+    2, 3, 10 and 64 key tiles, and at 65 tiles (past one VGPR of block-table
+    entries: the 3-deep form defers to the double buffer, whose table cache
+    refills) against fp32 softmax attention, with a shuffled block table."""
+    monkeypatch.setenv("MCP_ATTN_PREFIX_RT", "2")
+    monkeypatch.setenv("MCP_ATTN_PREFIX_NW", "8")
+    monkeypatch.setenv("MCP_ATTN_PREFIX_RING", ring)
+    torch.manual_seed(13)
+    Hq, Hkv, D, T = 32, 8, 128, 150
+    n_pre = P // 64
+    kc, vc = _cache(n_pre + 2, Hkv)
+    kc = (kc.float() * (1 + torch.arange(n_pre + 2, device=DEV).view(-1, 1, 1, 1) % 5)).bfloat16()
+    pre_bt = (torch.randperm(n_pre + 2, device=DEV)[:n_pre]).to(torch.int32)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    out = torch.empty_like(q)
+    lse = torch.empty(T, Hq, device=DEV, dtype=torch.float32)
+    scale = 1 / math.sqrt(D)
+    ops.lib().prefix_attention(q, kc, vc, out, lse, pre_bt, P, T, scale)
+    G = Hq // Hkv
+    k = kc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    v = vc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    s = torch.einsum("thgd,hpd->thgp", q.float().view(T, Hkv, G, D), k) * scale
+    exp_o = torch.einsum("thgp,hpd->thgd", torch.softmax(s, -1), v).reshape(T, Hq, D)
+    exp_lse = (torch.logsumexp(s, -1) / math.log(2)).reshape(T, Hq)
+    assert rel_err(out, exp_o) < 2e-2
+    assert torch.allclose(lse, exp_lse, atol=5e-2, rtol=1e-3)
+    again = torch.empty_like(q)
+    ops.lib().prefix_attention(q, kc, vc, again, lse, pre_bt, P, T, scale)
+    assert torch.equal(out, again)
