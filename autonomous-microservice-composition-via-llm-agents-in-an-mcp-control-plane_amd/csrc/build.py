@@ -93,8 +93,23 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
               str(KERNELS_SO), f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip",
               "-ltorch_hip", "-ltorch_python", "-L/opt/rocm/lib", "-lrccl", f"-Wl,-rpath,{tlib}",
               "-Wl,-rpath,/opt/rocm/lib"], verbose)
+    _check_stubs(KERNELS_SO)
     build_runtime(force, verbose)
     return KERNELS_SO
+
+
+def _check_stubs(so: Path) -> None:
+    """Fail the build when a kernel's host launch stub is missing from the
+    library: hipcc's host pass silently drops the stub of a kernel whose body
+    it rejects (e.g. a class local to the kernel used by its lambdas), and the
+    library then fails only at load time on the GPU box."""
+    nm = shutil.which("nm")
+    if not nm:
+        return
+    r = subprocess.run([nm, "-D", "--undefined-only", str(so)], capture_output=True, text=True)
+    missing = [ln.split()[-1] for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        raise RuntimeError(f"{so.name}: {len(missing)} kernel launch stubs undefined, e.g. {missing[0]}")
 
 
 def build_runtime(force: bool = False, verbose: bool = False) -> Path | None:

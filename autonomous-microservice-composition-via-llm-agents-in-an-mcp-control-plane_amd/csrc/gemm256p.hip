@@ -96,6 +96,17 @@ DEV void waitcnt_vm_lgkm0() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
 }
 
+// per-tile DMA state: X row offsets (clamped rows) and the first W row
+// (vector-typed so it stays in registers: an array member whose address a
+// select could take goes to scratch).  At namespace scope: a class local to
+// the kernel, used by the kernel's lambdas, leaves hipcc's host pass without
+// the kernel's launch stub (undefined symbol at load time).
+typedef __attribute__((ext_vector_type(8))) unsigned u32x8;
+struct TileDma {
+  u32x8 offA;
+  int rowB0;
+};
+
 template <int EPI, int BMT>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
@@ -129,14 +140,6 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
   const unsigned offB = (unsigned)(((lane >> 3) * K + chunk * 8) * 2);
   const int nt = K / BK;                             // >= 2, even (launcher)
 
-  // per-tile DMA state: X row offsets (clamped rows) and the first W row
-  // (vector-typed so the two copies stay in registers: an array member whose
-  // address the current / next select could take goes to scratch)
-  typedef __attribute__((ext_vector_type(8))) unsigned u32x8;
-  struct TileDma {
-    u32x8 offA;
-    int rowB0;
-  };
   auto tile_dma = [&](int m0, int n0, TileDma& d) {
 #pragma unroll
     for (int q = 0; q < QA; ++q)
@@ -426,8 +429,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+}  // namespace
+
+// (outside the anonymous namespace, as gemm256d.hip's launch_height: a kernel
+// template launched from a launcher template inside it gets no host stub)
 template <int BMT>
-int launch_p_height(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+static int launch_p_height(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                     int epi, int grid, int group, const RopeArgs& ra, hipStream_t s) {
   auto x = (const bf16*)X;
   auto w = (const bf16*)W;
@@ -441,8 +448,6 @@ int launch_p_height(const void* X, const void* W, void* Y, const void* R, int M,
     default: return 2;
   }
 }
-
-}  // namespace
 
 // Persistent AGPR GEMM: grid = min(tiles, CUs) workgroups, each walking tiles
 // blockIdx.x + k * grid.  Same shape rules as gemm256d_ok (K % 128 == 0,
