@@ -493,31 +493,14 @@ void attn_kernel(const AttnArgs a) {
 // no mask (pre_keys is a multiple of 64).  Same row layout, online softmax,
 // swizzled double-buffered LDS-DMA ring and outputs (normalised O + LSE) as
 // MODE 1; the key-split form for few tokens stays on attn_kernel.
-//
-// NB = 3 (8-wave blocks, which run one per CU at 234 VGPRs anyway): a 3-deep
-// ring, tile kt + 2's DMA issued at the top of step kt, one barrier per tile.
-// The DMAs are inline asm, invisible to hipcc's wait-count pass: through the
-// builtin, hipcc puts vmcnt(0) in front of every transposed V read (the
-// builtin carries no alias information), which waits for the DMA issued at the
-// top of the same step and makes every key tile pay a full memory round trip.
-// The waits are counted by hand (each wave's 4 DMAs of a tile; vmcnt retires
-// in issue order, so the compiler's own waits on its loads stay correct, only
-// stricter).  hipcc itself never writes M0 in this kernel (no builtin DMA,
-// no indexed register access), so setting it inside the asm is safe.
-DEV void glds16_asm(const void* gptr, unsigned lds_byte_addr) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-               :: "s"(lds_byte_addr), "v"(gptr) : "memory");
-}
-
-template <int NW, int G, int RT, int NB = 2>
+template <int NW, int G, int RT>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(RT >= 4 ? 1 : 2)))
 void attn_prefix_kernel(const AttnArgs a) {
   constexpr int TPT = 16 / G;                 // tokens per 16-row tile
   constexpr int QT = NW * RT * TPT;           // tokens per block
   constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
   static_assert(PIECES % NW == 0, "pieces split evenly");
-  static_assert(NB == 2 || (NB == 3 && NW == 8), "3-deep ring: 8-wave blocks (4 DMAs per wave)");
-  __shared__ __attribute__((aligned(16))) bf16 smem[NB * 2 * TILE];   // [buf][K|V][64][128]
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];   // [buf][K|V][64][128]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kvh = a.head_major ? blockIdx.x : blockIdx.y;
@@ -546,13 +529,8 @@ void attn_prefix_kernel(const AttnArgs a) {
 
   const int srow = lane >> 4;
   BtLanes bt_at(a.pre_bt, 0, ntiles);
-  // NB = 3: at most 64 tiles (the dispatcher checks), one VGPR of table
-  // entries and no refill branch in the loop (its load would make hipcc wait
-  // for every DMA in flight before the next one)
-  const int btv = NB == 3 && lane < ntiles ? a.pre_bt[lane] : 0;
-  const unsigned lds0 = (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)(void*)smem);
   auto stage = [&](int kt, int buf) {
-    const size_t blk = (size_t)(NB == 3 ? __builtin_amdgcn_readlane(btv, kt) : bt_at(kt));
+    const size_t blk = (size_t)bt_at(kt);
     const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
     const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
@@ -562,13 +540,7 @@ void attn_prefix_kernel(const AttnArgs a) {
       const int tile = p >> 4, pr = p & 15;
       const int row = pr * 4 + srow;
       const int chunk = (lane & 15) ^ (row & 15);
-      const bf16* src = (tile ? vb : kb) + row * D + chunk * 8;
-      if constexpr (NB == 3) {
-        const unsigned dst = lds0 + (unsigned)((buf * 2 * TILE + tile * TILE + pr * 512) * 2);
-        glds16_asm(src, __builtin_amdgcn_readfirstlane(dst));
-      } else {
-        glds16(src, base + tile * TILE + pr * 512);
-      }
+      glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
     }
   };
 
@@ -583,29 +555,11 @@ void attn_prefix_kernel(const AttnArgs a) {
   }
 
   if (ntiles > 0) stage(0, 0);
-  if constexpr (NB == 3) {
-    if (ntiles > 1) stage(1, 1);
-  } else {
-    __syncthreads();
-  }
+  __syncthreads();
   const int tq = (lane & 15) >> 2, tp = lane & 3;
   for (int kt = 0; kt < ntiles; ++kt) {
-    int cur;
-    if constexpr (NB == 3) {
-      // this wave's DMAs of tile kt have landed (tile kt + 1's 4 may still
-      // fly); the barrier makes every wave's pieces visible and retires every
-      // wave's reads of tile kt - 1, whose buffer tile kt + 2 now refills
-      if (kt + 1 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      cur = kt % 3;
-      if (kt + 2 < ntiles) stage(kt + 2, cur == 0 ? 2 : cur - 1);
-    } else {
-      cur = kt & 1;
-      if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
-    }
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
     const bf16* Kl = smem + cur * 2 * TILE;
     const bf16* Vl = Kl + TILE;
 
@@ -670,7 +624,7 @@ void attn_prefix_kernel(const AttnArgs a) {
         for (int r = 0; r < RT; ++r) o[r][dt] = mfma16x16x32(vf, pf[r][k2], o[r][dt]);
       }
     }
-    if constexpr (NB == 2) __syncthreads();   // its fence also drains the next tile's LDS-DMA
+    __syncthreads();             // its fence also drains the next tile's LDS-DMA
   }
 
   // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + e]
@@ -920,16 +874,10 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
       const int nblk = (a.pre_tokens + qt - 1) / qt;
       return a.head_major ? dim3(a.Hkv, nblk) : dim3(nblk, a.Hkv);
     };
-    // MCP_ATTN_PREFIX_RING: 3 (default) = the 8-wave form's 3-deep ring with
-    // hand-counted DMA waits, 2 = the double-buffered form (A/B; read per launch)
-    const char* ring_env = getenv("MCP_ATTN_PREFIX_RING");
-    const int ring = ring_env ? atoi(ring_env) : 3;
     if (rt == 4)
       attn_prefix_kernel<4, G, 4><<<grid_for(4 * 4 * (16 / G)), 256, 0, s>>>(a);
     else if (prefix_nw(a.pre_tokens, 8 * 2 * (16 / G), a.Hkv) == 4)
       attn_prefix_kernel<4, G, 2><<<grid_for(4 * 2 * (16 / G)), 256, 0, s>>>(a);
-    else if (ring == 3 && a.pre_keys <= 64 * KT)
-      attn_prefix_kernel<8, G, 2, 3><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     else
       attn_prefix_kernel<8, G, 2><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     return;

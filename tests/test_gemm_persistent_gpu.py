@@ -5,7 +5,8 @@ QKV + RoPE + paged K/V write.  Shapes give several tiles per workgroup (the
 next tile's operands prefetched by the previous one, stores drained under the
 next mainloop), a last M tile that is partial (range-checked stores), and a
 grid smaller than the CU count.  Repeated runs are bitwise equal, and the
-residual statistic equals the one-tile kernel's bit for bit."""
+residual statistic equals the one-tile kernel's bit for bit (tile heights
+below 256 rows, whose one-tile dispatch has no stream-K form)."""
 import math
 
 import pytest
@@ -56,13 +57,16 @@ def test_persistent_plain_and_residual(M, N, K, persist):
         assert rel_err(y, exp_r) < 1e-2, code
         e_ss = y.double().pow(2).sum(-1) * ref.SS_FIX
         assert ((ss.double() - e_ss).abs() / e_ss).max().item() < 1e-5, code
-        # the same statistic as the one-tile kernel, bit for bit
+        # the same result and statistic as the one-tile kernel, bit for bit
+        # (256-row tiles excepted: that dispatch sends small grids and tail
+        # waves through the stream-K kernel, another summation order)
         L.gemm_persist_force(0)
         y1 = R.clone()
         ss1 = torch.zeros(M, dtype=torch.int64, device=DEV)
         ops.gemm(X, W, R=y1, out=y1, ss_out=ss1)
         L.gemm_persist_force(2)
-        assert torch.equal(y, y1) and torch.equal(ss, ss1), code
+        if code != 1:
+            assert torch.equal(y, y1) and torch.equal(ss, ss1), code
 
 
 @pytest.mark.parametrize("M", [700, 2600])

@@ -962,19 +962,15 @@ def test_fused_norm_qkv_fallback_rope_kv(monkeypatch):
     assert rel_err(kc.cpu(), kr) < 2e-2 and rel_err(vc.cpu(), vr) < 2e-2
 
 
-@pytest.mark.parametrize("ring", ["2", "3"])
 @pytest.mark.parametrize("P", [64, 128, 192, 640, 4096, 4160])
-def test_prefix_pass_dma_ring(P, ring, monkeypatch):
-    """The 8-wave prefix pass in both DMA rings (2 = double buffer through the
-    builtin, 3 = 3-deep ring with hand-counted waits on inline-asm DMAs) at 1,
-    2, 3, 10 and 64 key tiles, and at 65 tiles (past one VGPR of block-table
-    entries: the 3-deep form defers to the double buffer, whose table cache
-    refills) against fp32 softmax attention, with a shuffled block table."""
+def test_prefix_pass_block_table_walk(P, monkeypatch):
+    """The prefix pass at 1, 2, 3, 10 and 64 key tiles and at 65 (past one
+    VGPR of cached block-table entries: the cache refills) against fp32
+    softmax attention, with a shuffled block table; 2100 query tokens give
+    the 8-wave grid (more blocks than CUs)."""
     monkeypatch.setenv("MCP_ATTN_PREFIX_RT", "2")
-    monkeypatch.setenv("MCP_ATTN_PREFIX_NW", "8")
-    monkeypatch.setenv("MCP_ATTN_PREFIX_RING", ring)
     torch.manual_seed(13)
-    Hq, Hkv, D, T = 32, 8, 128, 150
+    Hq, Hkv, D, T = 32, 8, 128, 2100
     n_pre = P // 64
     kc, vc = _cache(n_pre + 2, Hkv)
     kc = (kc.float() * (1 + torch.arange(n_pre + 2, device=DEV).view(-1, 1, 1, 1) % 5)).bfloat16()
