@@ -680,6 +680,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_set_persist", &gemm_plan_set_persist_py,
         "per 64-row M bucket for one (N, K): 1 = the persistent AGPR kernel measured faster");
   m.def("gemm_plan_persist", &gemm_plan_persist);
+  m.def("gemm256d_persist", &gemm256d_persist,
+        "1 if an AGPR GEMM of this shape and tile count runs the persistent form");
   m.def("gemm_persist_force", &gemm_persist_force,
         "persistent AGPR GEMM: -1 plan / MCP_GEMM_PERSIST, 0 off, 1 when tiles > CUs, 2 always");
   m.def("gemm_plan_clear", &gemm_plan_clear);
