@@ -232,13 +232,15 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
     cuda = torch.cuda.is_available()
     reg = MemoryRegistry(synthetic_registry(n, seed=3))
     st = Settings(planner_backend="local", model=model, max_batch=max(16, 2 * conc),
-                  max_nodes=6, temperature=0.2, kv_blocks=0 if cuda else 1024)
+                  max_nodes=6, temperature=0.2, kv_blocks=0 if cuda else 1024,
+                  topk=int(os.environ.get("MCP_TOPK", "32")))
     t0 = time.perf_counter()
     planner = LocalPlanner.from_settings(st, reg)
     startup_s = time.perf_counter() - t0
     app = create_app(st, registry=reg, planner=planner,
                      transport=httpx.MockTransport(lambda r: httpx.Response(200, json={})))
     names_seen = set()
+    hit = {}
 
     def client(c, base, k, lats):
         for i in range(k):
@@ -248,8 +250,13 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
             assert r.status_code == 200, r.text
             names_seen.update(x["name"] for x in r.json()["graph"]["nodes"])
 
+    def blocks():
+        st_ = planner.engine.stats
+        return st_.get("prefix_blocks", 0), st_.get("prefix_blocks_reused", 0)
+
     def phase(c, clients, base):
         lats, ths, errs = [], [], []
+        b0 = blocks()
 
         def run(j):
             try:
@@ -264,6 +271,12 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
             th.join()
         if errs:
             raise errs[0]
+        b1 = blocks()
+        nb, nr = b1[0] - b0[0], b1[1] - b0[1]
+        # prompt-prefix 64-token blocks this phase needed, and the share found
+        # already computed (block-level prefix cache, engine.block_reuse)
+        hit.update(prefix_blocks=nb, prefix_blocks_reused=nr,
+                   prefix_block_hit_rate=round(nr / nb, 3) if nb else None)
         return lats, time.perf_counter() - t
 
     def report(name, lats, wall, clients, **extra):
@@ -276,8 +289,9 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
                           "p90_ms": round(q[89] * 1e3, 2), "p99_ms": round(q[98] * 1e3, 2),
                           "plans_per_s": round(len(lats) / wall, 2),
                           "retrieval_p50_ms": round(statistics.median(ret) * 1e3, 3) if ret else None,
-                          "startup_s": round(startup_s, 1), "data": "synthetic registry + intents, "
-                          "random-init weights", **extra}), flush=True)
+                          "startup_s": round(startup_s, 1), "topk": st.topk, **hit,
+                          "data": "synthetic registry + intents, random-init weights", **extra}),
+              flush=True)
 
     with TestClient(app) as c:
         phase(c, 1, 900_000)                                 # warm the request path
