@@ -73,6 +73,7 @@ struct DecArgs {
   int rows;                // T * Hq
   int* split_cnt;          // per (block row, kv head) arrival tickets, zero between launches
   int tpw;                 // tiles per wave
+  int rel;                 // 1: block z covers the own tiles [kt0 + z C, ...), kt0 = kv_begin / 64
 };
 
 template <int G>
@@ -123,15 +124,21 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
   };
 
   // the first tile's block id needs only the grid position: read in the same
-  // round trip as the sequence's sizes; its K / V and the Q loads go next
-  const int kt_first = z * C + wave;
+  // round trip as the sequence's sizes; its K / V and the Q loads go next.
+  // rel: the tiles count from the sequence's first own key tile (one more
+  // round trip, for kv_begin), so a step of many sequences behind a cascade
+  // prefix launches ceil(own tiles / C) blocks per item instead of
+  // ceil(table width / C), most of which would find nothing to do
+  const int kvb = a.kv_begin ? a.kv_begin[s] : 0;
+  const int zbase = (a.rel ? kvb / KT : 0) + z * C;  // this block's first tile
+  const int kt_first = zbase + wave;
   const int blk0 = kt_first < a.max_blocks ? bt[kt_first] : -1;
   const int qs = a.q_start[s], ql = a.q_len[s], cl = a.ctx_len[s];
-  const int kvb = a.kv_begin ? a.kv_begin[s] : 0;
   const int last_tok = min(q0 + TPR, ql) - 1;
   const int kv_end = cl - ql + last_tok + 1;
   const int kt0 = kvb / KT, kt1 = (kv_end + KT - 1) / KT;
-  const int z_first = kt0 / C, z_last = (kt1 - 1) / C;
+  const int z_first = a.rel ? 0 : kt0 / C;
+  const int z_last = a.rel ? (kt1 - 1 - kt0) / C : (kt1 - 1) / C;
   // padding items / row tiles past the span, blocks wholly outside the own keys
   if (q0 >= ql || kt1 <= kt0 || z < z_first || z > z_last) return;
   const int nact = z_last - z_first + 1;
@@ -154,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
   float m_run = -INFINITY, l_part = 0.f;
 
   for (int j = 0; j < a.tpw; ++j) {
-    const int kt = z * C + wave + NWV * j;
+    const int kt = zbase + wave + NWV * j;
     const bool use = kt >= kt0 && kt < kt1;
     if (j > 0 && use) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the last V
@@ -373,6 +380,8 @@ int attn_decode_blocks(int max_blocks) {
   const int C = NWV * attn_decode_tpw(max_blocks);
   return (max_blocks + C - 1) / C;
 }
+// own-span (rel) mode: the same rule over the longest own key span
+int attn_decode_rel_blocks(int own_tiles) { return attn_decode_blocks(own_tiles > 0 ? own_tiles : 1); }
 
 // nonzero: not launched (the caller uses the work-list split path)
 int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, void* out,
@@ -381,13 +390,15 @@ int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, 
                        const int* work_q04, int nwork4, const int* work_seq1, const int* work_q01,
                        int nwork1, int Hq, int Hkv, int head_dim, float scale, const int* kv_begin,
                        const void* pre_o, const float* pre_lse, float* split_o, float* split_lse,
-                       int rows, int nz, hipStream_t s) {
+                       int rows, int nz, hipStream_t s, int own_tiles) {
   if (head_dim != D) return 1;
   const int nitems = 4 * nwork4 + nwork1;            // 4-wave items: one block per row tile
   if (nitems <= 0) return 0;
   if (max_blocks <= 0) return 2;
-  const int tpw = attn_decode_tpw(max_blocks);
-  if (nz != attn_decode_blocks(max_blocks)) return 3;
+  // own_tiles > 0: own-span mode, the longest own key span in tiles
+  const int span = own_tiles > 0 ? own_tiles : max_blocks;
+  const int tpw = attn_decode_tpw(span);
+  if (nz != attn_decode_blocks(span)) return 3;
   int* cnt = attn_split_counters();
   if (!cnt || (long long)nitems * Hkv > (1 << 16)) return 5;
   if (nz > 1 && (!split_o || !split_lse || (long long)nz * rows * D * 4 >= (1ll << 31))) return 6;
@@ -417,6 +428,7 @@ int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, 
   a.rows = rows;
   a.split_cnt = cnt;
   a.tpw = tpw;
+  a.rel = own_tiles > 0;
   const dim3 grid(nitems, Hkv, nz);
   switch (Hq / Hkv) {
     case 1: attn_decode_kernel<1><<<grid, 256, 0, s>>>(a); break;

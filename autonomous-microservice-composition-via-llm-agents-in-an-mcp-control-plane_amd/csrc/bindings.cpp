@@ -411,7 +411,7 @@ bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, cons
                             int64_t nz, at::Tensor& split_o, at::Tensor& split_lse,
                             const c10::optional<at::Tensor>& kv_begin,
                             const c10::optional<at::Tensor>& pre_o,
-                            const c10::optional<at::Tensor>& pre_lse) {
+                            const c10::optional<at::Tensor>& pre_lse, int64_t own_tiles) {
   CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
   CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
   CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq4); CHECK_I32_TENSOR(work_q04);
@@ -424,7 +424,10 @@ bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, cons
   TORCH_CHECK(block_table.dim() == 2 && block_table.size(0) == q_len.numel(), "block_table [S, max_blocks]");
   TORCH_CHECK(work_seq4.numel() == work_q04.numel() && work_seq1.numel() == work_q01.numel(),
               "work lists");
-  TORCH_CHECK(nz == attn_decode_blocks(block_table.size(1)), "nz must be attn_decode_blocks(max_blocks)");
+  TORCH_CHECK(own_tiles >= 0 && own_tiles <= block_table.size(1), "own_tiles in [0, max_blocks]");
+  TORCH_CHECK(nz == (own_tiles > 0 ? attn_decode_rel_blocks((int)own_tiles)
+                                   : attn_decode_blocks(block_table.size(1))),
+              "nz must be attn_decode_blocks(max_blocks), or attn_decode_rel_blocks(own_tiles)");
   TORCH_CHECK(split_o.scalar_type() == at::kFloat && split_o.is_contiguous() &&
               (nz == 1 || split_o.numel() >= nz * q.numel()), "split_o [nz, T, Hq, D] f32");
   TORCH_CHECK(split_lse.scalar_type() == at::kFloat && split_lse.is_contiguous() &&
@@ -449,7 +452,7 @@ bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, cons
       block_table.size(1), work_seq4.data_ptr<int>(), work_q04.data_ptr<int>(), work_seq4.numel(),
       work_seq1.data_ptr<int>(), work_q01.data_ptr<int>(), work_seq1.numel(), Hq, Hkv, D,
       (float)scale, kb, po, pl, split_o.data_ptr<float>(), split_lse.data_ptr<float>(),
-      (int)(q.size(0) * Hq), (int)nz, stream());
+      (int)(q.size(0) * Hq), (int)nz, stream(), (int)own_tiles);
   TORCH_CHECK(rc != 1 && rc != 3 && rc != 4, "paged_attention_decode: unsupported config (code ", rc, ")");
   if (rc != 0) return false;
   check_launch("paged_attention_decode");
@@ -735,7 +738,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("block_table"), py::arg("work_seq4"), py::arg("work_q04"), py::arg("work_seq1"),
         py::arg("work_q01"), py::arg("scale"), py::arg("nz"), py::arg("split_o"),
         py::arg("split_lse"), py::arg("kv_begin") = py::none(), py::arg("pre_o") = py::none(),
-        py::arg("pre_lse") = py::none());
+        py::arg("pre_lse") = py::none(), py::arg("own_tiles") = 0);
+  m.def("attn_decode_rel_blocks", &attn_decode_rel_blocks,
+        "grid z of paged_attention_decode in own-span mode (own_tiles > 0)");
   m.def("copy_blocks", &copy_blocks);
   m.def("car_handle_bytes", []() { return (int64_t)car_handle_bytes(); });
   m.def("car_init", &car_init);

@@ -44,6 +44,9 @@ class AttnMeta:
     # hipGraph steps: device [pre_tokens, pre_keys] (the host ints above are
     # then the bucket's capacities, engine/graphs.py)
     pre_dims: Optional[torch.Tensor] = None
+    # longest own key span of the step in 64-key tiles (keys after the cascade
+    # prefix); 0 = unknown (hipGraph layouts)
+    own_tiles: int = 0
 
     def work_lists(self):
         return self.work
@@ -356,7 +359,8 @@ def views(t: torch.Tensor, layout):
             work_l.append((nw, ws, wq))
     meta = AttnMeta(q_start=vs[4], q_len=vs[5], ctx_len=vs[6], block_table=bt, work=work_l,
                     kv_splits=int(layout[N_SIZES + 2]) if len(layout) > N_SIZES + 2 else 1,
-                    padded=len(layout) > N_SIZES + 3 and bool(layout[N_SIZES + 3]))
+                    padded=len(layout) > N_SIZES + 3 and bool(layout[N_SIZES + 3]),
+                    own_tiles=int(layout[N_SIZES + 4]) if len(layout) > N_SIZES + 4 else 0)
     if pre_tokens > 0:
         meta.kv_begin, meta.pre_bt = vs[14], vs[15]
         meta.pre_keys, meta.pre_tokens = int(vs[15].numel()) * BLOCK_SIZE, pre_tokens

@@ -746,16 +746,19 @@ class LLMEngine:
         cascade = pre_tokens > 0
         # split-KV for few long-context decode sequences (K6), over the keys
         # each sequence attends itself (after the cascade prefix, if any)
+        own_keys = [e[2] + e[1] - (e[4] if cascade else 0) for e in entries]
         kv_splits = choose_kv_splits(
-            [e[1] for e in entries],
-            [e[2] + e[1] - (e[4] if cascade else 0) for e in entries],
+            [e[1] for e in entries], own_keys,
             group, self.model.hkv, hq=self.model.hq) if self.device.type == "cuda" else 1
         with span("sched.pack"):
             host, layout = pack_step(entries, BLOCK_SIZE, group, copies,
                                      casc.blocks[:casc_keys // BLOCK_SIZE] if cascade else None,
                                      pre_tokens if cascade else 0, allowed, ctr)
+            # layout extras: split factor, (hipGraph padding flag), longest own
+            # key span in tiles (the decode kernel's own-span grid)
+            own_tiles = -(-max(own_keys, default=0) // BLOCK_SIZE)
+            layout = list(layout) + [kv_splits, 0, own_tiles]
             if kv_splits > 1:
-                layout = list(layout) + [kv_splits]
                 self.stats["kv_split_steps"] += 1
         t0 = time.perf_counter()
         self.stats["schedule_s"] += t0 - t_sched

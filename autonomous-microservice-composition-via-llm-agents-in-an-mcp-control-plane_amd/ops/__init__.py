@@ -237,6 +237,9 @@ _MIXED_SPLIT = os.environ.get("MCP_ATTN_MIXED", "1") == "1"
 _DECODE_SPLIT = os.environ.get("MCP_ATTN_DECODE", "1") == "1"
 _DECODE_BLOCKS_PER_CU = 2
 _DECODE_FORCE = os.environ.get("MCP_ATTN_DECODE_FORCE", "0") == "1"
+# unsplit steps' items on the decode kernel in own-span mode (attention_decode.hip
+# rel): 0 off, 1 the 1-wave items, 2 both work lists
+_DECODE_OWN = int(os.environ.get("MCP_ATTN_DECODE_OWN", "0"))
 
 
 _CUS = {}
@@ -374,7 +377,30 @@ def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
                     L.cascade_merge(out, kw["own_lse"], pre_o, pre_lse, meta.pre_tokens,
                                     pre_dims=pre_dims)
                 return out
+        done_nw = ()
+        own = int(getattr(meta, "own_tiles", 0))
+        if (ns == 1 and _DECODE_OWN and not concurrent and not getattr(meta, "padded", False)
+                and own > 0 and hasattr(L, "attn_decode_rel_blocks")):
+            # unsplit step on the decode kernel in own-span mode: every item's
+            # own key tiles in flight at once (4 waves x 4 tiles per block)
+            # instead of one wave walking them (MCP_ATTN_DECODE_OWN: 1 = the
+            # 1-wave items, 2 = both lists)
+            lists = {nw: (ws, wq) for nw, ws, wq in meta.work_lists()}
+            e = torch.empty(0, dtype=torch.int32, device=q.device)
+            ws1, wq1 = lists.get(1, (e, e))
+            ws4, wq4 = lists.get(4, (e, e)) if _DECODE_OWN == 2 else (e, e)
+            if ws1.numel() or ws4.numel():
+                nz = L.attn_decode_rel_blocks(own)
+                so = torch.empty(nz if nz > 1 else 0, *q.shape, device=q.device, dtype=torch.float32)
+                sl = torch.empty(nz if nz > 1 else 0, q.shape[0], q.shape[1], device=q.device,
+                                 dtype=torch.float32)
+                if L.paged_attention_decode(q, k_cache, v_cache, out, meta.q_start, meta.q_len,
+                                            meta.ctx_len, meta.block_table, ws4, wq4, ws1, wq1,
+                                            scale, nz, so, sl, own_tiles=own, **kw):
+                    done_nw = (1, 4) if _DECODE_OWN == 2 else (1,)
         for nw, ws, wq in meta.work_lists():
+            if nw in done_nw:
+                continue
             if ns > 1:
                 # split-KV (K6): fp32 partials + LSE per split, merged by a second kernel
                 so = torch.empty(ns, *q.shape, device=q.device, dtype=torch.float32)

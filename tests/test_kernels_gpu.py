@@ -991,3 +991,55 @@ def test_prefix_pass_block_table_walk(P, monkeypatch):
     again = torch.empty_like(q)
     ops.lib().prefix_attention(q, kc, vc, again, lse, pre_bt, P, T, scale)
     assert torch.equal(out, again)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("own_keys,q_lens", [([5, 200, 64, 65], [1, 1, 1, 2]),
+                                              ([300, 130, 1100, 20, 700], [1, 9, 2, 16, 5]),
+                                              ([3000, 64], [1, 1])])
+def test_decode_kernel_own_span_mode(own_keys, q_lens, mode, monkeypatch):
+    """The decode kernel in own-span mode (unsplit steps, MCP_ATTN_DECODE_OWN:
+    1 = the 1-wave items on it, the 4-wave items on the work-list kernel; 2 =
+    both): grid z over each sequence's own tiles after a 640-key cascade
+    prefix, single- and multi-block own spans (last-arriver merge, prefix
+    fold), against fp32 full attention; repeated launches bitwise equal."""
+    monkeypatch.setattr(ops, "_DECODE_OWN", mode)
+    monkeypatch.setenv("MCP_ATTN_CONCURRENT", "0")
+    monkeypatch.setenv("MCP_KV_SPLIT", "0")
+    torch.manual_seed(37)
+    Hq, Hkv, D, BS, P_full = 32, 8, 128, 64, 640
+    ctx = [P_full + k for k in own_keys]
+    n_pre = P_full // BS
+    own_blocks = [(k + BS - 1) // BS for k in own_keys]
+    nb = n_pre + sum(own_blocks) + 2
+    kc, vc = _cache(nb, Hkv)
+    pre = list(range(n_pre))
+    o = n_pre
+    tables = []
+    for nbk in own_blocks:
+        tables.append(pre + list(range(o, o + nbk)))
+        o += nbk
+    bt = np.zeros((len(q_lens), max(len(t) for t in tables) + 3), np.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = t
+    T = sum(q_lens)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    qs = np.concatenate([[0], np.cumsum(q_lens)[:-1]]).astype(np.int32)
+    step = StepInputs(token_ids=np.zeros(T, np.int32), positions=np.zeros(T, np.int32),
+                      slots=np.zeros(T, np.int32), q_start=qs,
+                      q_len=np.asarray(q_lens, np.int32), ctx_len=np.asarray(ctx, np.int32),
+                      block_table=bt, logit_rows=np.zeros(0, np.int32),
+                      kv_begin=np.full(len(q_lens), P_full, np.int32),
+                      pre_bt=np.asarray(pre, np.int32), pre_tokens=T)
+    dev = pack(step, Hq // Hkv, DEV)
+    dev.attn.kv_splits = 1
+    dev.attn.own_tiles = max(own_blocks)
+    exp = ref.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), torch.from_numpy(qs),
+                              torch.tensor(q_lens), torch.tensor(ctx), torch.from_numpy(bt),
+                              1 / math.sqrt(D))
+    outs = []
+    for _ in range(2):
+        out = ops.paged_attention(q, kc, vc, dev.attn, 1 / math.sqrt(D)).cpu()
+        assert rel_err(out, exp) < 2e-2, (own_keys, q_lens)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])

@@ -47,6 +47,7 @@ step = StepInputs(token_ids=np.zeros(T, np.int32), positions=np.zeros(T, np.int3
                   kv_begin=np.full(S, prefix, np.int32), pre_bt=np.arange(nb_pre, dtype=np.int32),
                   pre_tokens=T)
 d = pack(step, Hq // Hkv, dev)
+d.attn.own_tiles = int(-(-(own + ql) // 64))      # as the engine's layout carries it
 scale = 1 / math.sqrt(D)
 L = ops.lib()
 pre_o = torch.empty_like(q)
