@@ -16,6 +16,17 @@ other character is forced.  Edges are derived from the chosen input sources
 (producer -> consumer), so the graph is acyclic and names are unique by
 construction.
 
+Compact model view (``MCP_PLAN_COMPACT=1``, the default): fields that are a
+function of earlier choices - a node's endpoint (its name's registry record)
+and an edge's fallback URL (the target's registry fallback) - are written to
+the output text by the decoder but never enter the model's token stream; the
+model sees ``{"name":"svc","inputs":{...`` and ``"fallback":true``.  The DAG is
+the same T2 JSON; the model's context holds the same information (the name
+determines both URLs) in ~30 % fewer tokens, each of which would otherwise
+run through every layer.  The reference's own prompt never asks its LLM for
+endpoints either (control_plane.py:61-62: service_name, input_keys,
+next_steps, fallback) although its executor reads them (:107).
+
 Decoding mechanics: a *choice* is a prefix-free set of alternative strings;
 each alternative is tokenised standalone and the choice becomes a token trie.
 At a trie node with one child the token is forced (no sampling); with several
@@ -30,6 +41,9 @@ import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 RETRY_CHOICES = ["0", "1", "2", "3"]
+COMPACT = os.environ.get("MCP_PLAN_COMPACT", "1") == "1"
+INPUTS_OPEN = ',"inputs":{'
+FALLBACK_MARK = ',"fallback":true}'
 
 
 class Trie:
@@ -70,9 +84,11 @@ class GrammarSpec:
     """Per-plan constants: candidate services, their token tries, caches."""
 
     def __init__(self, services: Sequence[dict], tokenizer, max_nodes: int = 6,
-                 allow_retries: bool = True, min_nodes: int = 1):
+                 allow_retries: bool = True, min_nodes: int = 1, compact: Optional[bool] = None):
         self.services = list(services)
         self.tok = tokenizer
+        # compact model view: endpoints / fallback URLs written to the output only
+        self.compact = COMPACT if compact is None else bool(compact)
         self.max_nodes = max(1, max_nodes)
         # the model decides when to stop only between min_nodes and max_nodes
         # (a fixed-size plan gives the benchmark a model-independent token count)
@@ -148,6 +164,16 @@ class GrammarSpec:
             self._src_cache[key] = r
         return r
 
+    def endpoint_chunk(self, svc) -> Tuple[str, str]:
+        """(output text, model text) of the forced span after a node's name."""
+        text = ',"endpoint":' + json.dumps(svc["endpoint"]) + INPUTS_OPEN
+        return text, (INPUTS_OPEN if self.compact else text)
+
+    def fallback_alts(self, fb: str) -> Tuple[Tuple[str, ...], Tuple[str, ...]]:
+        """(output alternatives, model alternatives) of an edge's fallback choice."""
+        out = (',"fallback":' + json.dumps(fb) + "}", "}")
+        return out, ((FALLBACK_MARK, "}") if self.compact else out)
+
     def trie(self, alts: Tuple[str, ...]) -> Trie:
         t = self._trie_cache.get(alts)
         if t is None:
@@ -206,10 +232,16 @@ class GrammarSpec:
         services = []
         for svc, ks in zip(self.services, self.keys):
             fb = svc.get("fallback")
+            ep_out, ep_model = self.endpoint_chunk(svc)
+            if fb:
+                fb_out, fb_model = self.fallback_alts(fb)
+                fallback = (list(fb_out), [list(self.tok.encode(x)) for x in fb_model])
+            else:
+                fallback = None
             services.append({
-                "endpoint": chunk(',"endpoint":' + json.dumps(svc["endpoint"]) + ',"inputs":{'),
+                "endpoint": (ep_out, self.encode(ep_model)),    # text out, tokens in
                 "keys": [key_ids[k] for k in ks],
-                "fallback": alts((',"fallback":' + json.dumps(fb) + "}", "}")) if fb else None,
+                "fallback": fallback,
             })
         return {
             "S": len(names), "max_nodes": self.max_nodes, "min_nodes": self.min_nodes,
@@ -256,9 +288,7 @@ class DagDecoder:
             live = ((1 << len(sp.names)) - 1) & ~used_mask
             idx = yield (None, (sp.jnames, sp.name_trie, live))
             used_mask |= 1 << idx
-            svc = sp.services[idx]
-            text = ',"endpoint":' + json.dumps(svc["endpoint"]) + ',"inputs":{'
-            yield (text, None)
+            yield (sp.endpoint_chunk(sp.services[idx]), None)
             inputs = {}
             prev_names = [sp.names[j] for j in chosen]
             for ki, key in enumerate(sp.keys[idx]):
@@ -310,8 +340,8 @@ class DagDecoder:
                 first = False
                 fb = sp.services[idx].get("fallback")
                 if fb:
-                    alts_f = (',"fallback":' + json.dumps(fb) + "}", "}")
-                    yield (None, (alts_f, sp.trie(alts_f), 3))
+                    alts_f, model_f = sp.fallback_alts(fb)
+                    yield (None, (alts_f, sp.trie(model_f), 3))
                 else:
                     yield ("}", None)
         yield ("]}", None)
@@ -328,8 +358,10 @@ class DagDecoder:
         while True:
             text, choice = item
             if text is not None:
-                self.text_parts.append(text)
-                self._pending_tokens += self.spec.encode(text)
+                # (output text, model text) when they differ (compact view)
+                out, model = text if isinstance(text, tuple) else (text, text)
+                self.text_parts.append(out)
+                self._pending_tokens += self.spec.encode(model)
                 try:
                     item = next(self._gen)
                 except StopIteration:

@@ -143,7 +143,7 @@ class LocalPlanner(Planner):
             self._spec_cache[key] = spec
         ptoks = self._prefix_cache.get(key)
         if ptoks is None:
-            prefix, _ = build_prompt_parts(cands, intent)
+            prefix, _ = build_prompt_parts(cands, intent, compact=spec.compact)
             ptoks = self.tok.prompt_ids(prefix)
             if len(self._prefix_cache) > 256:
                 self._prefix_cache.clear()

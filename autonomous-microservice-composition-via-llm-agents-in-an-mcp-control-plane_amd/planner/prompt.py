@@ -25,16 +25,32 @@ HEADER = (
     "\"fallback\": <url>}]}. Edges must point from producers to consumers.\n\n"
     "Available services:\n"
 )
+# the grammar's compact model view (planner/grammar.py): endpoints and fallback
+# URLs come from the registry, the model names services and marks fallbacks
+HEADER_COMPACT = (
+    "You are the planning agent of a microservice control plane. Compose the "
+    "available services into an execution graph that fulfils the user's intent.\n"
+    "Answer with one JSON object and nothing else: {\"nodes\": [{\"name\": <service>, "
+    "\"inputs\": {<input field>: <payload field or upstream node>}, "
+    "\"retries\": <int>}], \"edges\": [{\"from\": <node>, \"to\": <node>, "
+    "\"fallback\": true}]}. Edges must point from producers to consumers; endpoints "
+    "and fallback URLs are filled in from the registry.\n\n"
+    "Available services:\n"
+)
 
 
-def service_line(s) -> str:
+def service_line(s, compact: bool = False) -> str:
     ins = json.dumps(s.get("input_schema") or {}, separators=(",", ":"), sort_keys=True)
     outs = json.dumps(s.get("output_schema") or {}, separators=(",", ":"), sort_keys=True)
+    if compact:
+        return f"- {s['name']} (inputs: {ins}, outputs: {outs})\n"
     return f"- {s['name']} (endpoint: {s['endpoint']}, inputs: {ins}, outputs: {outs})\n"
 
 
-def build_prompt_parts(services: Sequence, intent: str) -> Tuple[str, str]:
-    prefix = HEADER + "".join(service_line(s) for s in services)
+def build_prompt_parts(services: Sequence, intent: str, compact: bool = False) -> Tuple[str, str]:
+    """``compact``: the prompt of the grammar's compact model view (no URLs)."""
+    prefix = (HEADER_COMPACT if compact else HEADER) + \
+        "".join(service_line(s, compact) for s in services)
     suffix = f"\nUser intent: “{intent}”\n\nJSON DAG:"
     return prefix, suffix
 

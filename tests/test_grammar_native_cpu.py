@@ -45,12 +45,14 @@ def _spec(reg, **kw):
     return spec
 
 
+@pytest.mark.parametrize("compact", [True, False])
 @pytest.mark.parametrize("nsvc,max_nodes,min_nodes,retries",
                          [(1, 3, 1, True), (3, 6, 1, True), (10, 5, 5, True), (10, 6, 2, False),
                           (50, 8, 1, True), (200, 4, 4, True)])
-def test_native_matches_python(nsvc, max_nodes, min_nodes, retries):
+def test_native_matches_python(nsvc, max_nodes, min_nodes, retries, compact):
     reg = synthetic_registry(nsvc, seed=nsvc)
-    spec = _spec(reg, max_nodes=max_nodes, min_nodes=min_nodes, allow_retries=retries)
+    spec = _spec(reg, max_nodes=max_nodes, min_nodes=min_nodes, allow_retries=retries,
+                 compact=compact)
     rng = random.Random(nsvc)
     names = [s["name"] for s in reg]
     for _ in range(30):
@@ -117,3 +119,36 @@ def test_native_spec_rejects_malformed_payload(corrupt):
     corrupt(p)
     with pytest.raises(ValueError):
         native._RT.grammar_spec(p)
+
+
+def _take(dec, idx, toks):
+    """Feed the tokens of alternative ``idx`` of the decoder's current choice."""
+    ch = dec._choice
+    while dec._choice is ch and not dec.done:
+        dec.feed(next(t for t, c in dec._node.children.items() if (c.mask >> idx) & 1))
+        toks += dec.advance()
+
+
+def test_compact_view_emits_the_same_dag_in_fewer_tokens():
+    """The compact model view (endpoints and fallback URLs filled from the
+    registry, never fed to the model) and the full view emit identical DAGs
+    for the same decisions; the compact token stream is shorter."""
+    reg = synthetic_registry(10, seed=4)
+    full = GrammarSpec(reg, get_tokenizer(), max_nodes=5, min_nodes=5, compact=False)
+    comp = GrammarSpec(reg, get_tokenizer(), max_nodes=5, min_nodes=5, compact=True)
+    rng = random.Random(5)
+    saved = []
+    for _ in range(30):
+        decs = [DagDecoder(full), DagDecoder(comp)]
+        toks = [d.advance() for d in decs]
+        while not decs[0].done:
+            assert not decs[1].done
+            live = decs[0]._choice[2]
+            assert live == decs[1]._choice[2]
+            idx = rng.choice([i for i in range(live.bit_length()) if (live >> i) & 1])
+            for d, tk in zip(decs, toks):
+                _take(d, idx, tk)
+        assert decs[1].done
+        assert decs[0].result() == decs[1].result()
+        saved.append(len(toks[0]) - len(toks[1]))
+    assert min(saved) > 0
