@@ -120,6 +120,7 @@ def main():
     from mcp_amd.planner.prompt import synthetic_intent
     from mcp_amd.registry import MemoryRegistry, synthetic_registry
     from mcp_amd.utils.heap import settle as settle_heap
+    from mcp_amd.planner.grammar import COMPACT as grammar_compact
 
     t0 = time.time()
     model = LlamaModel.random(args.model, dev, seed=args.seed)
@@ -243,6 +244,9 @@ def main():
                        "seq_len": None, "parallelism": f"dp{world}", "tp": 1,
                        "services": args.services, "nodes_per_plan": [args.min_nodes, args.max_nodes],
                        "tokens_per_plan": round(tokens_total / max(1, plans_total), 1),
+                       # compact: URLs filled from the registry, not run through
+                       # the model (planner/grammar.py; MCP_PLAN_COMPACT=0: full)
+                       "plan_view": "compact" if grammar_compact else "full",
                        "temperature": 0.2},
         }), flush=True)
     if world > 1:
