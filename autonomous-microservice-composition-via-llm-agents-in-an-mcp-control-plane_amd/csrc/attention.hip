@@ -28,6 +28,8 @@
 // attn_split_combine merges the splits with LSE weights.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -365,14 +367,14 @@ void attn_kernel(const AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt * KT + nt * 16 + fq * 4 + r;
-        float v = sacc[nt][r] * a.scale_log2;
-        v = (key <= qpos && key < cl) ? v : -INFINITY;
+        // unscaled (max commutes with the positive scale; one fma per score below)
+        const float v = (key <= qpos && key < cl) ? sacc[nt][r] : -INFINITY;
         sacc[nt][r] = v;
         tmax = fmaxf(tmax, v);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
+    const float m_new = fmaxf(m_run, tmax * a.scale_log2);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
     const float alpha = fexp2(m_run - m_use);
     m_run = m_new;
@@ -382,7 +384,7 @@ void attn_kernel(const AttnArgs a) {
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = fexp2(sacc[nt][r] - m_use);
+        const float p = fexp2(fmaf(sacc[nt][r], a.scale_log2, -m_use));
         psum += p;
         pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
       }
@@ -557,8 +559,11 @@ void attn_prefix_kernel(const AttnArgs a) {
   if (ntiles > 0) stage(0, 0);
   __syncthreads();
   const int tq = (lane & 15) >> 2, tp = lane & 3;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
+  // one key tile; the buffer index is a compile-time constant (the loop below
+  // runs two tiles per trip), so every LDS address is a per-lane base plus an
+  // immediate offset instead of ~50 VALU address ops per tile
+  auto step = [&](int kt, auto cc) {
+    constexpr int cur = decltype(cc)::value;
     if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
     const bf16* Kl = smem + cur * 2 * TILE;
     const bf16* Vl = Kl + TILE;
@@ -578,7 +583,11 @@ void attn_prefix_kernel(const AttnArgs a) {
         for (int r = 0; r < RT; ++r) sacc[r][nt] = mfma16x16x32(kf, qf[r][ks], sacc[r][nt]);
       }
     }
-    // ---- online softmax per row tile (lane: query row fr, keys 16nt + 4fq + r)
+    // ---- online softmax per row tile (lane: query row fr, keys 16nt + 4fq + r).
+    //      The scores stay unscaled: the max commutes with the positive scale,
+    //      and exp2(s c - m) is one fma + exp per score (the pass is VALU-bound,
+    //      profiles/attention_tuning.md round 4)
+    const float c = a.scale_log2;
     bf16x8 pf[RT][2];
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
@@ -586,13 +595,10 @@ void attn_prefix_kernel(const AttnArgs a) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          sacc[r][nt][e] *= a.scale_log2;
-          tmax = fmaxf(tmax, sacc[r][nt][e]);
-        }
+        for (int e = 0; e < 4; ++e) tmax = fmaxf(tmax, sacc[r][nt][e]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_run[r], tmax);
+      const float m_new = fmaxf(m_run[r], tmax * c);
       const float alpha = fexp2(m_run[r] - m_new);
       m_run[r] = m_new;
       float psum = 0.f;
@@ -600,7 +606,7 @@ void attn_prefix_kernel(const AttnArgs a) {
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = fexp2(sacc[r][nt][e] - m_new);
+          const float p = fexp2(fmaf(sacc[r][nt][e], c, -m_new));
           psum += p;
           pf[r][nt >> 1][(nt & 1) * 4 + e] = (bf16)p;
         }
@@ -625,7 +631,15 @@ void attn_prefix_kernel(const AttnArgs a) {
       }
     }
     __syncthreads();             // its fence also drains the next tile's LDS-DMA
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  int kt = 0;
+  for (; kt + 1 < ntiles; kt += 2) {
+    step(kt, C0{});
+    step(kt + 1, C1{});
   }
+  if (kt < ntiles) step(kt, C0{});
 
   // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + e]
 #pragma unroll

@@ -185,14 +185,14 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt * KT + nt * 16 + fq * 4 + r;
-        float v = sacc[nt][r] * a.scale_log2;
-        v = (key <= qpos && key < cl) ? v : -INFINITY;
+        // unscaled (max commutes with the positive scale; one fma per score below)
+        const float v = (key <= qpos && key < cl) ? sacc[nt][r] : -INFINITY;
         sacc[nt][r] = v;
         tmax = fmaxf(tmax, v);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
+    const float m_new = fmaxf(m_run, tmax * a.scale_log2);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
     const float alpha = fexp2(m_run - m_use);
     m_run = m_new;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = fexp2(sacc[nt][r] - m_use);
+        const float p = fexp2(fmaf(sacc[nt][r], a.scale_log2, -m_use));
         psum += p;
         pf[nt >> 1][(nt & 1) * 4 + r] = (bf16)p;
       }
