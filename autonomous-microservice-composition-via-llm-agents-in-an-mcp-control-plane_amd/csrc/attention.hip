@@ -28,8 +28,6 @@
 // attn_split_combine merges the splits with LSE weights.
 #include <stdlib.h>
 
-#include <type_traits>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -559,11 +557,8 @@ void attn_prefix_kernel(const AttnArgs a) {
   if (ntiles > 0) stage(0, 0);
   __syncthreads();
   const int tq = (lane & 15) >> 2, tp = lane & 3;
-  // one key tile; the buffer index is a compile-time constant (the loop below
-  // runs two tiles per trip), so every LDS address is a per-lane base plus an
-  // immediate offset instead of ~50 VALU address ops per tile
-  auto step = [&](int kt, auto cc) {
-    constexpr int cur = decltype(cc)::value;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
     if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
     const bf16* Kl = smem + cur * 2 * TILE;
     const bf16* Vl = Kl + TILE;
@@ -585,8 +580,7 @@ void attn_prefix_kernel(const AttnArgs a) {
     }
     // ---- online softmax per row tile (lane: query row fr, keys 16nt + 4fq + r).
     //      The scores stay unscaled: the max commutes with the positive scale,
-    //      and exp2(s c - m) is one fma + exp per score (the pass is VALU-bound,
-    //      profiles/attention_tuning.md round 4)
+    //      and exp2(s c - m) is one fma + exp per score
     const float c = a.scale_log2;
     bf16x8 pf[RT][2];
 #pragma unroll
@@ -631,15 +625,7 @@ void attn_prefix_kernel(const AttnArgs a) {
       }
     }
     __syncthreads();             // its fence also drains the next tile's LDS-DMA
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  int kt = 0;
-  for (; kt + 1 < ntiles; kt += 2) {
-    step(kt, C0{});
-    step(kt + 1, C1{});
   }
-  if (kt < ntiles) step(kt, C0{});
 
   // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + e]
 #pragma unroll
