@@ -296,6 +296,7 @@ def main():
     from mcp_amd.planner.local import LocalPlanner
     from mcp_amd.planner.prompt import synthetic_intent
     from mcp_amd.registry import MemoryRegistry, synthetic_registry
+    import mcp_amd.planner.grammar as planner_grammar
 
     eng = LLMEngine(model, num_blocks=nb, max_batch=args.batch + 8, max_step_tokens=16384,
                     temperature=0.2, seed=args.seed, bcast=bcast)
@@ -371,7 +372,11 @@ def main():
         "p50_latency_ms": round(statistics.median(lats) * 1e3, 1) if lats else None,
         "p99_latency_ms": round(statistics.quantiles(lats, n=100)[98] * 1e3, 1)
         if len(lats) >= 2 else None,
-        "tokens": eng.stats["tokens"], "execution": exec_stats,
+        "tokens": eng.stats["tokens"], "engine_steps": eng.stats["steps"],
+        # plan size is the random model's choice here (1 - max_nodes nodes)
+        "nodes_per_plan": round(statistics.mean(len(d["nodes"]) for d in dags), 2) if dags else None,
+        "plan_view": "compact" if getattr(planner_grammar, "COMPACT", True) else "full",
+        "execution": exec_stats,
     }), flush=True)
     if world > 1:
         dist.destroy_process_group()
