@@ -137,7 +137,8 @@ def simulate_rank(args):
     eng = LLMEngine(model, num_blocks=nb, max_batch=args.batch + 8, max_step_tokens=16384,
                     temperature=0.2, seed=args.seed, graphs=cuda)
     reg = MemoryRegistry(synthetic_registry(args.services, seed=4))
-    planner = LocalPlanner(eng, reg, max_nodes=args.max_nodes, retrieval_threshold=10 ** 9)
+    planner = LocalPlanner(eng, reg, max_nodes=args.max_nodes, min_nodes=args.min_nodes,
+                           retrieval_threshold=10 ** 9)
     names = [s.name for s in reg.list_services()]
     ncap = eng.warm_graphs(contexts=(8192,))
     steps = []
@@ -244,7 +245,11 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--max-nodes", type=int, default=6)
+    ap.add_argument("--max-nodes", type=int, default=5)
+    ap.add_argument("--min-nodes", type=int, default=5,
+                    help="min == max fixes the plan size, so the work per plan does not depend on "
+                         "the random weights' stop decisions (as bench.py; round 3 ran 1-6 nodes, "
+                         "where a random 70B stopped after one)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--seq-parallel", action="store_true",
                     help="Megatron sequence parallelism (reduce-scatter / all-gather) for TP > 1")
@@ -301,7 +306,8 @@ def main():
     eng = LLMEngine(model, num_blocks=nb, max_batch=args.batch + 8, max_step_tokens=16384,
                     temperature=0.2, seed=args.seed, bcast=bcast)
     reg = MemoryRegistry(synthetic_registry(args.services, seed=4))
-    planner = LocalPlanner(eng, reg, max_nodes=args.max_nodes, retrieval_threshold=10 ** 9)
+    planner = LocalPlanner(eng, reg, max_nodes=args.max_nodes, min_nodes=args.min_nodes,
+                           retrieval_threshold=10 ** 9)
     names = [s.name for s in reg.list_services()]
     t0 = time.perf_counter()
     ncap = eng.warm_graphs(contexts=(8192,))         # server start-up capture (planner.local)
@@ -373,7 +379,7 @@ def main():
         "p99_latency_ms": round(statistics.quantiles(lats, n=100)[98] * 1e3, 1)
         if len(lats) >= 2 else None,
         "tokens": eng.stats["tokens"], "engine_steps": eng.stats["steps"],
-        # plan size is the random model's choice here (1 - max_nodes nodes)
+        # min_nodes - max_nodes nodes (the random model's stop decisions in between)
         "nodes_per_plan": round(statistics.mean(len(d["nodes"]) for d in dags), 2) if dags else None,
         "plan_view": "compact" if getattr(planner_grammar, "COMPACT", True) else "full",
         "execution": exec_stats,
