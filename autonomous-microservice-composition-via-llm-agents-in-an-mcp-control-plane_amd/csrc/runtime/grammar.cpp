@@ -108,6 +108,7 @@ struct NativeSpec {
   std::vector<std::vector<int>> pos;          // [key][service] -> alternative or -1
   std::vector<std::vector<int>> alt_name;     // [key][alt] -> service index of that source or -1
   py::object encode;                          // str -> list[int] (edge chunks)
+  py::object edge_model;                      // (first, src, dst) -> the model's text (compact view)
   std::map<std::tuple<int, int, int>, Chunk> edge_cache;
 
   const Chunk& edge(bool first, int src, int dst) {
@@ -116,7 +117,9 @@ struct NativeSpec {
     if (it != edge_cache.end()) return it->second;
     Chunk c;
     c.text = std::string(first ? "" : ",") + "{\"from\":" + jnames[src] + ",\"to\":" + jnames[dst];
-    c.toks = encode(c.text).cast<std::vector<int>>();
+    const std::string model =
+        edge_model.is_none() ? c.text : edge_model(first, src, dst).cast<std::string>();
+    if (!model.empty()) c.toks = encode(model).cast<std::vector<int>>();
     return edge_cache.emplace(key, std::move(c)).first->second;
   }
 };
@@ -443,6 +446,7 @@ std::shared_ptr<NativeSpec> make_spec(const py::dict& d) {
   }
   validate(*sp);
   sp->encode = d["encode"];
+  sp->edge_model = d.contains("edge_model") ? py::object(d["edge_model"]) : py::object(py::none());
   return sp;
 }
 

@@ -20,9 +20,11 @@ Compact model view (``MCP_PLAN_COMPACT=1``, the default): fields that are a
 function of earlier choices - a node's endpoint (its name's registry record)
 and an edge's fallback URL (the target's registry fallback) - are written to
 the output text by the decoder but never enter the model's token stream; the
-model sees ``{"name":"svc","inputs":{...`` and ``"fallback":true``.  The DAG is
-the same T2 JSON; the model's context holds the same information (the name
-determines both URLs) in ~30 % fewer tokens, each of which would otherwise
+model sees ``{"name":"svc","inputs":{...`` and ``"fallback":true``.  Edges follow
+from the chosen input sources, so the model sees only those it decides on
+(``{"to":"<dst>"`` before a fallback choice).  The DAG is the same T2 JSON;
+the model's context holds the same information (names determine the URLs,
+inputs determine the edges) in fewer tokens, each of which would otherwise
 run through every layer.  The reference's own prompt never asks its LLM for
 endpoints either (control_plane.py:61-62: service_name, input_keys,
 next_steps, fallback) although its executor reads them (:107).
@@ -169,6 +171,21 @@ class GrammarSpec:
         text = ',"endpoint":' + json.dumps(svc["endpoint"]) + INPUTS_OPEN
         return text, (INPUTS_OPEN if self.compact else text)
 
+    def edge_chunk(self, first: bool, src: str, dst_idx: int) -> Tuple[str, str]:
+        """(output text, model text) of an edge's opening.  Edges follow from
+        the input sources already chosen; in the compact view the model sees
+        only the edges it decides on (a target with a registry fallback), as
+        ``{"to":"<dst>"`` before the fallback choice, and nothing otherwise."""
+        dst = self.names[dst_idx]
+        out = ("" if first else ",") + '{"from":' + json.dumps(src) + ',"to":' + json.dumps(dst)
+        if not self.compact:
+            return out, out
+        return out, ('{"to":' + json.dumps(dst) if self.services[dst_idx].get("fallback") else "")
+
+    def edge_model_text(self, first: bool, src: int, dst: int) -> str:
+        """The model text of an edge by service indices (native decoder callback)."""
+        return self.edge_chunk(first, self.names[src], dst)[1]
+
     def fallback_alts(self, fb: str) -> Tuple[Tuple[str, ...], Tuple[str, ...]]:
         """(output alternatives, model alternatives) of an edge's fallback choice."""
         out = (',"fallback":' + json.dumps(fb) + "}", "}")
@@ -250,8 +267,11 @@ class GrammarSpec:
             "cont_trie": alts((',{"name":', '],"edges":[')),
             "chunks": {"start": chunk('{"nodes":[{"name":'), "retries": chunk('},"retries":'),
                        "close1": chunk("}"), "close2": chunk("}}"), "next": chunk(',{"name":'),
-                       "edges": chunk('],"edges":['), "close_edge": chunk("}"), "end": chunk("]}")},
+                       "edges": chunk('],"edges":['), "end": chunk("]}"),
+                       # closes an edge without a fallback choice: silent in the compact view
+                       "close_edge": ("}", [] if self.compact else self.encode("}"))},
             "services": services, "keys": keys, "encode": self.encode,
+            "edge_model": self.edge_model_text,
         }
 
 
@@ -335,15 +355,14 @@ class DagDecoder:
                         sp.names.index(v) in chosen[:j]:
                     srcs.append(v)
             for src in srcs:
-                yield (("" if first else ",") + '{"from":' + json.dumps(src) + ',"to":'
-                       + json.dumps(dst), None)
+                yield (sp.edge_chunk(first, src, idx), None)
                 first = False
                 fb = sp.services[idx].get("fallback")
                 if fb:
                     alts_f, model_f = sp.fallback_alts(fb)
                     yield (None, (alts_f, sp.trie(model_f), 3))
                 else:
-                    yield ("}", None)
+                    yield (("}", "" if sp.compact else "}"), None)
         yield ("]}", None)
 
     def _step_gen(self, send):
@@ -361,7 +380,8 @@ class DagDecoder:
                 # (output text, model text) when they differ (compact view)
                 out, model = text if isinstance(text, tuple) else (text, text)
                 self.text_parts.append(out)
-                self._pending_tokens += self.spec.encode(model)
+                if model:
+                    self._pending_tokens += self.spec.encode(model)
                 try:
                     item = next(self._gen)
                 except StopIteration:

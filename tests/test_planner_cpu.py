@@ -39,11 +39,17 @@ def random_walk(spec, rng):
     return dec, toks, n
 
 
-def model_view(text: str) -> str:
-    """The compact model view of an emitted DAG: no endpoints, fallback URLs
-    replaced by the mark the model chose (planner/grammar.py)."""
-    text = re.sub(r',"endpoint":"[^"]*"', "", text)
-    return re.sub(r',"fallback":"[^"]*"', ',"fallback":true', text)
+def model_view(text: str, by) -> str:
+    """The compact model view of an emitted DAG (planner/grammar.py): no
+    endpoints; of the edges only those whose target has a registry fallback,
+    as {"to":...} with the fallback mark the model chose."""
+    head, edges = re.sub(r',"endpoint":"[^"]*"', "", text).split('],"edges":[')
+    parts = []
+    for e in json.loads("[" + edges[:-2] + "]"):
+        if by[e["to"]]["fallback"]:
+            parts.append('{"to":' + json.dumps(e["to"]) +
+                         (',"fallback":true}' if "fallback" in e else "}"))
+    return head + '],"edges":[' + "".join(parts) + "]}"
 
 
 @pytest.mark.parametrize("compact", [False, True])
@@ -60,8 +66,8 @@ def test_grammar_always_valid_t2(nsvc, max_nodes, compact):
         assert len(dag["nodes"]) <= max_nodes
         # the token stream decodes to exactly the emitted JSON text (compact:
         # to its model view, URLs left to the registry)
-        assert tok.decode(toks) == (model_view(dec.text) if compact else dec.text)
         by = {s["name"]: s for s in reg}
+        assert tok.decode(toks) == (model_view(dec.text, by) if compact else dec.text)
         for node in dag["nodes"]:
             assert node["endpoint"] == by[node["name"]]["endpoint"]
             assert set(node["inputs"]) == set(by[node["name"]].input_keys())
@@ -473,11 +479,14 @@ def test_prefix_cache_yields_blocks_when_the_pool_is_full():
     assert eng.alloc.num_free == eng.kv.num_blocks
 
 
-def test_preemption_by_recompute_under_a_small_kv_pool():
+def test_preemption_by_recompute_under_a_small_kv_pool(monkeypatch):
     """A pool too small for every admitted request's growth: requests are
     preempted (blocks freed, history recomputed later, shared prefix blocks
     kept) and the greedy plans equal a large pool's; a pool that cannot hold
-    one request fails it cleanly; no block leaks either way."""
+    one request fails it cleanly; no block leaks either way.  (Pool sizes for
+    the full model view's token counts.)"""
+    import mcp_amd.planner.grammar as grammar
+    monkeypatch.setattr(grammar, "COMPACT", False)
     reg = MemoryRegistry(synthetic_registry(5, seed=7))
     intents = [synthetic_intent(i) for i in range(8)]
 
