@@ -279,10 +279,22 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
                    prefix_block_hit_rate=round(nr / nb, 3) if nb else None)
         return lats, time.perf_counter() - t
 
+    def phases(n):
+        """p50 / p99 (ms) of the engine-side phases of the phase's last n requests
+        (queue: submit -> admitted, ttft: -> first sampled token, decode: the rest)."""
+        out = {}
+        for k in ("queue_s", "ttft_s", "decode_s"):
+            if k in METRICS.windows:
+                v = sorted(list(METRICS.windows[k].samples)[-n:])
+                if v:
+                    out[k[:-2]] = [round(v[len(v) // 2] * 1e3, 1), round(v[min(len(v) - 1, int(len(v) * 0.99))] * 1e3, 1)]
+        return out
+
     def report(name, lats, wall, clients, **extra):
         q = statistics.quantiles(lats, n=100) if len(lats) >= 2 else [lats[0]] * 99
         ret = list(METRICS.windows["retrieval_s"].samples)[-len(lats):] \
             if "retrieval_s" in METRICS.windows else []
+        extra = {"phase_p50_p99_ms": phases(len(lats)), **extra}
         print(json.dumps({"config": f"e2e/plan/{name}", "services": n, "model": model,
                           "device": "cuda" if cuda else "cpu", "clients": clients,
                           "requests": len(lats), "p50_ms": round(statistics.median(lats) * 1e3, 2),
