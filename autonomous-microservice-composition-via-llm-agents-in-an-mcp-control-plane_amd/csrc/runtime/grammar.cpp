@@ -465,4 +465,16 @@ void register_grammar(py::module_& m) {
       .def("result", [](const NativeDecoder& d) {
         return py::module_::import("json").attr("loads")(d.text());
       });
+  // one engine step's sampled tokens: feed + advance for every decoder in one
+  // call (the per-sequence Python loop was most of the host update per step)
+  m.def("feed_advance_many", [](const py::list& decs, const std::vector<int>& toks) {
+    if ((size_t)py::len(decs) != toks.size()) throw py::value_error("decoders / tokens length");
+    py::list out(toks.size());
+    for (size_t i = 0; i < toks.size(); ++i) {
+      NativeDecoder& d = decs[i].cast<NativeDecoder&>();
+      d.feed(toks[i]);
+      out[i] = py::cast(d.advance());
+    }
+    return out;
+  });
 }

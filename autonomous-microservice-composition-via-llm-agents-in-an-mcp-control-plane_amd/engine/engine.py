@@ -135,6 +135,21 @@ def tp_graph_safe(model) -> bool:
     return True
 
 
+_FEED_ADVANCE = False
+
+
+def _native_feed_advance():
+    """(runtime.feed_advance_many, native DagDecoder type) or None."""
+    global _FEED_ADVANCE
+    if _FEED_ADVANCE is False:
+        _FEED_ADVANCE = None
+        from . import native
+        rt = native._RT if native.available() else None
+        if rt is not None and hasattr(rt, "feed_advance_many") and hasattr(rt, "DagDecoder"):
+            _FEED_ADVANCE = (rt.feed_advance_many, rt.DagDecoder)
+    return _FEED_ADVANCE
+
+
 class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
@@ -815,12 +830,20 @@ class LLMEngine:
             del seq.pending[:take]
             if seq.is_prefix_job and not seq.pending:
                 self._finish(seq)
-        for seq, tok in zip(sample_seqs, new_tokens):
+        decs = [seq.decoder for seq in sample_seqs]
+        fa = _native_feed_advance()
+        if fa is not None and decs and all(type(d) is fa[1] for d in decs):
+            news = fa[0](decs, new_tokens)          # native decoders: one call per step
+        else:
+            news = []
+            for d, tok in zip(decs, new_tokens):
+                d.feed(int(tok))
+                news.append(d.advance())
+        now = None
+        for seq, new in zip(sample_seqs, news):
             if seq.t_first is None:
-                seq.t_first = time.perf_counter()
+                seq.t_first = now = now or time.perf_counter()
             seq.n_samples += 1
-            seq.decoder.feed(int(tok))
-            new = seq.decoder.advance()
             seq.pending += new
             seq.tokens += new
         max_pos = getattr(self.model.cfg, "max_pos", None)
