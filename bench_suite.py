@@ -231,9 +231,13 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
     logging.getLogger("httpx").setLevel(logging.WARNING)
     cuda = torch.cuda.is_available()
     reg = MemoryRegistry(synthetic_registry(n, seed=3))
+    # fixed 5-node plans (min == max, as bench.py / bench_tp.py): the work per
+    # request does not depend on the random weights' stop decisions, so the
+    # latency spread is the system's, not the plan sizes' (MCP_E2E_NODES)
+    nodes = int(os.environ.get("MCP_E2E_NODES", "5"))
     st = Settings(planner_backend="local", model=model, max_batch=max(16, 2 * conc),
-                  max_nodes=6, temperature=0.2, kv_blocks=0 if cuda else 1024,
-                  topk=int(os.environ.get("MCP_TOPK", "32")))
+                  max_nodes=nodes, min_nodes=nodes, temperature=0.2,
+                  kv_blocks=0 if cuda else 1024, topk=int(os.environ.get("MCP_TOPK", "32")))
     t0 = time.perf_counter()
     planner = LocalPlanner.from_settings(st, reg)
     startup_s = time.perf_counter() - t0
@@ -301,7 +305,8 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
                           "p90_ms": round(q[89] * 1e3, 2), "p99_ms": round(q[98] * 1e3, 2),
                           "plans_per_s": round(len(lats) / wall, 2),
                           "retrieval_p50_ms": round(statistics.median(ret) * 1e3, 3) if ret else None,
-                          "startup_s": round(startup_s, 1), "topk": st.topk, **hit,
+                          "startup_s": round(startup_s, 1), "topk": st.topk,
+                          "nodes_per_plan": [st.min_nodes, st.max_nodes], **hit,
                           "data": "synthetic registry + intents, random-init weights", **extra}),
               flush=True)
 
