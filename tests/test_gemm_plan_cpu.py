@@ -24,4 +24,4 @@ def test_plan_covers_every_shard_shape(model, tp):
     for nk in shard_shapes(model, tp):
         assert nk in have, (model, tp, nk)
         codes = have[nk]["codes"]
-        assert len(codes) == 64 and all(-1 <= c <= 5 for c in codes)
+        assert len(codes) >= 64 and all(-1 <= c <= 5 for c in codes)
