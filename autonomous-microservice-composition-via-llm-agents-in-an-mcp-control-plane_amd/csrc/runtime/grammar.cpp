@@ -108,17 +108,19 @@ struct NativeSpec {
   std::vector<std::vector<int>> pos;          // [key][service] -> alternative or -1
   std::vector<std::vector<int>> alt_name;     // [key][alt] -> service index of that source or -1
   py::object encode;                          // str -> list[int] (edge chunks)
-  py::object edge_model;                      // (first, src, dst) -> the model's text (compact view)
+  bool compact = false;                       // compact model view (planner/grammar.py)
   std::map<std::tuple<int, int, int>, Chunk> edge_cache;
 
+  // an edge's opening: the output text, and the model's tokens - in the
+  // compact view only edges to a service with a fallback choice, as
+  // {"to":"<dst>" (GrammarSpec.edge_chunk)
   const Chunk& edge(bool first, int src, int dst) {
     auto key = std::make_tuple((int)first, src, dst);
     auto it = edge_cache.find(key);
     if (it != edge_cache.end()) return it->second;
     Chunk c;
     c.text = std::string(first ? "" : ",") + "{\"from\":" + jnames[src] + ",\"to\":" + jnames[dst];
-    const std::string model =
-        edge_model.is_none() ? c.text : edge_model(first, src, dst).cast<std::string>();
+    const std::string model = !compact ? c.text : fb_trie[dst] ? "{\"to\":" + jnames[dst] : "";
     if (!model.empty()) c.toks = encode(model).cast<std::vector<int>>();
     return edge_cache.emplace(key, std::move(c)).first->second;
   }
@@ -446,7 +448,7 @@ std::shared_ptr<NativeSpec> make_spec(const py::dict& d) {
   }
   validate(*sp);
   sp->encode = d["encode"];
-  sp->edge_model = d.contains("edge_model") ? py::object(d["edge_model"]) : py::object(py::none());
+  sp->compact = d.contains("compact") && d["compact"].cast<bool>();
   return sp;
 }
 

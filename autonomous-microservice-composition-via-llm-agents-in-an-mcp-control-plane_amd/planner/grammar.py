@@ -182,10 +182,6 @@ class GrammarSpec:
             return out, out
         return out, ('{"to":' + json.dumps(dst) if self.services[dst_idx].get("fallback") else "")
 
-    def edge_model_text(self, first: bool, src: int, dst: int) -> str:
-        """The model text of an edge by service indices (native decoder callback)."""
-        return self.edge_chunk(first, self.names[src], dst)[1]
-
     def fallback_alts(self, fb: str) -> Tuple[Tuple[str, ...], Tuple[str, ...]]:
         """(output alternatives, model alternatives) of an edge's fallback choice."""
         out = (',"fallback":' + json.dumps(fb) + "}", "}")
@@ -270,8 +266,12 @@ class GrammarSpec:
                        "edges": chunk('],"edges":['), "end": chunk("]}"),
                        # closes an edge without a fallback choice: silent in the compact view
                        "close_edge": ("}", [] if self.compact else self.encode("}"))},
-            "services": services, "keys": keys, "encode": self.encode,
-            "edge_model": self.edge_model_text,
+            # the tokenizer's own encode, not a bound method of this spec: the
+            # native spec keeps it, and a reference back to the spec would be a
+            # cycle through C++ that the garbage collector cannot see (a leak per
+            # retrieved candidate set)
+            "services": services, "keys": keys, "encode": self.tok.encode,
+            "compact": self.compact,
         }
 
 

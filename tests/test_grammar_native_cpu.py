@@ -152,3 +152,18 @@ def test_compact_view_emits_the_same_dag_in_fewer_tokens():
         assert decs[0].result() == decs[1].result()
         saved.append(len(toks[0]) - len(toks[1]))
     assert min(saved) > 0
+
+
+def test_native_spec_does_not_keep_its_grammar_spec_alive():
+    """The native spec holds the tokenizer's encode, not a bound method of the
+    Python spec: a reference back would be a cycle through C++ that the
+    collector cannot see, leaking every retrieved candidate set's spec."""
+    import gc
+    import weakref
+    spec = GrammarSpec(synthetic_registry(6, seed=3), get_tokenizer(), max_nodes=3)
+    dec = spec.decoder()
+    assert type(dec).__module__ != DagDecoder.__module__      # the native decoder
+    ref = weakref.ref(spec)
+    del spec, dec
+    gc.collect()
+    assert ref() is None
