@@ -79,6 +79,10 @@ def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
     forced = int(os.environ.get("MCP_KV_SPLIT", "-1"))
     if forced == 0:
         return 1
+    if forced < 0 and sum(1 for ql in q_lens if ql > 0) * hkv >= _SPLIT_WORK_FACTOR * num_cus:
+        # every sequence is at least one work item per kv head: never split
+        # (the per-step host path skips the loop below for large batches)
+        return 1
     t1 = tokens_per_item(1, group)
     t4 = tokens_per_item(4, group)
     cutoff = int(os.environ.get("MCP_ATTN_NW1_CUTOFF", str(t1 * 2)))
