@@ -469,6 +469,12 @@ void register_grammar(py::module_& m) {
       });
   // one engine step's sampled tokens: feed + advance for every decoder in one
   // call (the per-sequence Python loop was most of the host update per step)
+  m.def("allowed_many", [](const py::list& decs) {
+    py::list out(py::len(decs));
+    for (size_t i = 0; i < (size_t)py::len(decs); ++i)
+      out[i] = py::cast(decs[i].cast<const NativeDecoder&>().allowed());
+    return out;
+  });
   m.def("feed_advance_many", [](const py::list& decs, const std::vector<int>& toks) {
     if ((size_t)py::len(decs) != toks.size()) throw py::value_error("decoders / tokens length");
     py::list out(toks.size());

@@ -139,14 +139,14 @@ _FEED_ADVANCE = False
 
 
 def _native_feed_advance():
-    """(runtime.feed_advance_many, native DagDecoder type) or None."""
+    """(runtime.feed_advance_many, native DagDecoder type, runtime.allowed_many) or None."""
     global _FEED_ADVANCE
     if _FEED_ADVANCE is False:
         _FEED_ADVANCE = None
         from . import native
         rt = native._RT if native.available() else None
-        if rt is not None and hasattr(rt, "feed_advance_many") and hasattr(rt, "DagDecoder"):
-            _FEED_ADVANCE = (rt.feed_advance_many, rt.DagDecoder)
+        if rt is not None and hasattr(rt, "allowed_many") and hasattr(rt, "DagDecoder"):
+            _FEED_ADVANCE = (rt.feed_advance_many, rt.DagDecoder, rt.allowed_many)
     return _FEED_ADVANCE
 
 
@@ -752,7 +752,12 @@ class LLMEngine:
         allowed = ctr = None
         if sample_seqs:            # grammar masks go in the same single H2D copy
             with span("sched.allowed"):
-                allowed = [q.decoder.allowed() for q in sample_seqs]
+                decs = [q.decoder for q in sample_seqs]
+                fa = _native_feed_advance()
+                if fa is not None and all(type(d) is fa[1] for d in decs):
+                    allowed = fa[2](decs)              # one native call per step
+                else:
+                    allowed = [d.allowed() for d in decs]
             ctr = [(q.uid * 4096 + q.n_samples) & 0x7FFFFFFF for q in sample_seqs]
         # a step that fits a captured bucket replays its hipGraph (prefix
         # copy-on-write, cascade and split-KV attention included)
