@@ -689,6 +689,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "persistent AGPR GEMM: -1 plan / MCP_GEMM_PERSIST, 0 off, 1 when tiles > CUs, 2 always");
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_flex_count", &gemm_flex_count, "flex tile candidates (gemm(..., algo=16 + i))");
+  m.def("gemm_flex_silu_ok", &gemm_flex_silu_ok, "1 if flex candidate i has the SwiGLU epilogue");
   m.def("gemm_flex_tiles", &gemm_flex_tiles, py::arg("cand"), py::arg("M"), py::arg("N"));
   m.def("gemm_plan_lookup", &gemm_plan_lookup);
   m.def("gemm_splitk_init", [](int64_t bytes) { return gemm_splitk_init((size_t)bytes); },

@@ -583,6 +583,11 @@ int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K,
   if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
       launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0)
     return 0;
+  // serving-size M: a measured flex tile with the SwiGLU epilogue (plan "flex")
+  const int fx = gemm_plan_flex(M, N, K);
+  if (fx >= 0 && gemm_flex_silu_ok(fx) &&
+      launch_gemm_flex_epi(X, W, Y, nullptr, M, N, K, fx, 2, s) == 0)
+    return 0;
   if (gemm_select(M, N, K) == 1) {
     launch_gemm_tn_256_silu(X, W, Y, M, N, K, s);
   } else if (!launch_gemm_128_split(X, W, Y, nullptr, M, N, K, 2, s)) {

@@ -7,8 +7,8 @@
 // TM, TN multiples of 32 (64 ... 256 rows, 32 ... 192 columns) and the
 // candidate whose tile count lands at or just under the CU count is chosen
 // by the measured plan (tools/tune_gemm_plan.py, code 3 + "flex" index);
-// each workgroup walks the whole K, the epilogue (plain / + residual) is
-// applied in registers, no workspace.
+// each workgroup walks the whole K, the epilogue (plain / + residual /
+// SwiGLU) is applied in registers, no workspace.
 //
 // Structure = the 128^2 kernel (gemm.hip) generalised: 4 waves in a 2 x 2
 // grid, each (TM/2) x (TN/2) = (TM/32) x (TN/32) v_mfma_f32_16x16x32_bf16
@@ -23,7 +23,41 @@ namespace {
 
 constexpr int FBK = 64;
 
-template <int EPI, int TM, int TN>     // EPI: 0 plain, 1 + residual
+// SwiGLU epilogue (EPI 2): W rows interleaved [gate 16 | up 16] per 32-row
+// group, so a wave's column tiles 2p / 2p + 1 hold gate / up of the same 4
+// features in the same lane (as gemm.hip's 128^2 kernel); Y is [M, N / 2],
+// the fused RMSNorm row scale of the input applied first
+template <int MT, int NT>
+DEV void store_silu(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y, int M, int N, int mb,
+                    int nb, int fr, int fq, const NormEpi& ne) {
+  static_assert(NT % 2 == 0, "gate / up tile pairs");
+  const int F = N >> 1;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mb + mt * 16 + fr;
+    if (m >= M) continue;
+    const float rs = norm_row_scale(ne, m);
+#pragma unroll
+    for (int p = 0; p < NT / 2; ++p) {
+      const int f = (nb >> 1) + p * 16 + fq * 4;
+      if (f >= F) continue;
+      const f32x4 gv = acc[mt][2 * p] * rs, uv = acc[mt][2 * p + 1] * rs;
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
+      *reinterpret_cast<bf16x4*>(Y + (size_t)m * F + f) = o;
+    }
+  }
+}
+
+template <int EPI, int MT, int NT>
+DEV void flex_store(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y, const bf16* __restrict__ R,
+                    int M, int N, int mb, int nb, int fr, int fq, const NormEpi& ne) {
+  if constexpr (EPI == 2) store_silu<MT, NT>(acc, Y, M, N, mb, nb, fr, fq, ne);
+  else store_direct<EPI>(acc, Y, R, M, N, mb, nb, fr, fq, ne);
+}
+
+template <int EPI, int TM, int TN>     // EPI: 0 plain, 1 + residual, 2 SwiGLU
 __global__ __launch_bounds__(256, 2) void gemm_tn_flex(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
@@ -112,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_flex(const bf16* __restrict__ 
   }
 
   // ---- epilogue: lane holds Y[m][n .. n+3]
-  store_direct<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
+  flex_store<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
 }
 
 // One workgroup per CU, NST LDS stages with NST - 2 k-tiles in flight across
@@ -214,28 +248,35 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_flexp(const bf16* __restrict__
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the trailing re-loads land before exit
 
-  store_direct<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
+  flex_store<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
 }
 
-template <int TM, int TN>
-void flex_launch(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                 hipStream_t s, int pipe) {
+template <int EPI, int TM, int TN>
+void flex_launch_epi(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                     hipStream_t s, int pipe) {
   const dim3 grid(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
-  if (pipe) {
-    if (R)
-      gemm_tn_flexp<1, TM, TN, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+  if (pipe)
+    gemm_tn_flexp<EPI, TM, TN, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
                                                        (const bf16*)R, M, N, K, norm_epi());
-    else
-      gemm_tn_flexp<0, TM, TN, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                       nullptr, M, N, K, norm_epi());
-    return;
-  }
-  if (R)
-    gemm_tn_flex<1, TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                 (const bf16*)R, M, N, K, norm_epi());
   else
-    gemm_tn_flex<0, TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y, nullptr,
-                                                 M, N, K, norm_epi());
+    gemm_tn_flex<EPI, TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                   (const bf16*)R, M, N, K, norm_epi());
+}
+
+// epi 2 only for tiles whose per-wave column span holds whole gate | up pairs
+template <int TM, int TN>
+int flex_launch(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                hipStream_t s, int pipe, int epi) {
+  if (epi == 2) {
+    if constexpr ((TN / 2) % 32 == 0) {
+      flex_launch_epi<2, TM, TN>(X, W, Y, nullptr, M, N, K, s, pipe);
+      return 0;
+    }
+    return 3;
+  }
+  if (epi == 1) flex_launch_epi<1, TM, TN>(X, W, Y, R, M, N, K, s, pipe);
+  else flex_launch_epi<0, TM, TN>(X, W, Y, nullptr, M, N, K, s, pipe);
+  return 0;
 }
 
 }  // namespace
@@ -253,26 +294,38 @@ int gemm_flex_tiles(int cand, int M, int N) {
          ((N + kFlexTiles[cand][1] - 1) / kFlexTiles[cand][1]);
 }
 
-// 0 ok; 1 unknown candidate; 2 shape (K % 64, N % 4)
-// cand + 32: the 4-stage one-workgroup-per-CU form
-int launch_gemm_flex(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
-                     int cand, hipStream_t s) {
-  if (K % FBK || N % 4 || M <= 0) return 2;
+// 0 ok; 1 unknown candidate; 2 shape (K % 64, N % 4; SwiGLU N % 64);
+// 3 the candidate has no SwiGLU form.  cand + 32: the 4-stage
+// one-workgroup-per-CU form.  epi: 0 plain, 1 + residual R, 2 SwiGLU (Y [M, N/2])
+int launch_gemm_flex_epi(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                         int K, int cand, int epi, hipStream_t s) {
+  if (K % FBK || N % 4 || M <= 0 || (epi == 2 && N % 64)) return 2;
   const int pipe = cand >= 32;
   cand &= 31;
   switch (cand) {
-    case 0: flex_launch<64, 64>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 1: flex_launch<64, 128>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 2: flex_launch<64, 160>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 3: flex_launch<96, 64>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 4: flex_launch<96, 128>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 5: flex_launch<128, 96>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 6: flex_launch<128, 128>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 7: flex_launch<128, 160>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 8: flex_launch<128, 192>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 9: flex_launch<256, 32>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 10: flex_launch<192, 128>(X, W, Y, R, M, N, K, s, pipe); return 0;
-    case 11: flex_launch<160, 128>(X, W, Y, R, M, N, K, s, pipe); return 0;
+    case 0: return flex_launch<64, 64>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 1: return flex_launch<64, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 2: return flex_launch<64, 160>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 3: return flex_launch<96, 64>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 4: return flex_launch<96, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 5: return flex_launch<128, 96>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 6: return flex_launch<128, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 7: return flex_launch<128, 160>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 8: return flex_launch<128, 192>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 9: return flex_launch<256, 32>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 10: return flex_launch<192, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 11: return flex_launch<160, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
     default: return 1;
   }
+}
+
+int launch_gemm_flex(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                     int cand, hipStream_t s) {
+  return launch_gemm_flex_epi(X, W, Y, R, M, N, K, cand, R ? 1 : 0, s);
+}
+
+// 1 if candidate cand (any form) has a SwiGLU epilogue
+int gemm_flex_silu_ok(int cand) {
+  cand &= 31;
+  return cand >= 0 && cand < gemm_flex_count() && (kFlexTiles[cand][1] / 2) % 32 == 0;
 }

@@ -43,6 +43,9 @@ void launch_add_inplace(void* y, const void* x, size_t n, hipStream_t s);
 // serving-size M: tile shape per (M, N) filling one wave of workgroups (gemm_flex.hip)
 int launch_gemm_flex(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                      int cand, hipStream_t s);
+int launch_gemm_flex_epi(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                         int K, int cand, int epi, hipStream_t s);   // epi 2: SwiGLU
+int gemm_flex_silu_ok(int cand);
 int gemm_flex_count();
 void gemm_plan_set_flex(int N, int K, const int* flex, int n);
 int gemm_plan_flex(int M, int N, int K);

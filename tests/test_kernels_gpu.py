@@ -1043,3 +1043,34 @@ def test_decode_kernel_own_span_mode(own_keys, q_lens, mode, monkeypatch):
         assert rel_err(out, exp) < 2e-2, (own_keys, q_lens)
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M", [100, 257, 640])
+def test_gemm_flex_swiglu(M):
+    """The SwiGLU epilogue of every flex tile that has one (per-wave column
+    spans of whole gate | up pairs), 2- and 4-stage forms, routed by a plan
+    "flex" entry through ops.gemm_silu, with and without the fused RMSNorm
+    row scale, against fp32 - ragged M included."""
+    torch.manual_seed(17)
+    L = ops.lib()
+    H, F, eps = 512, 1536, 1e-5
+    N = 2 * F
+    x = (torch.randn(M, H, device=DEV) * 2).bfloat16()
+    Wg = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    g, u = ref.deinterleave_gate_up(Wg.float())
+    e_plain = torch.nn.functional.silu(x.float() @ g.t()) * (x.float() @ u.t())
+    ss = ref.row_sumsq(x.cpu()).to(DEV)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps)
+    e_norm = torch.nn.functional.silu(xn @ g.t()) * (xn @ u.t())
+    cands = [c for c in range(L.gemm_flex_count()) if L.gemm_flex_silu_ok(c)]
+    assert cands
+    try:
+        for c in cands + [32 + c for c in cands]:
+            L.gemm_plan_set(N, H, [0] * 16)
+            L.gemm_plan_set_flex(N, H, [c] * 16)
+            assert L.gemm_plan_flex(M, N, H) == c
+            assert rel_err(ops.gemm_silu(x, Wg), e_plain) < 2e-2, c
+            assert rel_err(ops.gemm_silu(x, Wg, ss_in=ss, eps=eps), e_norm) < 2e-2, c
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)

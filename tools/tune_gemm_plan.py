@@ -139,8 +139,10 @@ for (N, K) in SHAPES:
         if M >= M_MIN and K % 128 == 0 and N % 256 == 0:
             cands += [(c, -1) for c in (1, 2, 3, 4, 5)]
         fl = []
-        if FLEX_MIN <= M <= FLEX_MAX and N not in SWIGLU_N:   # gate|up runs the SwiGLU epilogue
-            fl = [("flex", f) for f in list(range(NFLEX)) + [32 + f for f in range(NFLEX)]]
+        if FLEX_MIN <= M <= FLEX_MAX:
+            # gate|up (SwiGLU epilogue): only tiles whose waves hold whole gate | up pairs
+            fcands = [f for f in range(NFLEX) if N not in SWIGLU_N or L.gemm_flex_silu_ok(f)]
+            fl = [("flex", f) for f in fcands + [32 + f for f in fcands]]
         allc = cands + fl + [("lib", -1)]
         best = {c: float("inf") for c in allc}
         for _ in range(3):
