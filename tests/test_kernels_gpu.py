@@ -1045,7 +1045,7 @@ def test_decode_kernel_own_span_mode(own_keys, q_lens, mode, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("M", [100, 257, 640])
+@pytest.mark.parametrize("M", [136, 257, 640])
 def test_gemm_flex_swiglu(M):
     """The SwiGLU epilogue of every flex tile that has one (per-wave column
     spans of whole gate | up pairs), 2- and 4-stage forms, routed by a plan

@@ -2,14 +2,24 @@
 shapes present in ``src`` replace those of ``dst``; keys of an existing shape
 that ``src`` lacks (e.g. the "lib" buckets) are kept.
 
-    python tools/merge_gemm_plan.py src.json [dst.json]
+    python tools/merge_gemm_plan.py src.json [dst.json] [--keys flex,...]
+
+``--keys``: fold only those per-bucket arrays, bucket by bucket over the
+buckets ``src`` measured (a short ``src`` overwrites the prefix), keeping every
+other key of ``dst``.
 """
 import json
 import os
 import sys
 
-src = json.load(open(sys.argv[1]))
-dst_path = sys.argv[2] if len(sys.argv) > 2 else os.path.join(
+args = sys.argv[1:]
+keys = None
+if "--keys" in args:
+    i = args.index("--keys")
+    keys = args[i + 1].split(",")
+    del args[i:i + 2]
+src = json.load(open(args[0]))
+dst_path = args[1] if len(args) > 1 else os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "..",
     "autonomous-microservice-composition-via-llm-agents-in-an-mcp-control-plane_amd", "ops",
     "gemm_plan_gfx950.json")
@@ -18,7 +28,14 @@ assert src["arch"] == dst["arch"] and src["mstep"] == dst["mstep"]
 by = {(s["N"], s["K"]): s for s in dst["shapes"]}
 for s in src["shapes"]:
     old = by.get((s["N"], s["K"]), {})
-    by[(s["N"], s["K"])] = {**old, **s}
+    if keys is None:
+        by[(s["N"], s["K"])] = {**old, **s}
+        continue
+    assert old, f"--keys needs the shape in dst: {(s['N'], s['K'])}"
+    for k in keys:
+        cur = list(old.get(k, [-1] * len(old["codes"])))
+        cur[:len(s[k])] = s[k]
+        old[k] = cur
 dst["shapes"] = list(by.values())
 for k, v in src.items():
     if k not in ("shapes", "generated"):

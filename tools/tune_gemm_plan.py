@@ -66,6 +66,10 @@ for spec in MODEL.split("+"):
             SHAPES.append(sh)
         if i == 2:
             SWIGLU_N.add(sh[0])
+# MCP_TUNE_SHAPES=swiglu: time the gate|up shapes only (merge their "flex" key
+# into the shipped plan with tools/merge_gemm_plan.py --keys flex)
+if os.environ.get("MCP_TUNE_SHAPES") == "swiglu":
+    SHAPES = [sh for sh in SHAPES if sh[0] in SWIGLU_N]
 MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
