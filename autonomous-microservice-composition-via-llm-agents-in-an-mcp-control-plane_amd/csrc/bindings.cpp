@@ -698,6 +698,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_stream_force_splits", &gemm_stream_force_splits, "split count of the K2 stream kernel: 0 auto");
   m.def("gemm_stream_splits", &gemm_stream_splits);
   m.def("gemm_splitk_force", &gemm_splitk_force, "split-K count of the 128^2 path: -1 auto, <= 1 off, S forced");
+  m.def("gemm_skinny_half", &gemm_skinny_half, "SwiGLU skinny form: 8 gate + 8 up rows per block at M <= 4 (1, default), always (2), never (0: 32-row blocks)");
   m.def("gemm_silu", &gemm_silu, py::arg("X"), py::arg("W"), py::arg("Y"),
         py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("gemm_f32out", &gemm_f32out);

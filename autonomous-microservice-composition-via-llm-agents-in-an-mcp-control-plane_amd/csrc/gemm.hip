@@ -532,8 +532,14 @@ static bool skinny_first(int M, int N, int K) {
     const char* e = getenv("MCP_GEMM_SKINNY_FIRST");
     on = e ? atoi(e) : 1;
   }
+  // wide (gate|up) projections: skinny up to MCP_GEMM_SKINNY_WIDE_MAXM rows
+  static const int wide = getenv("MCP_GEMM_SKINNY_WIDE_MAXM") ? atoi(getenv("MCP_GEMM_SKINNY_WIDE_MAXM")) : 8;
   // o-proj sized (N, K <= 4096): skinny up to 16 rows (8.0-10.0 vs 7.8-10.5 us)
-  return on && (M <= 4 || (N >= 16384 && M <= 8) || (N <= 4096 && K <= 4096 && M <= 16));
+  // tall-K projections (down: K >= 2 N) go to the split-K stream kernel even at
+  // M <= 4: N / 16 workgroups each walking all of K lose to it (4096 x 14336,
+  // M = 1-4: 28.1-29.2 vs 23.6-23.8 us cold, profiles/gemm_decode_probe_r4.jsonl)
+  const bool tall = gemm_stream_rule() != 0 && K >= 2 * N;
+  return on && ((M <= 4 && !tall) || (N >= 16384 && M <= wide) || (N <= 4096 && K <= 4096 && M <= 16));
 }
 
 void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,

@@ -10,10 +10,14 @@
 //    and its up group), so N = 4096 launches 256 x 8 waves;
 //  * the waves split K (128-deep steps, strided) and reduce through LDS;
 //  * no LDS staging of W: v_mfma_f32_16x16x32_bf16 takes W straight from
-//    registers.  Lane l = (row r = l&15, group g = l>>4) loads 64 contiguous
-//    bytes W[r][s*128 + 32g .. +32) per step; the X fragment uses the SAME
-//    k permutation (a dot product is order-free), so MFMA j consumes the 8-wide
-//    chunk j of every lane group and four MFMAs cover the 128-k step;
+//    registers.  Lane l = (row r = l&15, group g = l>>4) loads
+//    W[r][s*128 + 32j + 8g .. +8) with load j = 0..3, so each load instruction
+//    reads 64 contiguous bytes of each of 16 rows (the 4 lane groups of a row
+//    together), and MFMA j consumes k = 32j .. 32j + 31 of the step; the X
+//    fragment uses the same offsets.  (The earlier order, 64 contiguous bytes
+//    per LANE over the 4 loads, sent each instruction to 64 scattered 16-B
+//    pieces: the activation rows' share of that request traffic cost up to
+//    12 us of a 52 us gate|up at M = 8, profiles/gemm_decode_probe_r4.jsonl);
 //  * the next step's W is loaded before this step's MFMAs (register double
 //    buffer) to keep ~8 KiB per wave in flight;
 //  * M > 64 runs ceil(M/64) token groups as extra workgroups placed on the
@@ -26,12 +30,18 @@ namespace {
 constexpr int SK_WAVES = 8;
 constexpr int SK_STEP = 128;
 
-template <int RB>
+// NT: non-temporal weight loads (MI355X_MICROARCH.md "nt-weights": a decode
+// step streams every weight once, from cold caches)
+template <int RB, bool NT>
 DEV void load_w(const bf16* const (&wrow)[RB], int k, bf16x8 (&w)[RB][4]) {
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[rb][j] = *reinterpret_cast<const bf16x8*>(wrow[rb] + k + 8 * j);
+    for (int j = 0; j < 4; ++j) {
+      const bf16x8* p = reinterpret_cast<const bf16x8*>(wrow[rb] + k + 32 * j);
+      if constexpr (NT) w[rb][j] = __builtin_nontemporal_load(p);
+      else w[rb][j] = *p;
+    }
 }
 
 // WV waves per workgroup split K (wave w takes steps w, w + WV, ...), each
@@ -39,13 +49,20 @@ DEV void load_w(const bf16* const (&wrow)[RB], int k, bf16x8 (&w)[RB][4]) {
 // next step is loaded while this one computes).  The SwiGLU shape (32 rows
 // per workgroup, gate|up = 235 MB) streams best with few waves per row group
 // and a deep ring was the hypothesis - measured no faster (launch_mb).
-template <int EPI, int MB, int WV, int DEPTH>
+// HALF (SwiGLU only): a workgroup owns 8 output features - 8 gate rows and
+// their 8 up rows in ONE 16-row MFMA block (lanes r < 8 read gate rows, r >= 8
+// up rows; the accumulator's rows 8..15 sit 32 lanes above rows 0..7), so the
+// gate|up GEMM launches N / 16 workgroups like the plain one (1,792 for
+// Llama-3-8B: 7 per CU) instead of N / 32 (896: 3.5 per CU, the CUs holding 4
+// set the time).
+template <int EPI, int MB, int WV, int DEPTH, bool NT, bool HALF>
 __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ X,
                                                    const bf16* __restrict__ W,
                                                    bf16* __restrict__ Y,
                                                    const bf16* __restrict__ R, int M, int N, int K,
-                                                   int nx, int ny, const NormEpi ne) {
-  constexpr int RB = EPI == 2 ? 2 : 1;               // 16-row weight blocks per workgroup
+                                                   int nx, int ny, const NormEpi ne, int mload) {
+  static_assert(!HALF || EPI == 2, "HALF is a SwiGLU form");
+  constexpr int RB = EPI == 2 && !HALF ? 2 : 1;      // 16-row weight blocks per workgroup
   __shared__ f32x4 red[WV][RB][MB][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -55,10 +72,14 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
 
   const bf16* wrow[RB];
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb) wrow[rb] = W + (size_t)min(n0 + rb * 16 + r, N - 1) * K + 32 * g;
+  for (int rb = 0; rb < RB; ++rb) {
+    // HALF: block bx = features 8 bx .. + 8 = pair bx / 2 (32 rows: 16 gate, 16 up), half bx & 1
+    const int row = HALF ? 32 * (bx >> 1) + 8 * (bx & 1) + (r & 7) + 16 * (r >> 3) : n0 + rb * 16 + r;
+    wrow[rb] = W + (size_t)min(row, N - 1) * K + 8 * g;
+  }
   const bf16* xrow[MB];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) xrow[mb] = X + (size_t)min(m0 + mb * 16 + r, M - 1) * K + 32 * g;
+  for (int mb = 0; mb < MB; ++mb) xrow[mb] = X + (size_t)min(m0 + mb * 16 + r, mload - 1) * K + 8 * g;
 
   f32x4 acc[RB][MB];
 #pragma unroll
@@ -71,7 +92,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
   bf16x8 wr[DEPTH][RB][4];
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
-    if (d < count) load_w<RB>(wrow, (wave + d * WV) * SK_STEP, wr[d]);
+    if (d < count) load_w<RB, NT>(wrow, (wave + d * WV) * SK_STEP, wr[d]);
   for (int i0 = 0; i0 < count; i0 += DEPTH) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
@@ -83,14 +104,14 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
         for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            x[mb][j] = *reinterpret_cast<const bf16x8*>(xrow[mb] + s * SK_STEP + 8 * j);
+            x[mb][j] = *reinterpret_cast<const bf16x8*>(xrow[mb] + s * SK_STEP + 32 * j);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
             for (int mb = 0; mb < MB; ++mb) acc[rb][mb] = mfma16x16x32(wr[d][rb][j], x[mb][j], acc[rb][mb]);
-        if (i + DEPTH < count) load_w<RB>(wrow, (s + DEPTH * WV) * SK_STEP, wr[d]);
+        if (i + DEPTH < count) load_w<RB, NT>(wrow, (s + DEPTH * WV) * SK_STEP, wr[d]);
       }
     }
   }
@@ -113,6 +134,23 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
     }
     // C layout: lane holds rows (weight n) 4g..4g+3 of column (token) r
     const int m = m0 + mb * 16 + r;
+    if constexpr (HALF) {
+      // lanes g < 2: gate features 8 bx + 4 g + q; the up values of the same
+      // features sit in lane + 32 (rows 8 + 4 g + q)
+      f32x4 up;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) up[q] = __shfl_xor(tot[0][q], 32, 64);
+      if (m >= M || g >= 2) continue;
+      const float rs = norm_row_scale(ne, m);
+      bf16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float gv = tot[0][q] * rs, uv = up[q] * rs;
+        o[q] = (bf16)(gv / (1.f + __expf(-gv)) * uv);
+      }
+      *reinterpret_cast<bf16x4*>(Y + (size_t)m * (N >> 1) + 8 * bx + 4 * g) = o;
+      continue;
+    }
     if (m >= M) continue;                            // all four g lanes of token r together
     if constexpr (EPI == 2) {
       const int F = N >> 1, f = (n0 >> 1) + 4 * g;   // f < F: N % 32 == 0 (skinny_ok)
@@ -147,13 +185,29 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
   }
 }
 
-template <int EPI, int MB, int WV, int DEPTH>
+// SwiGLU form: 1 = HALF at M <= 4 (default), 2 = HALF always, 0 = 32-row blocks.
+// Cold weights (tools/bench_swiglu_decode.py, profiles/gemm_swiglu_decode_r4.jsonl):
+// HALF 40.3-41.1 vs 43.2-43.6 us on 8B gate|up at M = 1-4, equal at 8-16 there,
+// but 167 vs 156 us on 70B gate|up at M = 8
+int g_skinny_half = -1;
+
+template <int EPI, int MB, int WV, int DEPTH, bool HALF>
 void launch_form(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                  hipStream_t s) {
-  constexpr int RB = EPI == 2 ? 2 : 1;
+  constexpr int RB = EPI == 2 && !HALF ? 2 : 1;
   const int nx = (N + 16 * RB - 1) / (16 * RB), ny = (M + 16 * MB - 1) / (16 * MB);
-  gemm_skinny<EPI, MB, WV, DEPTH><<<nx * ny, 64 * WV, 0, s>>>(
-      (const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, nx, ny, norm_epi());
+  // non-temporal weight loads: measured 12-19 % slower end to end (config 2,
+  // profiles/gemm_decode_nt_r4_ab.txt); kept selectable
+  static const int nt = getenv("MCP_GEMM_SKINNY_NT") ? atoi(getenv("MCP_GEMM_SKINNY_NT")) : 0;
+  // timing probe only (wrong results): every token row loads row 0 of X
+  static const int x1 = getenv("MCP_PROBE_SKINNY_X1") ? atoi(getenv("MCP_PROBE_SKINNY_X1")) : 0;
+  const int mload = x1 ? 1 : M;
+  if (nt)
+    gemm_skinny<EPI, MB, WV, DEPTH, true, HALF><<<nx * ny, 64 * WV, 0, s>>>(
+        (const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, nx, ny, norm_epi(), mload);
+  else
+    gemm_skinny<EPI, MB, WV, DEPTH, false, HALF><<<nx * ny, 64 * WV, 0, s>>>(
+        (const bf16*)X, (const bf16*)W, (bf16*)Y, (const bf16*)R, M, N, K, nx, ny, norm_epi(), mload);
 }
 
 template <int EPI, int MB>
@@ -161,7 +215,13 @@ void launch_mb(const void* X, const void* W, void* Y, const void* R, int M, int 
                hipStream_t s) {
   // 8 waves x a 1-deep ring: 2 x 2, 4 x 2 and 4 x 4 measured no faster at
   // M = 1-16 on any Llama-3-8B shape, cold weights (profiles/gemm_skinny_forms_r3.jsonl)
-  launch_form<EPI, MB, SK_WAVES, 1>(X, W, Y, R, M, N, K, s);
+  if (g_skinny_half < 0) {
+    const char* e = getenv("MCP_GEMM_SKINNY_HALF");
+    g_skinny_half = e ? atoi(e) : 1;
+  }
+  if (EPI == 2 && (g_skinny_half == 2 || (g_skinny_half == 1 && M <= 4)))
+    launch_form<EPI, MB, SK_WAVES, 1, EPI == 2>(X, W, Y, R, M, N, K, s);
+  else launch_form<EPI, MB, SK_WAVES, 1, false>(X, W, Y, R, M, N, K, s);
 }
 
 template <int EPI>
@@ -173,6 +233,8 @@ void launch_epi(const void* X, const void* W, void* Y, const void* R, int M, int
 }
 
 }  // namespace
+
+void gemm_skinny_half(int on) { g_skinny_half = on; }
 
 int skinny_ok(int M, int N, int K, int epi) {
   if (M <= 0 || M > SKINNY_MAX_M || K % SK_STEP) return 0;

@@ -333,6 +333,12 @@ int g_stream_force_s = 0;      // tuning: > 0 forces the split count
 
 }  // namespace
 
+// MCP_STREAM_SPLIT_RULE=0: the round-3 split rule and skinny-first test (A/B)
+int gemm_stream_rule() {
+  static const int r = getenv("MCP_STREAM_SPLIT_RULE") ? atoi(getenv("MCP_STREAM_SPLIT_RULE")) : 1;
+  return r;
+}
+
 void gemm_stream_force_splits(int S) { g_stream_force_s = S; }
 
 // split count: fill two workgroups per CU with >= 4 k-steps per wave, S <= 8,
@@ -344,9 +350,19 @@ int gemm_stream_splits(int M, int N, int K, int epi) {
   // wide projections (gate|up, 448 tiles): measured with cold weights
   // (tools/bench_cold_stream.py) S = 3 at M <= 16, no split above
   if (tiles >= 256) return M <= 16 ? 3 : 1;
-  const int target = 2 * gemm256_num_cus();
+  if (gemm_stream_rule() == 0) {                     // round-3 rule (A/B)
+    const int target = 2 * gemm256_num_cus();
+    int S = 1;
+    while (S < 8 && tiles * S * 2 <= target + tiles && nsteps / (2 * S) >= 4 * SW_WAVES) S *= 2;
+    return S;
+  }
+  // about one workgroup per CU (<= 1.5 per CU), >= 4 k-steps per wave:
+  // cold-weight sweep (tools/bench_decode_probe.py, profiles/gemm_decode_probe_r4.jsonl):
+  // down 4096 x 14336 S = 4 23.6-24.4 us vs S = 8 24.7-25.6; o S = 4 best;
+  // qkv S = 4 13.7-14.6 vs S = 2 14.2-15.0, S = 8 16.9-17.4
+  const int G = gemm256_num_cus();
   int S = 1;
-  while (S < 8 && tiles * S * 2 <= target + tiles && nsteps / (2 * S) >= 4 * SW_WAVES) S *= 2;
+  while (S < 8 && 2 * tiles * S * 2 <= 3 * G && nsteps / (2 * S) >= 4 * SW_WAVES) S *= 2;
   (void)M;
   (void)epi;
   return S;

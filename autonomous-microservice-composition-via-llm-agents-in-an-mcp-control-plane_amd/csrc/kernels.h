@@ -79,6 +79,8 @@ void launch_copy_blocks(void* data, const int* src, const int* dst, int npairs, 
 
 // gemm_skinny.hip (K2): decode-sized M, weight-streaming; epi 0 plain, 1 +R, 2 SwiGLU
 #define SKINNY_MAX_M 128
+void gemm_skinny_half(int on);   // SwiGLU skinny form: 8+8-row blocks at M <= 4 (1), always (2), never (0)
+int gemm_stream_rule();          // 1: round-4 stream split rule / skinny-first test, 0: round 3
 int skinny_ok(int M, int N, int K, int epi);
 int launch_gemm_skinny(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                        int epi, hipStream_t s);

@@ -582,6 +582,31 @@ def test_gemm_skinny(M, N, K):
     assert rel_err(ops.gemm_silu(X, Wi), e) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("half", [2, 0])
+def test_gemm_skinny_swiglu_forms(M, half):
+    """Both SwiGLU forms of the skinny kernel (8 gate + 8 up rows per block,
+    default; 32-row blocks) at decode M on a wide gate|up (N >= 16384 goes to
+    the skinny kernel up to M = 8), with and without the fused RMSNorm row
+    scale, against fp32."""
+    torch.manual_seed(23)
+    L = ops.lib()
+    H, F, eps = 512, 8192, 1e-5
+    x = (torch.randn(M, H, device=DEV) * 2).bfloat16()
+    Wg = (torch.randn(2 * F, H, device=DEV) / math.sqrt(H)).bfloat16()
+    g, u = ref.deinterleave_gate_up(Wg.float())
+    e_plain = torch.nn.functional.silu(x.float() @ g.t()) * (x.float() @ u.t())
+    ss = ref.row_sumsq(x.cpu()).to(DEV)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps)
+    e_norm = torch.nn.functional.silu(xn @ g.t()) * (xn @ u.t())
+    try:
+        L.gemm_skinny_half(half)
+        assert rel_err(ops.gemm_silu(x, Wg), e_plain) < 2e-2
+        assert rel_err(ops.gemm_silu(x, Wg, ss_in=ss, eps=eps), e_norm) < 2e-2
+    finally:
+        L.gemm_skinny_half(1)
+
+
 @pytest.mark.parametrize("M,N,K", [(2600, 4096, 4096), (100, 512, 256), (513, 1024, 384),
                                    (4096, 6144, 4096)])
 def test_gemm_256d_agpr(M, N, K):
