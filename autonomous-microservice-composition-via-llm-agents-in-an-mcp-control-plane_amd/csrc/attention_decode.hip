@@ -374,7 +374,11 @@ int* attn_split_counters();   // attention.hip
 // tiles per wave for a block-table width: <= 64 blocks per (item, kv head)
 int attn_decode_tpw(int max_blocks) {
   const int per_pass = NWV * 64;
-  return max_blocks <= per_pass ? 1 : (max_blocks + per_pass - 1) / per_pass;
+  const int tpw = max_blocks <= per_pass ? 1 : (max_blocks + per_pass - 1) / per_pass;
+  // MCP_ATTN_DECODE_TPW: at least this many tiles per wave (fewer blocks to
+  // merge, more tiles walked per wave; A/B)
+  static const int force = getenv("MCP_ATTN_DECODE_TPW") ? atoi(getenv("MCP_ATTN_DECODE_TPW")) : 0;
+  return force > tpw ? force : tpw;
 }
 int attn_decode_blocks(int max_blocks) {
   const int C = NWV * attn_decode_tpw(max_blocks);
