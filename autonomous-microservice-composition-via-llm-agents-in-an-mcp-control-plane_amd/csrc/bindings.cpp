@@ -176,6 +176,16 @@ void gemm(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, const c10::op
   check_launch("gemm");
 }
 
+// read up to `nbytes` of W once on the current stream (MALL warm-up, prefetch.hip)
+void weight_prefetch(const at::Tensor& W, int64_t nbytes, int64_t wgs, at::Tensor& sink) {
+  TORCH_CHECK(W.is_cuda() && W.is_contiguous() && sink.is_cuda() && sink.dtype() == at::kInt &&
+              sink.numel() >= 256, "weight_prefetch: contiguous device tensor and an int32 sink of >= 256");
+  const int64_t total = W.numel() * W.element_size();
+  const int64_t n = nbytes < 0 || nbytes > total ? total : nbytes;
+  launch_prefetch(W.data_ptr(), (size_t)n, (int)wgs, sink.data_ptr<int>(), stream());
+  check_launch("weight_prefetch");
+}
+
 void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y,
                const c10::optional<at::Tensor>& ss_in, double norm_eps) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
@@ -699,6 +709,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_stream_splits", &gemm_stream_splits);
   m.def("gemm_splitk_force", &gemm_splitk_force, "split-K count of the 128^2 path: -1 auto, <= 1 off, S forced");
   m.def("gemm_skinny_half", &gemm_skinny_half, "SwiGLU skinny form: 8 gate + 8 up rows per block at M <= 4 (1, default), always (2), never (0: 32-row blocks)");
+  m.def("weight_prefetch", &weight_prefetch, py::arg("W"), py::arg("nbytes"), py::arg("wgs"), py::arg("sink"),
+        "read up to nbytes of W once on the current stream (Infinity Cache warm-up)");
   m.def("gemm_silu", &gemm_silu, py::arg("X"), py::arg("W"), py::arg("Y"),
         py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("gemm_f32out", &gemm_f32out);

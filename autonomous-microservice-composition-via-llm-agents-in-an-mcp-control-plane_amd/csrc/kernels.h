@@ -209,3 +209,6 @@ int rccl_reduce_scatter(void* comm, const void* send, void* recv, size_t count, 
 int rccl_broadcast(void* comm, void* buf, size_t count, int dtype, int root, hipStream_t s);
 const char* rccl_last_error(void* comm);
 void rccl_destroy(void* comm);
+
+// prefetch.hip: read a weight range once (MALL warm-up beside latency-bound work)
+int launch_prefetch(const void* p, size_t bytes, int wgs, int* sink, hipStream_t s);

@@ -46,6 +46,14 @@ import torch
 from .. import ops
 from ..ops import reference as ref
 
+# Infinity Cache weight prefetch beside the decode attention (measured A/B:
+# profiles/config2_decode_gemm_r4_ab.txt): on/off, largest step (tokens),
+# bytes read per layer (o-projection first, then the head of gate|up), grid
+_PF_ON = os.environ.get("MCP_WEIGHT_PREFETCH", "0") == "1"
+_PF_MAX_T = int(os.environ.get("MCP_WEIGHT_PREFETCH_MAX_T", "64"))
+_PF_BYTES = int(float(os.environ.get("MCP_WEIGHT_PREFETCH_MB", "64")) * (1 << 20))
+_PF_WGS = int(os.environ.get("MCP_WEIGHT_PREFETCH_WGS", "256"))
+
 
 @dataclasses.dataclass(frozen=True)
 class LlamaConfig:
@@ -295,6 +303,11 @@ class LlamaModel:
         self.cos_sin = ref.rope_cos_sin(cfg.max_pos, cfg.head_dim, cfg.rope_theta, self.device,
                                         cfg.rope_scaling)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        # weight prefetch: side stream and sink made here, never inside a capture
+        self._pf_side = None
+        if _PF_ON and self.device.type == "cuda":
+            self._pf_side = torch.cuda.Stream(device=self.device)
+            ops.weight_prefetch_init(self.device)
         self._allreduce = allreduce      # injectable (simulated ranks in tests)
         if tp > 1 and allreduce is None:
             from ..parallel.comm import make_allreduce
@@ -430,11 +443,24 @@ class LlamaModel:
         ss = torch.zeros(L + 1, 2, max(T, rows.numel()), dtype=torch.int64, device=x.device)
         ops.row_sumsq(x, ss[0, 0])
         q = torch.empty(T, self.hq, D, device=x.device, dtype=x.dtype)
+        side = self._prefetch_stream(x, T)
         for l in range(L):
             lw = self.w.layers[l]
             kc, vc = kv.layer(l)
             ops.qkv_rope(x, lw.wqkv, step.positions, step.slots, self.cos_sin, q, kc, vc,
                          self.hq, self.hkv, D, ss_in=ss[l, 0], eps=eps)
+            if side is not None:
+                # decode-sized step: while the (latency-bound) attention runs,
+                # a second stream reads the o-projection's weights and the head
+                # of gate|up once, so those GEMMs stream them from the Infinity
+                # Cache (csrc/prefetch.hip); joined after the layer
+                cur = torch.cuda.current_stream(x.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    ops.weight_prefetch(lw.wo, -1, _PF_WGS)
+                    rest = _PF_BYTES - lw.wo.numel() * lw.wo.element_size()
+                    if rest > 0:
+                        ops.weight_prefetch(lw.w_gate_up, rest, _PF_WGS)
             a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
             if l + 1 == L:
                 # last layer: only the sampled rows go on (see ``forward``)
@@ -447,4 +473,13 @@ class LlamaModel:
             x = ops.gemm(a.view(T, self.hq * D), lw.wo, R=x, out=x, ss_out=ss[l, 1])
             act = ops.gemm_silu(x, lw.w_gate_up, ss_in=ss[l, 1], eps=eps)
             x = ops.gemm(act, lw.w_down, R=x, out=x, ss_out=ss[l + 1, 0])
+            if side is not None:
+                torch.cuda.current_stream(x.device).wait_stream(side)
         return ops.rmsnorm(x, self.w.final_norm, eps)
+
+    def _prefetch_stream(self, x, T):
+        """The side stream of the weight prefetch (MCP_WEIGHT_PREFETCH=1) for
+        steps of at most _PF_MAX_T tokens, else None."""
+        if not (_PF_ON and x.is_cuda and T <= _PF_MAX_T):
+            return None
+        return self._pf_side

@@ -171,6 +171,30 @@ def gemm(X, W, R=None, out=None, algo: int = -1, ss_out=None):
     return r if out is None else out.copy_(r)
 
 
+_PF_SINK = {}
+
+
+def weight_prefetch(W, nbytes: int = -1, wgs: int = 256):
+    """Read up to ``nbytes`` of ``W`` once on the current stream, so a GEMM that
+    streams it next finds it in the Infinity Cache (csrc/prefetch.hip).  No-op
+    on CPU."""
+    if not W.is_cuda:
+        return
+    lib().weight_prefetch(W, int(nbytes), int(wgs), weight_prefetch_init(W.device))
+
+
+def weight_prefetch_init(device):
+    """The prefetch kernel's sink buffer for ``device`` (allocate it outside
+    hipGraph capture: the model does at construction)."""
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device(device.type, torch.cuda.current_device())
+    sink = _PF_SINK.get(device)
+    if sink is None:
+        sink = _PF_SINK[device] = torch.zeros(256, dtype=torch.int32, device=device)
+    return sink
+
+
 def gemm_silu(X, W, out=None, ss_in=None, eps: float = 0.0):
     """SwiGLU projection: silu(X Wg^T) * (X Wu^T) with W = interleave_gate_up(Wg, Wu)
     ([2F, K], 16-row groups); the activation is fused into the MFMA GEMM epilogue.

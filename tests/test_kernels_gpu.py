@@ -1099,3 +1099,31 @@ def test_gemm_flex_swiglu(M):
     finally:
         L.gemm_plan_clear()
         ops._load_gemm_plan(L)
+
+
+def test_weight_prefetch_in_graph():
+    """The Infinity Cache prefetch (csrc/prefetch.hip) runs eagerly and as a
+    forked side-stream branch of a captured hipGraph without touching its
+    input; the GEMM after it is unchanged."""
+    torch.manual_seed(31)
+    W = torch.randn(4096, 1024, device=DEV).bfloat16()
+    X = torch.randn(8, 1024, device=DEV).bfloat16()
+    W0 = W.clone()
+    ops.weight_prefetch_init(DEV)
+    ops.weight_prefetch(W, -1, 64)
+    ops.weight_prefetch(W, 12345, 8)                 # ragged length: the 16-B head only
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    out = torch.empty(8, 4096, device=DEV, dtype=torch.bfloat16)
+    with torch.cuda.graph(g):
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            ops.weight_prefetch(W, 1 << 20, 32)
+        ops.gemm(X, W, out=out)
+        cur.wait_stream(side)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(W, W0)
+    assert rel_err(out, ref.gemm(X, W)) < 1e-2
+
