@@ -255,10 +255,15 @@ template <int EPI, int TM, int TN>
 void flex_launch_epi(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                      hipStream_t s, int pipe) {
   const dim3 grid(((M + TM - 1) / TM) * ((N + TN - 1) / TN));
-  if (pipe)
-    gemm_tn_flexp<EPI, TM, TN, 4><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
-                                                       (const bf16*)R, M, N, K, norm_epi());
-  else
+  // tiles too tall for two workgroups per CU (TM + TN > 320: the whole-M
+  // tiles of wide projections, one W read per column panel) have only the
+  // one-workgroup-per-CU form, with as many stages as LDS holds
+  constexpr bool two = 2 * (TM + TN) * FBK * 2 <= 80 * 1024;
+  constexpr int NST = 4 * (TM + TN) * FBK * 2 <= 160 * 1024 ? 4 : 3;
+  if (pipe || !two)
+    gemm_tn_flexp<EPI, TM, TN, NST><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                         (const bf16*)R, M, N, K, norm_epi());
+  else if constexpr (two)
     gemm_tn_flex<EPI, TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
                                                    (const bf16*)R, M, N, K, norm_epi());
 }
@@ -284,7 +289,8 @@ int flex_launch(const void* X, const void* W, void* Y, const void* R, int M, int
 // candidate tiles (TM rows x TN columns); the index is what the plan records
 static const int kFlexTiles[][2] = {{64, 64},   {64, 128},  {64, 160},  {96, 64},
                                     {96, 128},  {128, 96},  {128, 128}, {128, 160},
-                                    {128, 192}, {256, 32},  {192, 128}, {160, 128}};
+                                    {128, 192}, {256, 32},  {192, 128}, {160, 128},
+                                    {256, 128}, {256, 64}};
 
 int gemm_flex_count() { return (int)(sizeof(kFlexTiles) / sizeof(kFlexTiles[0])); }
 
@@ -315,6 +321,8 @@ int launch_gemm_flex_epi(const void* X, const void* W, void* Y, const void* R, i
     case 9: return flex_launch<256, 32>(X, W, Y, R, M, N, K, s, pipe, epi);
     case 10: return flex_launch<192, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
     case 11: return flex_launch<160, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 12: return flex_launch<256, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
+    case 13: return flex_launch<256, 64>(X, W, Y, R, M, N, K, s, pipe, epi);
     default: return 1;
   }
 }

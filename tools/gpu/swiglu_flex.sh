@@ -5,7 +5,7 @@
 # and the headline, shipped vs candidate, alternated.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/${1:-r4ad}
+O=gpurun_out/${1:-r4as}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "flex" > $O/test.log 2>&1 || { echo "flex tests failed"; tail -30 $O/test.log; exit 1; }
 tail -1 $O/test.log
