@@ -289,8 +289,10 @@ int flex_launch(const void* X, const void* W, void* Y, const void* R, int M, int
 // candidate tiles (TM rows x TN columns); the index is what the plan records
 static const int kFlexTiles[][2] = {{64, 64},   {64, 128},  {64, 160},  {96, 64},
                                     {96, 128},  {128, 96},  {128, 128}, {128, 160},
-                                    {128, 192}, {256, 32},  {192, 128}, {160, 128},
-                                    {256, 128}, {256, 64}};
+                                    {128, 192}, {256, 32},  {192, 128}, {160, 128}};
+// (round 4: whole-M tiles 256 x 128 / 256 x 64 for the wide gate|up at M <=
+// 256, one W read per column panel, were timed by the tuner on every gate|up
+// shape and won no bucket - profiles/gemm_tuning.md)
 
 int gemm_flex_count() { return (int)(sizeof(kFlexTiles) / sizeof(kFlexTiles[0])); }
 
@@ -321,8 +323,6 @@ int launch_gemm_flex_epi(const void* X, const void* W, void* Y, const void* R, i
     case 9: return flex_launch<256, 32>(X, W, Y, R, M, N, K, s, pipe, epi);
     case 10: return flex_launch<192, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
     case 11: return flex_launch<160, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
-    case 12: return flex_launch<256, 128>(X, W, Y, R, M, N, K, s, pipe, epi);
-    case 13: return flex_launch<256, 64>(X, W, Y, R, M, N, K, s, pipe, epi);
     default: return 1;
   }
 }
