@@ -219,9 +219,22 @@ void launch_mb(const void* X, const void* W, void* Y, const void* R, int M, int 
     const char* e = getenv("MCP_GEMM_SKINNY_HALF");
     g_skinny_half = e ? atoi(e) : 1;
   }
-  if (EPI == 2 && (g_skinny_half == 2 || (g_skinny_half == 1 && M <= 4)))
+  if (EPI == 2 && (g_skinny_half == 2 || (g_skinny_half == 1 && M <= 4))) {
     launch_form<EPI, MB, SK_WAVES, 1, EPI == 2>(X, W, Y, R, M, N, K, s);
-  else launch_form<EPI, MB, SK_WAVES, 1, false>(X, W, Y, R, M, N, K, s);
+    return;
+  }
+  // MCP_GEMM_SKINNY_FORM (A/B after the round-4 load-order fix, M <= 16):
+  // 0 = 8 waves x 1-deep ring, 1 = 8 x 2, 2 = 4 x 2, 3 = 4 x 4
+  static const int form = getenv("MCP_GEMM_SKINNY_FORM") ? atoi(getenv("MCP_GEMM_SKINNY_FORM")) : 0;
+  if constexpr (MB == 1) {
+    switch (form) {
+      case 1: launch_form<EPI, MB, 8, 2, false>(X, W, Y, R, M, N, K, s); return;
+      case 2: launch_form<EPI, MB, 4, 2, false>(X, W, Y, R, M, N, K, s); return;
+      case 3: launch_form<EPI, MB, 4, 4, false>(X, W, Y, R, M, N, K, s); return;
+      default: break;
+    }
+  }
+  launch_form<EPI, MB, SK_WAVES, 1, false>(X, W, Y, R, M, N, K, s);
 }
 
 template <int EPI>
