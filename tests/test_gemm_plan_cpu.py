@@ -25,3 +25,29 @@ def test_plan_covers_every_shard_shape(model, tp):
         assert nk in have, (model, tp, nk)
         codes = have[nk]["codes"]
         assert len(codes) >= 64 and all(-1 <= c <= 5 for c in codes)
+
+
+def test_merge_keys_folds_only_named_buckets(tmp_path):
+    """tools/merge_gemm_plan.py --keys flex: a short source (the buckets it
+    measured) overwrites that key's prefix in the destination shape and leaves
+    every other key and bucket alone; a shape missing from dst is an error."""
+    import subprocess
+    import sys
+    tool = pathlib.Path(__file__).resolve().parents[1] / "tools" / "merge_gemm_plan.py"
+    dst = {"arch": "gfx950", "mstep": 64, "shapes": [
+        {"N": 64, "K": 64, "codes": [1, 2, 3, 4], "splits": [0, 0, 0, 0], "flex": [-1, -1, 5, 6]}]}
+    src = {"arch": "gfx950", "mstep": 64, "generated": "x", "shapes": [
+        {"N": 64, "K": 64, "codes": [9, 9], "splits": [8, 8], "flex": [7, -1]}]}
+    d, s = tmp_path / "dst.json", tmp_path / "src.json"
+    d.write_text(json.dumps(dst))
+    s.write_text(json.dumps(src))
+    subprocess.run([sys.executable, str(tool), str(s), str(d), "--keys", "flex"], check=True,
+                   capture_output=True)
+    out = json.loads(d.read_text())["shapes"][0]
+    assert out["flex"] == [7, -1, 5, 6]
+    assert out["codes"] == [1, 2, 3, 4] and out["splits"] == [0, 0, 0, 0]
+    src["shapes"][0]["N"] = 128
+    s.write_text(json.dumps(src))
+    r = subprocess.run([sys.executable, str(tool), str(s), str(d), "--keys", "flex"],
+                       capture_output=True)
+    assert r.returncode != 0
