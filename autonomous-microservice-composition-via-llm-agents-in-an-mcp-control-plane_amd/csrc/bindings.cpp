@@ -227,6 +227,14 @@ void gemm_plan_set_flex_py(int64_t N, int64_t K, const std::vector<int64_t>& fle
   gemm_plan_set_flex((int)N, (int)K, c.data(), (int)c.size());
 }
 
+void gemm_plan_set_fsplit_py(int64_t N, int64_t K, const std::vector<int64_t>& fs) {
+  std::vector<int> c(fs.begin(), fs.end());
+  for (int v : c)
+    TORCH_CHECK(v == -1 || (v >= 0 && v / 16 < 14 && v % 16 >= 2),
+                "gemm plan fsplit must be -1 or 16 cand + S (cand < 14, S >= 2)");
+  gemm_plan_set_fsplit((int)N, (int)K, c.data(), (int)c.size());
+}
+
 void gemm_plan_set_group_py(int64_t N, int64_t K, const std::vector<int64_t>& group) {
   std::vector<int> c(group.begin(), group.end());
   for (int v : c) TORCH_CHECK(v >= 0 && v <= 64, "gemm plan group must be 0..64");
@@ -682,6 +690,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_plan_set_splits", &gemm_plan_set_splits_py,
         "measured split-K of the 128^2 path for one (N, K): a count per 64-row M bucket (0 = rule)");
   m.def("gemm_plan_split", &gemm_plan_split);
+  m.def("gemm_plan_set_fsplit", &gemm_plan_set_fsplit_py,
+        "measured flex tile with split-K per 64-row M bucket for one (N, K) (16 cand + S; -1 = none)");
+  m.def("gemm_plan_fsplit", &gemm_plan_fsplit);
   m.def("gemm_plan_set_flex", &gemm_plan_set_flex_py,
         "measured flex tile per 64-row M bucket for one (N, K) (-1 = none; +32 = 4-stage form)");
   m.def("gemm_plan_flex", &gemm_plan_flex);

@@ -252,6 +252,7 @@ struct GemmPlan {
   std::vector<signed char> flex;     // measured flex tile (gemm_flex.hip) or -1
   std::vector<signed char> group;    // measured tile group of the AGPR kernel (0: default)
   std::vector<signed char> persist;  // 1: the persistent AGPR kernel (gemm256p.hip) measured faster
+  std::vector<short> fsplit;         // measured flex tile x split-K (16 cand + S) or -1
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -341,6 +342,30 @@ int gemm_plan_split(int M, int N, int K) {
       return b < p.split.size() ? p.split[b] : 0;
     }
   return 0;
+}
+
+void gemm_plan_set_fsplit(int N, int K, const int* fs, int n) {
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.fsplit.assign(fs, fs + n);
+      return;
+    }
+  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}};
+  q.fsplit.assign(fs, fs + n);
+  g_plans.push_back(std::move(q));
+}
+
+// measured flex tile with split-K for this M bucket: 16 cand + S, -1 = none
+// (MCP_GEMM_FSPLIT=0 disables)
+int gemm_plan_fsplit(int M, int N, int K) {
+  static const int on = getenv("MCP_GEMM_FSPLIT") ? atoi(getenv("MCP_GEMM_FSPLIT")) : 1;
+  if (!on) return -1;
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.fsplit.size() ? p.fsplit[b] : -1;
+    }
+  return -1;
 }
 
 void gemm_plan_clear() { g_plans.clear(); }
@@ -501,6 +526,24 @@ static bool launch_gemm_128_split(const void* X, const void* W, void* Y, const v
   return true;
 }
 
+// flex tile cand, S-way split-K through the fp32 workspace + the reduce
+// (epilogue 0/1/2); nonzero if unsupported or the workspace is too small
+int launch_gemm_flex_split(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                           int K, int cand, int S, int epi, hipStream_t s) {
+  if (!g_splitk_ws || (size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) return 4;
+  if (epi == 2 && N % 64) return 2;
+  const int rc = launch_gemm_flex_partials(X, W, g_splitk_ws, M, N, K, cand, S, s);
+  if (rc) return rc;
+  const size_t n4 = (size_t)M * (epi == 2 ? N / 2 : N) / 4;
+  const dim3 rg((unsigned)((n4 + 255) / 256));
+  switch (epi) {
+    case 0: splitk_reduce<0><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N, norm_epi()); break;
+    case 1: splitk_reduce<1><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, (const bf16*)R, M, N, norm_epi()); break;
+    default: splitk_reduce<2><<<rg, 256, 0, s>>>(g_splitk_ws, S, (bf16*)Y, nullptr, M, N, norm_epi()); break;
+  }
+  return 0;
+}
+
 static void launch_gemm_tn_128(const void* X, const void* W, void* Y, const void* R, int M, int N,
                                int K, hipStream_t s) {
   if (launch_gemm_128_split(X, W, Y, R, M, N, K, R ? 1 : 0, s)) return;
@@ -553,6 +596,13 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
   if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
       launch_gemm_skinny(X, W, Y, R, M, N, K, R ? 1 : 0, s) == 0)
     return;
+  // serving-size M: a flex tile with split-K through the fp32 workspace,
+  // measured faster than every other path for this bucket (plan "fsplit": the
+  // narrow projections at M = 65-512, e.g. down 4096 x 14336 at M = 320-384
+  // 59-64 vs 72-76 us, profiles/gemm_flex_split_r4.jsonl)
+  const int fs = gemm_plan_fsplit(M, N, K);
+  if (fs >= 0 && launch_gemm_flex_split(X, W, Y, R, M, N, K, fs / 16, fs % 16, R ? 1 : 0, s) == 0)
+    return;
   // serving-size M: a tile shape that fills one wave of workgroups, measured
   // faster than the 128^2 split-K / AGPR paths for this bucket (plan "flex")
   const int fx = gemm_plan_flex(M, N, K);
@@ -565,7 +615,11 @@ void launch_gemm_tn(const void* X, const void* W, void* Y, const void* R, int M,
 
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                          int algo, hipStream_t s) {
-  if (algo >= 16 && launch_gemm_flex(X, W, Y, R, M, N, K, algo - 16, s) == 0) return;   // tuning
+  // tuning: 1000 + 16 cand + S = flex tile cand with S-way split-K
+  if (algo >= 1000 && launch_gemm_flex_split(X, W, Y, R, M, N, K, (algo - 1000) / 16,
+                                             (algo - 1000) % 16, R ? 1 : 0, s) == 0)
+    return;
+  if (algo >= 16 && algo < 1000 && launch_gemm_flex(X, W, Y, R, M, N, K, algo - 16, s) == 0) return;   // tuning
   // 9..13: the AGPR kernel at the tile height of plan code algo - 8 (tuning)
   if (algo >= 9 && algo <= 13 &&
       launch_gemm_tn_256d_bm(X, W, Y, R, M, N, K, R ? 1 : 0, gemm256d_code_height(algo - 8), s) == 0)

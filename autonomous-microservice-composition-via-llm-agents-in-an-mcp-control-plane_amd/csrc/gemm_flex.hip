@@ -149,6 +149,108 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_flex(const bf16* __restrict__ 
   flex_store<EPI>(acc, Y, R, M, N, m0 + wm * (TM / 2), n0 + wn * (TN / 2), fr, fq, ne);
 }
 
+// Split-K form of the 2-stage flex tile: gridDim.y = S workgroups per tile
+// each walk K / S and write fp32 partials [S][M][N] (lane: Y[m][n .. n+3]);
+// gemm.hip's splitk_reduce sums them and applies the epilogue.  Serving-M
+// tiles that hold all M rows (W read once) but are too few to fill the chip.
+template <int TM, int TN>
+__global__ __launch_bounds__(256, 2) void gemm_tn_flex_sk(const bf16* __restrict__ X,
+                                                          const bf16* __restrict__ W,
+                                                          float* __restrict__ ws, int M, int N,
+                                                          int K) {
+  static_assert(TM % 32 == 0 && TN % 32 == 0, "tile dims are multiples of 32");
+  static_assert(2 * (TM + TN) * FBK * 2 <= 80 * 1024, "two workgroups per CU");
+  constexpr int MT = TM / 32, NT = TN / 32;
+  constexpr int PA = TM / 32, PB = TN / 32;
+  constexpr int AE = TM * FBK, BE = TN * FBK;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (AE + BE)];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nm = (M + TM - 1) / TM, nn = (N + TN - 1) / TN;
+  const int wg = xcd_remap(blockIdx.x, nm * nn);
+  const int tm = wg % nm, tn = wg / nm;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int klen = K / (int)gridDim.y, kbeg = (int)blockIdx.y * klen;
+  float* Yp = ws + (size_t)blockIdx.y * M * N;
+
+  const int lrow = lane >> 3;
+  const int lchunk = (lane & 7) ^ lrow;
+  const bf16* srcA[PA];
+  const bf16* srcB[PB];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int row = (wave * PA + i) * 8 + lrow;
+    srcA[i] = X + (size_t)min(m0 + row, M - 1) * K + kbeg + lchunk * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int row = (wave * PB + i) * 8 + lrow;
+    srcB[i] = W + (size_t)min(n0 + row, N - 1) * K + kbeg + lchunk * 8;
+  }
+  auto stage = [&](int kt, int buf) {
+    bf16* la = smem + buf * (AE + BE);
+    bf16* lb = la + AE;
+    const int koff = kt * FBK;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) glds16(srcA[i] + koff, la + (wave * PA + i) * 512);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) glds16(srcB[i] + koff, lb + (wave * PB + i) * 512);
+  };
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = klen / FBK;
+  stage(0, 0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const bf16* la = smem + cur * (AE + BE);
+    const bf16* lb = la + AE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;
+      bf16x8 af[MT], bfr[NT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int ra = wm * (TM / 2) + t * 16 + fr;
+        af[t] = *reinterpret_cast<const bf16x8*>(la + ra * FBK + ((c ^ (ra & 7)) << 3));
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int rb = wn * (TN / 2) + t * 16 + fr;
+        bfr[t] = *reinterpret_cast<const bf16x8*>(lb + rb * FBK + ((c ^ (rb & 7)) << 3));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(bfr[nt], af[mt], acc[mt][nt]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = m0 + wm * (TM / 2) + mt * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n0 + wn * (TN / 2) + nt * 16 + fq * 4;
+      if (n < N) *reinterpret_cast<f32x4*>(Yp + (size_t)m * N + n) = acc[mt][nt];
+    }
+  }
+}
+
+template <int TM, int TN>
+void flex_sk_launch(const void* X, const void* W, float* ws, int M, int N, int K, int S,
+                    hipStream_t s) {
+  const dim3 grid(((M + TM - 1) / TM) * ((N + TN - 1) / TN), S);
+  gemm_tn_flex_sk<TM, TN><<<grid, 256, 0, s>>>((const bf16*)X, (const bf16*)W, ws, M, N, K);
+}
+
 // One workgroup per CU, NST LDS stages with NST - 2 k-tiles in flight across
 // a raw s_barrier and a counted vmcnt: ONE barrier per k-tile (the 2-stage
 // loop above drains vmcnt(0) every k-tile - at one wave of workgroups each
@@ -330,6 +432,30 @@ int launch_gemm_flex_epi(const void* X, const void* W, void* Y, const void* R, i
 int launch_gemm_flex(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                      int cand, hipStream_t s) {
   return launch_gemm_flex_epi(X, W, Y, R, M, N, K, cand, R ? 1 : 0, s);
+}
+
+// fp32 split-K partials [S][M][N] of flex tile cand (2-stage form) into ws;
+// nonzero if unsupported (K % (64 S), N % 4, the 2-stage form's LDS)
+int launch_gemm_flex_partials(const void* X, const void* W, float* ws, int M, int N, int K,
+                              int cand, int S, hipStream_t s) {
+  if (S < 2 || K % (FBK * S) || N % 4 || M <= 0) return 2;
+  switch (cand & 31) {
+    case 0: flex_sk_launch<64, 64>(X, W, ws, M, N, K, S, s); return 0;
+    case 1: flex_sk_launch<64, 128>(X, W, ws, M, N, K, S, s); return 0;
+    case 2: flex_sk_launch<64, 160>(X, W, ws, M, N, K, S, s); return 0;
+    case 3: flex_sk_launch<96, 64>(X, W, ws, M, N, K, S, s); return 0;
+    case 4: flex_sk_launch<96, 128>(X, W, ws, M, N, K, S, s); return 0;
+    case 5: flex_sk_launch<128, 96>(X, W, ws, M, N, K, S, s); return 0;
+    case 6: flex_sk_launch<128, 128>(X, W, ws, M, N, K, S, s); return 0;
+    case 7: flex_sk_launch<128, 160>(X, W, ws, M, N, K, S, s); return 0;
+    case 8: flex_sk_launch<128, 192>(X, W, ws, M, N, K, S, s); return 0;
+    case 9: flex_sk_launch<256, 32>(X, W, ws, M, N, K, S, s); return 0;
+    case 10: flex_sk_launch<192, 128>(X, W, ws, M, N, K, S, s); return 0;
+    case 11: flex_sk_launch<160, 128>(X, W, ws, M, N, K, S, s); return 0;
+    case 12: flex_sk_launch<256, 64>(X, W, ws, M, N, K, S, s); return 0;
+    case 13: flex_sk_launch<192, 64>(X, W, ws, M, N, K, S, s); return 0;
+    default: return 1;
+  }
 }
 
 // 1 if candidate cand (any form) has a SwiGLU epilogue

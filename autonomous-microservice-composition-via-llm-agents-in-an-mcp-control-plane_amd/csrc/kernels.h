@@ -212,3 +212,11 @@ void rccl_destroy(void* comm);
 
 // prefetch.hip: read a weight range once (MALL warm-up beside latency-bound work)
 int launch_prefetch(const void* p, size_t bytes, int wgs, int* sink, hipStream_t s);
+// gemm_flex.hip: fp32 split-K partials of a flex tile (candidates 0..11 as
+// the flex list; 12 = 256 x 64, 13 = 192 x 64: split-only whole-M tiles)
+int launch_gemm_flex_partials(const void* X, const void* W, float* ws, int M, int N, int K,
+                              int cand, int S, hipStream_t s);
+void gemm_plan_set_fsplit(int N, int K, const int* fs, int n);
+int gemm_plan_fsplit(int M, int N, int K);
+int launch_gemm_flex_split(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                           int K, int cand, int S, int epi, hipStream_t s);

@@ -71,6 +71,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
             mod.gemm_plan_set_splits(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["splits"]])
         if "flex" in sh and hasattr(mod, "gemm_plan_set_flex"):
             mod.gemm_plan_set_flex(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["flex"]])
+        if "fsplit" in sh and hasattr(mod, "gemm_plan_set_fsplit"):
+            mod.gemm_plan_set_fsplit(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["fsplit"]])
         if "group" in sh and hasattr(mod, "gemm_plan_set_group"):
             mod.gemm_plan_set_group(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["group"]])
         if "persist" in sh and hasattr(mod, "gemm_plan_set_persist"):

@@ -101,6 +101,38 @@ def test_gemm_plan_flex_dispatch():
         ops._load_gemm_plan(L)
 
 
+@pytest.mark.parametrize("M,K", [(100, 512), (320, 1792)])
+def test_gemm_plan_fsplit_dispatch(M, K):
+    """A plan "fsplit" entry (flex tile x split-K: fp32 partials + the reduce)
+    routes ops.gemm there; every tile and split, plain and residual + the
+    fused-norm statistic, against fp32 (ragged M tiles included)."""
+    torch.manual_seed(29)
+    L = ops.lib()
+    N = 768
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    try:
+        for c in range(14):
+            for S in (2, 4, 7):
+                if (K // 64) % S:
+                    continue
+                fs = 16 * c + S
+                L.gemm_plan_set(N, K, [0] * 8)
+                L.gemm_plan_set_fsplit(N, K, [fs] * 8)
+                assert L.gemm_plan_fsplit(M, N, K) == fs
+                assert rel_err(ops.gemm(X, W), ref.gemm(X, W)) < 1e-2, fs
+                y = R.clone()
+                ss = torch.zeros(M, dtype=torch.int64, device=DEV)
+                ops.gemm(X, W, R=y, out=y, ss_out=ss)
+                assert rel_err(y, ref.gemm(X, W, R)) < 1e-2, fs
+                exp = y.float().pow(2).sum(-1) * ref.SS_FIX
+                assert ((ss.double() - exp.double()).abs() / exp.double()).max().item() < 1e-5, fs
+    finally:
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)
+
+
 def test_gemm_orientation_exact():
     # A = I, asymmetric B: catches a transposed C-write (cdna_hip_programming.md §3)
     K = 128

@@ -70,6 +70,8 @@ for spec in MODEL.split("+"):
 # into the shipped plan with tools/merge_gemm_plan.py --keys flex)
 if os.environ.get("MCP_TUNE_SHAPES") == "swiglu":
     SHAPES = [sh for sh in SHAPES if sh[0] in SWIGLU_N]
+elif os.environ.get("MCP_TUNE_SHAPES") == "narrow":     # all but gate|up
+    SHAPES = [sh for sh in SHAPES if sh[0] not in SWIGLU_N]
 MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
@@ -86,8 +88,15 @@ s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timin
 RESIDUAL = set()                           # (N, K) timed with the residual epilogue
 
 
+FS_TILES = [(64, 64), (64, 128), (64, 160), (96, 64), (96, 128), (128, 96), (128, 128), (128, 160),
+            (128, 192), (256, 32), (192, 128), (160, 128), (256, 64), (192, 64)]
+FS_MIN, FS_MAX = 65, 512                   # flex x split-K measured here (narrow shapes)
+
+
 def run(code, X, W, Y, split=-1, R=None):
-    if code == "flex":                     # flex tile, split = candidate
+    if code == "fsplit":                   # flex tile x split-K, split = 16 cand + S
+        L.gemm(X, W, Y, R, 1000 + split)
+    elif code == "flex":                   # flex tile, split = candidate
         L.gemm(X, W, Y, R, 16 + split)
     elif code == "lib":                    # hipBLASLt yardstick (never dispatched)
         if R is not None:
@@ -117,6 +126,7 @@ result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
           "codes": "0=128x128, 1..5=AGPR 256/192/160/224/128-row tiles",
           "splits": "measured split-K of code 0 per bucket (0 = the rule)",
           "flex": "measured flex tile per bucket (gemm_flex.hip candidate, +32 = 4-stage; -1 = none)",
+          "fsplit": "measured flex tile x split-K per bucket (16 cand + S, partials + reduce; -1 = none)",
           "ref_us": "[ours, hipBLASLt] us per bucket, yardstick only",
           "generated": time.strftime("%Y-%m-%d"), "shapes": []}
 RESIDUAL.update(sh for spec in MODEL.split("+") for i, sh in enumerate(shard_shapes(spec)) if i in (1, 3))
@@ -128,7 +138,7 @@ for (N, K) in SHAPES:
                    for _ in range(int(1.5e9 // (N * K * 2)))]
     Yf = torch.empty(m_max, N, device=dev, dtype=torch.bfloat16)
     Rf = torch.randn(m_max, N, device=dev).bfloat16() if (N, K) in RESIDUAL else None
-    codes, tf, splits, flex, ref = [], [], [], [], []
+    codes, tf, splits, flex, fsplit, ref = [], [], [], [], [], []
     for b in range(m_max // MSTEP):
         M = (b + 1) * MSTEP
         X, Y = Xf[:M], Yf[:M]
@@ -147,7 +157,14 @@ for (N, K) in SHAPES:
             # gate|up (SwiGLU epilogue): only tiles whose waves hold whole gate | up pairs
             fcands = [f for f in range(NFLEX) if N not in SWIGLU_N or L.gemm_flex_silu_ok(f)]
             fl = [("flex", f) for f in fcands + [32 + f for f in fcands]]
-        allc = cands + fl + [("lib", -1)]
+        fsl = []
+        if FS_MIN <= M <= FS_MAX and N not in SWIGLU_N:
+            for c, (tm, tn) in enumerate(FS_TILES):
+                tiles = -(-M // tm) * -(-N // tn)
+                for S in (2, 3, 4, 7, 8):
+                    if (K // 64) % S == 0 and 128 <= tiles * S <= 1024:
+                        fsl.append(("fsplit", 16 * c + S))
+        allc = cands + fl + fsl + [("lib", -1)]
         best = {c: float("inf") for c in allc}
         for _ in range(3):
             for c in allc:
@@ -159,6 +176,9 @@ for (N, K) in SHAPES:
         fbest = min(fl, key=lambda c: best[c]) if fl else None
         flex.append(fbest[1] if fbest and best[fbest] * 1.01 < ref_ms else -1)
         ours_ms = min(ref_ms, best[fbest]) if fbest else ref_ms
+        sbest = min(fsl, key=lambda c: best[c]) if fsl else None
+        fsplit.append(sbest[1] if sbest and best[sbest] * 1.01 < ours_ms else -1)
+        ours_ms = min(ours_ms, best[sbest]) if sbest else ours_ms
         ref.append([round(ours_ms * 1e3, 1), round(lib_ms * 1e3, 1)])
         if M < M_MIN:
             codes.append(-1)
@@ -174,8 +194,10 @@ for (N, K) in SHAPES:
         codes.append(win)
         tf.append({str(c): round(2 * M * N * K / best[c] / 1e9, 1) for c in cands})
     result["shapes"].append({"N": N, "K": K, "codes": codes, "splits": splits, "flex": flex,
+                             "fsplit": fsplit,
                              "tflops": tf, "ref_us": ref})
-    print(json.dumps({"N": N, "K": K, "codes": codes, "flex": flex, "s": round(time.time() - t0, 1)}),
+    print(json.dumps({"N": N, "K": K, "codes": codes, "flex": flex, "fsplit": fsplit,
+                      "s": round(time.time() - t0, 1)}),
           flush=True)
     del Xf, W, Yf, Wcold, Rf
 with open(out_path, "w") as f:
