@@ -643,7 +643,11 @@ int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K,
   if (M <= SKINNY_MAX_M && gemm128_splits(M, N, K) <= 1 &&
       launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0)
     return 0;
-  // serving-size M: a measured flex tile with the SwiGLU epilogue (plan "flex")
+  // serving-size M: a measured flex tile with split-K (plan "fsplit"; the
+  // reduce applies the SwiGLU) or with the SwiGLU epilogue (plan "flex")
+  const int fs = gemm_plan_fsplit(M, N, K);
+  if (fs >= 0 && launch_gemm_flex_split(X, W, Y, nullptr, M, N, K, fs / 16, fs % 16, 2, s) == 0)
+    return 0;
   const int fx = gemm_plan_flex(M, N, K);
   if (fx >= 0 && gemm_flex_silu_ok(fx) &&
       launch_gemm_flex_epi(X, W, Y, nullptr, M, N, K, fx, 2, s) == 0)

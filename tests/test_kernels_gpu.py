@@ -1128,6 +1128,13 @@ def test_gemm_flex_swiglu(M):
             assert L.gemm_plan_flex(M, N, H) == c
             assert rel_err(ops.gemm_silu(x, Wg), e_plain) < 2e-2, c
             assert rel_err(ops.gemm_silu(x, Wg, ss_in=ss, eps=eps), e_norm) < 2e-2, c
+        # flex x split-K through the plan's "fsplit" entry: the reduce applies
+        # the SwiGLU and the row scale
+        L.gemm_plan_set_flex(N, H, [-1] * 16)
+        for fs in (16 * 6 + 2, 16 * 12 + 4, 16 * 1 + 8):
+            L.gemm_plan_set_fsplit(N, H, [fs] * 16)
+            assert rel_err(ops.gemm_silu(x, Wg), e_plain) < 2e-2, fs
+            assert rel_err(ops.gemm_silu(x, Wg, ss_in=ss, eps=eps), e_norm) < 2e-2, fs
     finally:
         L.gemm_plan_clear()
         ops._load_gemm_plan(L)

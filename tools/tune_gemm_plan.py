@@ -158,7 +158,9 @@ for (N, K) in SHAPES:
             fcands = [f for f in range(NFLEX) if N not in SWIGLU_N or L.gemm_flex_silu_ok(f)]
             fl = [("flex", f) for f in fcands + [32 + f for f in fcands]]
         fsl = []
-        if FS_MIN <= M <= FS_MAX and N not in SWIGLU_N:
+        # (gate|up timed with the plain epilogue: same partials, a reduce
+        # that writes half the columns - a slightly pessimistic proxy)
+        if FS_MIN <= M <= FS_MAX:
             for c, (tm, tn) in enumerate(FS_TILES):
                 tiles = -(-M // tm) * -(-N // tn)
                 for S in (2, 3, 4, 7, 8):
