@@ -35,20 +35,27 @@ def t_us(fn, R, n=20):
     return round(best, 1)
 
 
-for (N, K, res) in [(4096, 14336, True), (4096, 4096, True), (6144, 4096, False)]:
+MS = [int(m) for m in os.environ.get("PROBE_MS", "128,192,256,320,384").split(",")]
+SHAPES = [(4096, 14336, True), (4096, 4096, True), (6144, 4096, False)]
+if os.environ.get("PROBE_WIDE") == "1":
+    SHAPES.append((28672, 4096, False))
+for (N, K, res) in SHAPES:
     R = max(4, int(1.6e9 // (N * K * 2)) + 1)
     Ws = [(torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16() for _ in range(R)]
-    for M in (128, 192, 256, 320, 384):
+    for M in MS:
         X = torch.randn(M, K, device="cuda").bfloat16()
         Y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         Rr = torch.randn(M, N, device="cuda").bfloat16() if res else None
         r = {"M": M, "N": N, "K": K, "floor_us": round(N * K * 2 / 6.0e12 * 1e6, 1),
              "auto_us": t_us(lambda i: L.gemm(X, Ws[i], Y, Rr, -1), R)}
+        if N == 28672:                     # gate|up: the shipped SwiGLU dispatch
+            Yh = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+            r["auto_silu_us"] = t_us(lambda i: L.gemm_silu(X, Ws[i], Yh, None, 0.0), R)
         best = None
         for c, (tm, tn) in enumerate(TILES):
             tiles = -(-M // tm) * -(-N // tn)
             for S in (2, 3, 4, 7, 8):
-                if (K // 64) % S or not (128 <= tiles * S <= 1024):
+                if (K // 64) % S or not (64 <= tiles * S <= 1024):
                     continue
                 t = t_us(lambda i: L.gemm(X, Ws[i], Y, Rr, 1000 + 16 * c + S), R)
                 if best is None or t < best[0]:
