@@ -526,6 +526,93 @@ static bool launch_gemm_128_split(const void* X, const void* W, void* Y, const v
   return true;
 }
 
+// QKV split-K reduce with the RoPE / paged K-V write fused in (the rope_kv
+// kernel's work, elementwise.hip, on the fp32 sums instead of a bf16 qkv
+// round trip): one thread per (token, head, 8-wide chunk of the first half)
+// of the S partials [S][M][(Hq + 2 Hkv) D]; V heads are copied to the cache
+template <int D>
+__global__ __launch_bounds__(256) void splitk_reduce_rope(const float* __restrict__ ws, int S, int M,
+                                                          const RopeArgs ra, const NormEpi ne) {
+  constexpr int CH = D / 16;
+  const int heads = ra.Hq + 2 * ra.Hkv;
+  const int N = heads * D;
+  const size_t total = (size_t)M * heads * CH;
+  const size_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % CH);
+  const int h = (int)((i / CH) % heads);
+  const int t = (int)(i / ((size_t)CH * heads));
+  const int d0 = c * 8;
+  const size_t MN = (size_t)M * N;
+  const float* p = ws + (size_t)t * N + (size_t)h * D + d0;
+  f32x4 lo0 = *reinterpret_cast<const f32x4*>(p), lo1 = *reinterpret_cast<const f32x4*>(p + 4);
+  f32x4 hi0 = *reinterpret_cast<const f32x4*>(p + D / 2), hi1 = *reinterpret_cast<const f32x4*>(p + D / 2 + 4);
+  for (int sp = 1; sp < S; ++sp) {
+    const float* q = p + sp * MN;
+    lo0 += *reinterpret_cast<const f32x4*>(q);
+    lo1 += *reinterpret_cast<const f32x4*>(q + 4);
+    hi0 += *reinterpret_cast<const f32x4*>(q + D / 2);
+    hi1 += *reinterpret_cast<const f32x4*>(q + D / 2 + 4);
+  }
+  const float rs = norm_row_scale(ne, t);
+  float lo[8], hi[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lo[j] = lo0[j] * rs;
+    lo[4 + j] = lo1[j] * rs;
+    hi[j] = hi0[j] * rs;
+    hi[4 + j] = hi1[j] * rs;
+  }
+  bf16x8 olo, ohi;
+  bf16* dst;
+  if (h >= ra.Hq + ra.Hkv) {                           // V: copy into the cache
+    const int slot = ra.slots[t];
+    if (slot < 0) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      olo[j] = (bf16)lo[j];
+      ohi[j] = (bf16)hi[j];
+    }
+    dst = reinterpret_cast<bf16*>(ra.v_cache) +
+          (((size_t)(slot / ra.BS) * ra.Hkv + (h - ra.Hq - ra.Hkv)) * ra.BS + slot % ra.BS) * D;
+  } else {
+    const float2* cs = reinterpret_cast<const float2*>(ra.cos_sin) + (size_t)ra.pos[t] * (D / 2) + d0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 r = cs[j];
+      olo[j] = (bf16)(lo[j] * r.x - hi[j] * r.y);
+      ohi[j] = (bf16)(hi[j] * r.x + lo[j] * r.y);
+    }
+    if (h < ra.Hq) {
+      dst = reinterpret_cast<bf16*>(ra.q_out) + ((size_t)t * ra.Hq + h) * D;
+    } else {
+      const int slot = ra.slots[t];
+      if (slot < 0) return;
+      dst = reinterpret_cast<bf16*>(ra.k_cache) +
+            (((size_t)(slot / ra.BS) * ra.Hkv + (h - ra.Hq)) * ra.BS + slot % ra.BS) * D;
+    }
+  }
+  *reinterpret_cast<bf16x8*>(dst + d0) = olo;
+  *reinterpret_cast<bf16x8*>(dst + d0 + D / 2) = ohi;
+}
+
+// QKV + RoPE + K/V write through the plan's flex x split-K entry for this
+// bucket, the reduce doing the rope_kv work; nonzero: not taken
+int launch_qkv_rope_fsplit(const void* X, const void* W, int M, int N, int K, int D,
+                           const RopeArgs& ra, hipStream_t s) {
+  static const int on = getenv("MCP_QKV_ROPE_FSPLIT") ? atoi(getenv("MCP_QKV_ROPE_FSPLIT")) : 1;
+  if (!on || D != 128 || N != (ra.Hq + 2 * ra.Hkv) * D) return 1;
+  const int fs = gemm_plan_fsplit(M, N, K);
+  if (fs < 0) return 1;
+  const int S = fs % 16;
+  if (!g_splitk_ws || (size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) return 4;
+  if (launch_gemm_flex_partials(X, W, g_splitk_ws, M, N, K, fs / 16, S, s)) return 2;
+  const size_t total = (size_t)M * (ra.Hq + 2 * ra.Hkv) * (D / 16);
+  splitk_reduce_rope<128><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(g_splitk_ws, S, M, ra,
+                                                                            norm_epi());
+  return 0;
+}
+
 // flex tile cand, S-way split-K through the fp32 workspace + the reduce
 // (epilogue 0/1/2); nonzero if unsupported or the workspace is too small
 int launch_gemm_flex_split(const void* X, const void* W, void* Y, const void* R, int M, int N,

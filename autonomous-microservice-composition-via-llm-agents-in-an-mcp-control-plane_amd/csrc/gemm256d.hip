@@ -594,6 +594,9 @@ void launch_qkv_rope(const void* X, const void* W, void* qkv, int M, int N, int 
   if (fused && gemm_stream_enabled() && gemm_stream_pick(M, N, K, 3) &&
       launch_gemm_stream(X, W, nullptr, nullptr, M, N, K, 3, ra, s) == 0)
     return;
+  // a measured flex x split-K bucket (timed against the AGPR heights by the
+  // tuner): the reduce applies RoPE and writes the cache
+  if (fused && launch_qkv_rope_fsplit(X, W, M, N, K, D, ra, s) == 0) return;
   if (fused && D == 128 && N == (ra.Hq + 2 * ra.Hkv) * 128 && M > SKINNY_MAX_M &&
       gemm_select(M, N, K) == 1 && gemm256d_ok(M, N, K) == 0 &&
       launch_256d_impl(X, W, nullptr, nullptr, M, N, K, 3, 0, ra, s) == 0)

@@ -220,3 +220,5 @@ void gemm_plan_set_fsplit(int N, int K, const int* fs, int n);
 int gemm_plan_fsplit(int M, int N, int K);
 int launch_gemm_flex_split(const void* X, const void* W, void* Y, const void* R, int M, int N,
                            int K, int cand, int S, int epi, hipStream_t s);
+int launch_qkv_rope_fsplit(const void* X, const void* W, int M, int N, int K, int D,
+                           const RopeArgs& ra, hipStream_t s);

@@ -978,9 +978,16 @@ def test_fused_norm_swiglu_and_qkv(M):
     qr, kr, vr = (torch.zeros(M, Hq, D), torch.zeros(nb, Hkv, BS, D), torch.zeros(nb, Hkv, BS, D))
     ref.rope_kv(qkv, pos.cpu(), slots.cpu(), cs.cpu(), qr, kr, vr, Hq, Hkv, D)
     codes = (None, 1, 2, 3, 4, 5) if M >= 256 else (None,)
+    # flex x split-K plan entries (the reduce applies the row scale, RoPE and
+    # the K / V write: gemm.hip splitk_reduce_rope), M > 64 (below: the stream kernel)
+    codes += tuple(("fs", fs) for fs in (16 * 5 + 4, 16 * 7 + 4, 16 * 6 + 2)) if M > 64 else ()
     try:
         for code in codes:
-            if code is not None:
+            if isinstance(code, tuple):
+                L.gemm_plan_set(Wqf.shape[0], H, [0] * 64)
+                L.gemm_plan_set_fsplit(Wqf.shape[0], H, [code[1]] * 64)
+            elif code is not None:
+                L.gemm_plan_set_fsplit(Wqf.shape[0], H, [-1] * 64)
                 L.gemm_plan_set(Wqf.shape[0], H, [code] * 64)
             q = torch.empty(M, Hq, D, device=DEV, dtype=torch.bfloat16)
             kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
