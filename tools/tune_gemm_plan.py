@@ -90,7 +90,8 @@ RESIDUAL = set()                           # (N, K) timed with the residual epil
 
 FS_TILES = [(64, 64), (64, 128), (64, 160), (96, 64), (96, 128), (128, 96), (128, 128), (128, 160),
             (128, 192), (256, 32), (192, 128), (160, 128), (256, 64), (192, 64)]
-FS_MIN, FS_MAX = 65, int(os.environ.get("MCP_TUNE_FS_MAX", "512"))   # flex x split-K (narrow shapes)
+FS_MIN = int(os.environ.get("MCP_TUNE_FS_MIN", "65"))    # flex x split-K measured here
+FS_MAX = int(os.environ.get("MCP_TUNE_FS_MAX", "512"))
 
 
 def run(code, X, W, Y, split=-1, R=None):
