@@ -71,7 +71,12 @@ class ExecuteResponse(BaseModel):
 def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegistry] = None,
                planner: Optional[Planner] = None,
                transport: Optional[httpx.AsyncBaseTransport] = None,
-               planner_transport: Optional[httpx.AsyncBaseTransport] = None) -> FastAPI:
+               planner_transport: Optional[httpx.AsyncBaseTransport] = None,
+               settle_gc: bool = False) -> FastAPI:
+    """``settle_gc``: after start-up, move the heap to the permanent GC
+    generation (``utils/heap.py``) - for a serving process's entry point only
+    (``main``, ``uvicorn ...:app``), never for apps built inside a library or
+    a test process, where frozen objects would never be collected."""
     settings = settings or Settings.from_env()
     if registry is None:
         registry = make_registry(settings.redis_url, settings.services_prefix)
@@ -132,6 +137,9 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
                                                settings.adaptive_error_rate,
                                                settings.adaptive_min_calls,
                                                settings.adaptive_retries)
+        if settle_gc:
+            from ..utils.heap import settle
+            settle()                       # start-up heap -> permanent GC generation
         try:
             yield
         finally:
@@ -209,7 +217,7 @@ def __getattr__(name):
     global _APP
     if name == "app":
         if _APP is None:
-            _APP = create_app()
+            _APP = create_app(settle_gc=True)     # a server process's own app
         return _APP
     raise AttributeError(name)
 
@@ -224,7 +232,7 @@ def main():  # pragma: no cover - CLI entry (reference :155-157)
     ap.add_argument("--no-access-log", action="store_true",
                     help="skip uvicorn's per-request access log line")
     args = ap.parse_args()
-    uvicorn.run(create_app(), host=args.host, port=args.port, access_log=not args.no_access_log)
+    uvicorn.run(create_app(settle_gc=True), host=args.host, port=args.port, access_log=not args.no_access_log)
 
 
 if __name__ == "__main__":  # pragma: no cover

@@ -465,6 +465,8 @@ class LlamaModel:
             if l + 1 == L:
                 # last layer: only the sampled rows go on (see ``forward``)
                 if rows.numel() == 0:
+                    if side is not None:             # join the prefetch before leaving
+                        torch.cuda.current_stream(x.device).wait_stream(side)
                     return x.new_empty(0, cfg.hidden)
                 ri = rows.long()
                 x = x.index_select(0, ri)

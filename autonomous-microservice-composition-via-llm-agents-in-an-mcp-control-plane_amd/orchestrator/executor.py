@@ -84,12 +84,16 @@ class Orchestrator:
     def _fast_ok(self) -> bool:
         c = self.client
         ok = getattr(self, "_fast", None)
-        if ok is None or ok[0] is not c:
+        # the client's default headers are re-read whenever they change (the
+        # raw list is compared, not cached by identity): headers set on the
+        # client after the first call are sent, as client.post would
+        raw = c.headers.raw if isinstance(c, httpx.AsyncClient) else None
+        if ok is None or ok[0] is not c or ok[4] != raw:
             usable = (isinstance(c, httpx.AsyncClient) and hasattr(c, "_transport_for_url")
                       and c.auth is None and not c.follow_redirects and not str(c.base_url)
                       and not any(c.event_hooks.values()) and not c.params)
-            self._fast = ok = (c, usable, [(k.encode("latin-1"), v.encode("latin-1"))
-                                           for k, v in c.headers.multi_items()] if usable else None, {})
+            self._fast = ok = (c, usable, list(raw) if usable else None,
+                               ok[3] if ok is not None and ok[0] is c else {}, raw)
         return ok[1] and not c.cookies
 
     async def _post(self, url: str, inputs: dict):
@@ -97,7 +101,9 @@ class Orchestrator:
             resp = await self.client.post(url, json=inputs, timeout=self.timeout)
             resp.raise_for_status()
             return resp.json()
-        c, _, base, urls = self._fast
+        c, _, base, urls, _ = self._fast
+        if c.is_closed:                 # client.post's own check, same text
+            raise RuntimeError("Cannot send a request, as the client has been closed.")
         u = urls.get(url)
         if u is None:
             if len(urls) > 4096:

@@ -26,7 +26,6 @@ import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
-from ..utils.heap import settle as settle_heap
 from ..utils.metrics import METRICS
 from .base import Planner
 from .grammar import GrammarSpec
@@ -101,7 +100,8 @@ class LocalPlanner(Planner):
         planner = cls(eng, registry, tokenizer=tok, max_nodes=settings.max_nodes,
                       min_nodes=getattr(settings, "min_nodes", 1), retriever=retr,
                       retrieval_threshold=settings.retrieval_threshold, topk=settings.topk)
-        settle_heap()                      # start-up heap -> permanent GC generation
+        # (no heap.settle() here: freezing the GC heap is a process entry
+        # point's decision - the server's lifespan, a router replica, a bench)
         return planner
 
     # ----------------------------------------------------------- prepare

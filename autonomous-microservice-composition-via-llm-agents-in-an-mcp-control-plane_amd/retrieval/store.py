@@ -294,12 +294,17 @@ class SchemaIndex:
     def _catch_up(self, max_changes: Optional[int] = None) -> bool:
         """Bring the shadow up to the registry's current version (diff + embed
         under ``_diff_lock``, then queue the update).  With ``max_changes``
-        only a change-log backlog of at most that many records is taken;
-        returns whether the shadow is now current."""
+        only a change-log backlog of at most that many records is taken, and
+        the call never waits for the lock: the engine thread passes it, and a
+        busy lock means the refresher is already diffing (and embedding) a
+        backlog, which stays on that thread.  Returns whether the shadow is
+        now current."""
         ver = getattr(self.registry, "version", None)
         if ver is None or ver == self._shadow_version:
             return True
-        with self._diff_lock:
+        if not self._diff_lock.acquire(blocking=max_changes is None):
+            return False
+        try:
             seen = self._shadow_version
             ver = getattr(self.registry, "version", None)
             if ver == seen:
@@ -320,6 +325,8 @@ class SchemaIndex:
             if u is not None:
                 with self._lock:
                     self._pending.append(u)
+        finally:
+            self._diff_lock.release()
         return True
 
     def start_background(self, poll_s: float = 0.05) -> None:

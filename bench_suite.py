@@ -80,33 +80,113 @@ def load_reference(path: str = "/root/reference/control_plane.py", canned=None):
     return mod
 
 
-def plumbing(runs: int = 30, rounds: int = 3, out=None):
-    """Config 1 on this host: ours and the reference (``load_reference``)
-    alternate ``rounds`` times per case, ``runs`` requests each; the p50 of
-    every round is reported, and the speedup from the medians of the rounds."""
-    import asyncio
+def _plumbing_cases():
+    """Config-1 cases shared by our timing and the reference worker."""
+    from mcp_amd.registry import synthetic_registry
+    canned = {"nodes": [{"name": "a", "endpoint": "http://a/api", "inputs": {"x": "uid"}}], "edges": []}
+    cases = []
+    for n in (3, 10, 50, 1000):
+        cases.append(("plan", n, synthetic_registry(n, seed=1), lambda i: {"intent": f"charge order {i}"}))
+    for n in (3, 10, 50):
+        nodes = [{"name": f"n{i}", "endpoint": f"http://n{i}/api",
+                  "inputs": {"x": f"n{i - 1}" if i else "uid"}} for i in range(n)]
+        edges = [{"from": f"n{i - 1}", "to": f"n{i}"} for i in range(1, n)]
+        body = (lambda nodes, edges: lambda i: {"graph": {"nodes": nodes, "edges": edges},
+                                               "payload": {"uid": 1}})(nodes, edges)
+        cases.append(("execute", n, synthetic_registry(3), body))
+    return canned, cases
+
+
+def _time_posts(c, route, body_fn, k):
+    for i in range(5):
+        c.post(route, json=body_fn(i))
+    ts = []
+    for i in range(k):
+        t = time.perf_counter()
+        r = c.post(route, json=body_fn(i))
+        ts.append(time.perf_counter() - t)
+        assert r.status_code == 200, r.text
+    return statistics.median(ts) * 1e3
+
+
+def _mock_handler(request):
+    import httpx
+    return httpx.Response(200, json={"ok": True})
+
+
+def reference_worker() -> None:
+    """Runs in its OWN process (``ReferenceTimer``): loads the scratch copy of
+    the reference and answers ``{"case": i, "runs": k}`` lines on stdin with
+    the p50 of that case on stdout.  The reference is third-party source: its
+    import-time code never runs inside the bench process."""
+    import httpx
+    from fastapi.testclient import TestClient
+    canned, cases = _plumbing_cases()
+    ref = load_reference(canned=canned)
+    print(json.dumps({"ready": ref is not None}), flush=True)
+    if ref is None:
+        return
+    clients = {}
+    for line in sys.stdin:
+        req = json.loads(line)
+        kind, n, services, body = cases[req["case"]]
+        if req["case"] not in clients:
+            ref._store.clear()
+            for s in services:
+                ref._store["mcp:service:" + s["name"]] = json.dumps(dict(s))
+            ref.orch.client = httpx.AsyncClient(transport=httpx.MockTransport(_mock_handler))
+            clients = {req["case"]: TestClient(ref.app)}
+        ms = _time_posts(clients[req["case"]], "/" + kind, body, req["runs"])
+        print(json.dumps({"p50_ms": ms}), flush=True)
+
+
+class ReferenceTimer:
+    """The same-host reference comparison, opt-in (``--with-reference``): a
+    child ``python -I`` (isolated mode: no user site, no PYTHON* env) in a
+    scratch working directory, with a minimal environment, driven over pipes."""
+
+    def __init__(self):
+        import subprocess
+        import tempfile
+        env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), "HOME": tempfile.gettempdir()}
+        code = ("import sys; sys.path.insert(0, %r); import bench_suite; bench_suite.reference_worker()"
+                % os.path.dirname(os.path.abspath(__file__)))
+        self.proc = subprocess.Popen([sys.executable, "-I", "-c", code], stdin=subprocess.PIPE,
+                                     stdout=subprocess.PIPE, text=True, env=env,
+                                     cwd=tempfile.mkdtemp(prefix="refbench_"))
+        self.ready = bool(json.loads(self.proc.stdout.readline() or "{}").get("ready"))
+
+    def time(self, case: int, runs: int) -> float:
+        self.proc.stdin.write(json.dumps({"case": case, "runs": runs}) + "\n")
+        self.proc.stdin.flush()
+        return json.loads(self.proc.stdout.readline())["p50_ms"]
+
+    def close(self):
+        try:
+            self.proc.stdin.close()
+            self.proc.wait(timeout=30)
+        except Exception:            # noqa: BLE001 - best effort
+            self.proc.kill()
+
+
+def plumbing(runs: int = 30, rounds: int = 3, out=None, with_reference: bool = False):
+    """Config 1 on this host.  With ``with_reference`` a stubbed scratch copy
+    of the reference runs in an isolated child process (``ReferenceTimer``)
+    and the two alternate ``rounds`` times per case, ``runs`` requests each;
+    otherwise the reference's recorded numbers (another host) are
+    quoted."""
     import httpx
     from fastapi.testclient import TestClient
     from mcp_amd.api.server import create_app
     from mcp_amd.config import Settings
     from mcp_amd.planner.base import StubPlanner
-    from mcp_amd.registry import MemoryRegistry, synthetic_registry
+    from mcp_amd.registry import MemoryRegistry
 
-    def handler(request):
-        return httpx.Response(200, json={"ok": True})
-    canned = {"nodes": [{"name": "a", "endpoint": "http://a/api", "inputs": {"x": "uid"}}], "edges": []}
-    ref = load_reference(canned=canned)
-
-    def time_posts(c, route, body_fn, k):
-        for i in range(5):
-            c.post(route, json=body_fn(i))
-        ts = []
-        for i in range(k):
-            t = time.perf_counter()
-            r = c.post(route, json=body_fn(i))
-            ts.append(time.perf_counter() - t)
-            assert r.status_code == 200, r.text
-        return statistics.median(ts) * 1e3
+    canned, cases = _plumbing_cases()
+    ref = ReferenceTimer() if with_reference else None
+    if ref is not None and not ref.ready:
+        ref.close()
+        ref = None
 
     def emit(rec):
         line = json.dumps(rec)
@@ -115,51 +195,30 @@ def plumbing(runs: int = 30, rounds: int = 3, out=None):
             with open(out, "a") as fh:
                 fh.write(line + "\n")
 
-    def ref_client(mod, services):
-        mod._store.clear()
-        for s in services:
-            mod._store["mcp:service:" + s["name"]] = json.dumps(dict(s))
-        mod.orch.client = httpx.AsyncClient(transport=httpx.MockTransport(handler))
-        return TestClient(mod.app)
-
-    def compare(kind, n, ours_fn, ref_fn):
-        o, r = [], []
-        for _ in range(rounds):
-            o.append(ours_fn())
-            if ref is not None:
-                r.append(ref_fn())
-        rec = {"config": f"plumbing/{kind}", ("services" if kind == "plan" else "nodes"): n,
-               "p50_ms": round(statistics.median(o), 3), "rounds_ms": [round(x, 3) for x in o]}
-        if r:
-            rec.update(reference_same_host_ms=round(statistics.median(r), 3),
-                       reference_rounds_ms=[round(x, 3) for x in r],
-                       speedup=round(statistics.median(r) / statistics.median(o), 2))
-        else:
-            rec.update(reference_other_host_ms=(REF_PLAN_MS if kind == "plan" else REF_EXEC_MS)[n])
-        emit(rec)
-
-    for n in (3, 10, 50, 1000):
-        services = synthetic_registry(n, seed=1)
-        reg = MemoryRegistry(services)
-        app = create_app(Settings(), registry=reg, planner=StubPlanner(reg, canned=canned),
-                         transport=httpx.MockTransport(handler))
-        body = lambda i: {"intent": f"charge order {i}"}
-        with TestClient(app) as c:
-            rc = ref_client(ref, services) if ref is not None else None
-            compare("plan", n, lambda: time_posts(c, "/plan", body, runs),
-                    lambda: time_posts(rc, "/plan", body, runs))
-    for n in (3, 10, 50):
-        nodes = [{"name": f"n{i}", "endpoint": f"http://n{i}/api",
-                  "inputs": {"x": f"n{i - 1}" if i else "uid"}} for i in range(n)]
-        edges = [{"from": f"n{i - 1}", "to": f"n{i}"} for i in range(1, n)]
-        reg = MemoryRegistry(synthetic_registry(3))
-        app = create_app(Settings(), registry=reg, planner=StubPlanner(reg),
-                         transport=httpx.MockTransport(handler))
-        body = lambda i: {"graph": {"nodes": nodes, "edges": edges}, "payload": {"uid": 1}}
-        with TestClient(app) as c:
-            rc = ref_client(ref, synthetic_registry(3)) if ref is not None else None
-            compare("execute", n, lambda: time_posts(c, "/execute", body, runs),
-                    lambda: time_posts(rc, "/execute", body, runs))
+    try:
+        for ci, (kind, n, services, body) in enumerate(cases):
+            reg = MemoryRegistry(services)
+            planner = StubPlanner(reg, canned=canned) if kind == "plan" else StubPlanner(reg)
+            app = create_app(Settings(), registry=reg, planner=planner,
+                             transport=httpx.MockTransport(_mock_handler))
+            o, r = [], []
+            with TestClient(app) as c:
+                for _ in range(rounds):
+                    o.append(_time_posts(c, "/" + kind, body, runs))
+                    if ref is not None:
+                        r.append(ref.time(ci, runs))
+            rec = {"config": f"plumbing/{kind}", ("services" if kind == "plan" else "nodes"): n,
+                   "p50_ms": round(statistics.median(o), 3), "rounds_ms": [round(x, 3) for x in o]}
+            if r:
+                rec.update(reference_same_host_ms=round(statistics.median(r), 3),
+                           reference_rounds_ms=[round(x, 3) for x in r],
+                           speedup=round(statistics.median(r) / statistics.median(o), 2))
+            else:
+                rec.update(reference_other_host_ms=(REF_PLAN_MS if kind == "plan" else REF_EXEC_MS)[n])
+            emit(rec)
+    finally:
+        if ref is not None:
+            ref.close()
 
 
 def topk(n: int, dim: int, k: int, batches=(1, 16, 32, 64), iters: int = 50):
@@ -240,6 +299,8 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
                   kv_blocks=0 if cuda else 1024, topk=int(os.environ.get("MCP_TOPK", "32")))
     t0 = time.perf_counter()
     planner = LocalPlanner.from_settings(st, reg)
+    from mcp_amd.utils.heap import settle as settle_heap
+    settle_heap()                  # as the server does once it is up
     startup_s = time.perf_counter() - t0
     app = create_app(st, registry=reg, planner=planner,
                      transport=httpx.MockTransport(lambda r: httpx.Response(200, json={})))
@@ -349,9 +410,12 @@ if __name__ == "__main__":
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--out", default=None, help="plumbing: also append the JSON lines here")
+    ap.add_argument("--with-reference", action="store_true",
+                    help="plumbing: time a stubbed scratch copy of /root/reference/control_plane.py "
+                         "in an isolated child process (off by default)")
     a = ap.parse_args()
     if a.which == "plumbing":
-        plumbing(out=a.out)
+        plumbing(out=a.out, with_reference=a.with_reference)
     elif a.which == "e2e":
         e2e(a.n, a.model, a.runs, a.clients, a.churn)
     else:

@@ -239,3 +239,38 @@ def test_llama3_8b_full_width_layers_match_fp32():
     got2 = model.forward(pack(step2, cfg.group, "cuda"), kv).float().cpu()
     want2 = cpu.forward(pack(step2, cfg.group, "cpu"), kvc).float()
     assert ((got2 - want2).norm() / want2.norm()).item() < 3e-2
+
+
+def test_weight_prefetch_step_with_no_logit_rows_joins_side_stream(monkeypatch):
+    """with MCP_WEIGHT_PREFETCH on, a step that samples no row
+    (the last layer returns early) still joins the prefetch side stream:
+    eagerly, and inside a captured hipGraph (an unjoined side stream is a
+    capture error)."""
+    import numpy as np
+    import mcp_amd.models.llama as llama_mod
+    from mcp_amd.engine.batch import StepInputs, pack
+    from mcp_amd.engine.kv_cache import KVCache
+    monkeypatch.setattr(llama_mod, "_PF_ON", True)
+    model = LlamaModel.random("tiny", "cuda", seed=3)
+    assert model._pf_side is not None and model.fused_norm
+    cfg = model.cfg
+    T = 8
+    step = StepInputs(token_ids=np.arange(T, dtype=np.int32), positions=np.arange(T, dtype=np.int32),
+                      slots=np.arange(T, dtype=np.int32), q_start=np.asarray([0], np.int32),
+                      q_len=np.asarray([T], np.int32), ctx_len=np.asarray([T], np.int32),
+                      block_table=np.asarray([[0]], np.int32),
+                      logit_rows=np.zeros(0, np.int32))
+    kv = KVCache(cfg.layers, cfg.kv_heads, cfg.head_dim, 4, "cuda")
+    packed = pack(step, cfg.group, "cuda")
+    out = model.forward(packed, kv)
+    assert out.shape[0] == 0
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = model.forward(packed, kv)
+    g.replay()
+    torch.cuda.synchronize()
+    assert out.shape[0] == 0

@@ -261,3 +261,26 @@ def test_fast_post_path_matches_client_post(caplog):
     assert o._fast_ok()
     o.client.cookies.set("sid", "1")                 # cookie jars take client.post
     assert not o._fast_ok()
+
+
+def test_fast_post_path_follows_client_header_changes_and_close():
+    """headers set on the client after the first call are
+    sent by the fast path (as client.post sends them), and a closed client
+    raises client.post's own error."""
+    seen = []
+
+    def handler(request: httpx.Request):
+        seen.append(dict(request.headers))
+        return httpx.Response(200, json={"ok": True})
+
+    o = make_orch(handler)
+    assert run(o._post("http://a/api", {"x": 1})) == {"ok": True}
+    o.client.headers["X-Trace"] = "t-1"
+    run(o._post("http://a/api", {"x": 1}))
+    o.client.headers["X-Trace"] = "t-2"
+    run(o._post("http://a/api", {"x": 1}))
+    assert "x-trace" not in seen[0] and seen[1]["x-trace"] == "t-1" and seen[2]["x-trace"] == "t-2"
+    assert o._fast_ok()
+    run(o.client.aclose())
+    with pytest.raises(RuntimeError, match="client has been closed"):
+        run(o._post("http://a/api", {"x": 1}))

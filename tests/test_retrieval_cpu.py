@@ -166,3 +166,35 @@ def test_background_index_sees_a_registration_made_just_before_the_search():
         assert idx._catch_up() and idx.sync() == 1 and "bulk-0" in idx.names
     finally:
         idx.stop_background()
+
+
+def test_engine_thread_search_never_waits_for_the_diff_lock():
+    """while the refresher holds ``_diff_lock`` (diffing and
+    embedding a backlog), a search on the engine thread must not block on it:
+    it serves the current index and leaves the backlog to the refresher."""
+    reg = MemoryRegistry(synthetic_registry(200, seed=5))
+    idx = SchemaIndex(reg, dim=256)
+    idx.refresh()
+    idx.start_background(poll_s=60.0)              # the refresher never runs in this test
+    try:
+        reg.register(make_service("late-arrival", {"x": "string"}, {"y": "string"}))
+        assert idx._diff_lock.acquire()            # stand-in for a refresher mid-diff
+        done = threading.Event()
+        out = []
+
+        def engine_thread():
+            out.append(idx.search("late arrival", 3, reg.list_services()))
+            done.set()
+
+        th = threading.Thread(target=engine_thread, daemon=True)
+        th.start()
+        try:
+            assert done.wait(5.0), "search() blocked on the refresher's diff lock"
+        finally:
+            idx._diff_lock.release()
+        th.join(5.0)
+        assert out and len(out[0]) == 3
+        assert "late-arrival" not in idx.names     # taken by the next catch-up, not inline
+        assert idx._catch_up() and idx.sync() == 1 and "late-arrival" in idx.names
+    finally:
+        idx.stop_background()
