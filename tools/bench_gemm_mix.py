@@ -1,4 +1,4 @@
-"""Replay the headline bench's GEMM mix (tools/gemm_shapes_bench.jsonl, a copy of profiles/gemm_shapes_bench_r1.jsonl:
+"""Replay the headline bench's GEMM mix (profiles/gemm_shapes_bench_r1.jsonl:
 every (M, N, K) the bench launched, with its call count) through our
 dispatch - with the production epilogue of each projection - and through
 hipBLASLt (torch), cold weights (each call reads the next of > 1 GB of weight
@@ -18,7 +18,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import mcp_amd.ops as ops  # noqa: E402
 
-trace = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_shapes_bench.jsonl")
+trace = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "gemm_shapes_bench_r1.jsonl")
 min_m = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 rows = [json.loads(l) for l in open(trace) if l.startswith("{")]
 calls = collections.Counter()

@@ -1,6 +1,6 @@
 """The headline's four projection families at M = 2560 through the production
 dispatch (plan heights, production epilogues), 6 launches each, for a
-rocprofv3 --pmc pass (tools/gpu/pmc_gemm_head.sh, tools/pmc_summary.py)."""
+rocprofv3 --pmc pass (tools/gpu_run.sh pmc, tools/pmc_summary.py)."""
 import math
 import os
 import sys
