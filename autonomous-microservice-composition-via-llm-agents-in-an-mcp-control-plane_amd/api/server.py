@@ -68,6 +68,71 @@ class ExecuteResponse(BaseModel):
     errors: dict
 
 
+def plan_response_json(graph) -> bytes:
+    """The ``/plan`` response body: the validated model serialised once (a
+    non-object plan raises here -> 500, T8).  Shared by the FastAPI route and
+    the fast front end (api/fasthttp.py)."""
+    resp = PlanResponse(graph=graph)
+    return resp.__pydantic_serializer__.to_json(resp)
+
+
+def replica_slice(groups: list, spec: Optional[str]) -> list:
+    """This API worker's share of the node's replicas: ``spec`` = "w/n" takes
+    the contiguous groups [w R / n, (w + 1) R / n) of R (``None``: all)."""
+    if not spec:
+        return groups
+    w, n = (int(x) for x in spec.split("/"))
+    R = len(groups)
+    if not 0 <= w < n <= R:
+        raise ValueError(f"replica slice {spec} of {R} replicas")
+    return groups[w * R // n:(w + 1) * R // n]
+
+
+def build_planner(settings: Settings, registry: BaseRegistry,
+                  planner_transport: Optional[httpx.AsyncBaseTransport] = None) -> Planner:
+    """The planner backend ``settings`` name: stub, a local engine (one
+    process, a TP group, or DP replicas behind a router), or a hosted
+    OpenAI-compatible endpoint."""
+    if settings.planner_backend == "local":
+        if settings.replicas > 1 or settings.router:
+            # request-level DP over replicas, each a TP group of
+            # settings.tp ranks (MCP_REPLICAS=2 MCP_TP=4: two TP=4 planners);
+            # with several API workers each routes to its own slice
+            from ..parallel.router import ReplicaConfig, ReplicaRouter, group_devices
+            cfg = ReplicaConfig(model=settings.model, max_batch=settings.max_batch,
+                                max_nodes=settings.max_nodes, min_nodes=settings.min_nodes,
+                                seed=settings.seed,
+                                num_blocks=settings.kv_blocks or None,
+                                max_step_tokens=settings.max_step_tokens,
+                                temperature=settings.temperature,
+                                retrieval_threshold=settings.retrieval_threshold,
+                                topk=settings.topk, embed_dim=settings.embed_dim,
+                                tp=max(1, int(settings.tp)))
+            groups = replica_slice(group_devices(settings.replicas, cfg.tp), settings.replica_slice)
+            return ReplicaRouter(groups, settings.model, registry, config=cfg)
+        if settings.tp > 1:
+            # this process becomes TP rank 0 (driver); ranks 1..tp-1 are
+            # spawned worker processes (parallel/tp_serve.py)
+            from ..parallel.tp_serve import TPPlanner
+            return TPPlanner.launch(settings, registry)
+        from ..planner.local import LocalPlanner
+        return LocalPlanner.from_settings(settings, registry)
+    if settings.planner_backend == "openai":
+        from ..planner.remote import RemotePlanner
+        return RemotePlanner(registry, settings.openai_base_url, settings.openai_api_key,
+                             settings.remote_model, settings.temperature,
+                             transport=planner_transport)
+    return StubPlanner(registry)
+
+
+def make_registry_from(settings: Settings) -> BaseRegistry:
+    registry = make_registry(settings.redis_url, settings.services_prefix)
+    if settings.synthetic_services > 0 and not settings.redis_url:
+        from ..registry import synthetic_registry
+        registry.register_many(synthetic_registry(settings.synthetic_services, seed=1))
+    return registry
+
+
 def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegistry] = None,
                planner: Optional[Planner] = None,
                transport: Optional[httpx.AsyncBaseTransport] = None,
@@ -79,44 +144,13 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
     a test process, where frozen objects would never be collected."""
     settings = settings or Settings.from_env()
     if registry is None:
-        registry = make_registry(settings.redis_url, settings.services_prefix)
-        if settings.synthetic_services > 0 and not settings.redis_url:
-            from ..registry import synthetic_registry
-            registry.register_many(synthetic_registry(settings.synthetic_services, seed=1))
+        registry = make_registry_from(settings)
     state = {}
 
     def _make_planner() -> Planner:
         if planner is not None:
             return planner
-        if settings.planner_backend == "local":
-            if settings.replicas > 1 or settings.router:
-                # request-level DP over replicas, each a TP group of
-                # settings.tp ranks (MCP_REPLICAS=2 MCP_TP=4: two TP=4 planners)
-                from ..parallel.router import ReplicaConfig, ReplicaRouter, group_devices
-                cfg = ReplicaConfig(model=settings.model, max_batch=settings.max_batch,
-                                    max_nodes=settings.max_nodes, min_nodes=settings.min_nodes,
-                                    seed=settings.seed,
-                                    num_blocks=settings.kv_blocks or None,
-                                    max_step_tokens=settings.max_step_tokens,
-                                    temperature=settings.temperature,
-                                    retrieval_threshold=settings.retrieval_threshold,
-                                    topk=settings.topk, embed_dim=settings.embed_dim,
-                                    tp=max(1, int(settings.tp)))
-                return ReplicaRouter(group_devices(settings.replicas, cfg.tp), settings.model,
-                                     registry, config=cfg)
-            if settings.tp > 1:
-                # this process becomes TP rank 0 (driver); ranks 1..tp-1 are
-                # spawned worker processes (parallel/tp_serve.py)
-                from ..parallel.tp_serve import TPPlanner
-                return TPPlanner.launch(settings, registry)
-            from ..planner.local import LocalPlanner
-            return LocalPlanner.from_settings(settings, registry)
-        if settings.planner_backend == "openai":
-            from ..planner.remote import RemotePlanner
-            return RemotePlanner(registry, settings.openai_base_url, settings.openai_api_key,
-                                 settings.remote_model, settings.temperature,
-                                 transport=planner_transport)
-        return StubPlanner(registry)
+        return build_planner(settings, registry, planner_transport)
 
     @contextlib.asynccontextmanager
     async def lifespan(app: FastAPI):
@@ -165,12 +199,13 @@ def create_app(settings: Optional[Settings] = None, registry: Optional[BaseRegis
 
     @app.post("/plan", response_model=PlanResponse)
     async def plan_intent(req: PlanRequest):
-        resp = PlanResponse(graph=await _plan(req.intent))   # a non-object plan -> 500 (T8)
+        graph = await _plan(req.intent)
         if not req.explain:
             # the validated model serialised once, straight into the response:
             # FastAPI's response_model pass would validate and encode it again
             # (~1/4 of the API process's time per plan at thousands of plans/s)
-            return Response(resp.__pydantic_serializer__.to_json(resp), media_type="application/json")
+            return Response(plan_response_json(graph), media_type="application/json")
+        resp = PlanResponse(graph=graph)                     # a non-object plan -> 500 (T8)
         try:
             text = _explain(resp.graph)
         except Exception as e:     # a plan the orchestrator would reject (T2 / cycle)
@@ -222,17 +257,127 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
+def _reuseport_socket(host: str, port: int):
+    import socket
+    fam = socket.AF_INET6 if ":" in host else socket.AF_INET
+    sock = socket.socket(fam, socket.SOCK_STREAM)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    sock.bind((host, port))
+    sock.listen(2048)
+    sock.set_inheritable(True)
+    return sock
+
+
+def _api_worker(idx: int, n: int, host: str, port: int, access_log: bool,
+                http: str = "fast"):  # pragma: no cover - process entry
+    """One API worker process: builds its planner (its slice of the node's
+    replicas) BEFORE it binds, so the kernel never hands a connection to a
+    worker that is still loading; then serves on its own SO_REUSEPORT socket."""
+    import os
+    os.environ["MCP_REPLICA_SLICE"] = f"{idx}/{n}"
+    settings = Settings.from_env()
+    registry = make_registry_from(settings)
+    planner = build_planner(settings, registry)
+    app = create_app(settings, registry=registry, planner=planner, settle_gc=True)
+    sock = _reuseport_socket(host, port)
+    msg = f"mcp api worker {idx}/{n} ready on {host}:{port} ({http})"
+    if http == "fast":
+        import asyncio
+        from .fasthttp import serve_fast
+        asyncio.run(serve_fast(app, sock=sock, ready=lambda: print(msg, flush=True)))
+        return
+    import uvicorn
+    server = uvicorn.Server(uvicorn.Config(app, host=host, port=port, access_log=access_log))
+    print(msg, flush=True)
+    server.run(sockets=[sock])
+
+
+def serve(host: str, port: int, workers: int = 1, access_log: bool = True,
+          max_restarts: int = 3, http: str = "fast") -> int:  # pragma: no cover - process entry
+    """Run the API.  ``http``: "fast" (api/fasthttp.py: own HTTP/1.1 parser,
+    /plan answered straight from the planner, everything else through the
+    FastAPI app) or "uvicorn" (the reference's server).  ``workers`` > 1: a
+    supervisor (which never touches the GPU) spawns that many API worker
+    processes on one SO_REUSEPORT port; the kernel spreads connections over
+    them, each worker parses HTTP and routes to its own contiguous slice of
+    the node's planner replicas (MCP_REPLICAS / MCP_TP), so no single process
+    carries every request of the node.  A worker that dies is restarted (its
+    replicas with it) up to ``max_restarts`` times."""
+    if workers <= 1:
+        if http == "fast":
+            import asyncio
+            from .fasthttp import serve_fast
+            asyncio.run(serve_fast(create_app(settle_gc=True), host=host, port=port,
+                                   ready=lambda: print(f"mcp api ready on {host}:{port} (fast)",
+                                                       flush=True)))
+            return 0
+        import uvicorn
+        uvicorn.run(create_app(settle_gc=True), host=host, port=port, access_log=access_log)
+        return 0
+    import multiprocessing as mp
+    import signal
+    import time
+    settings = Settings.from_env()
+    if settings.planner_backend == "local" and (settings.replicas > 1 or settings.router):
+        if workers > settings.replicas:
+            raise SystemExit(f"--workers {workers} > MCP_REPLICAS {settings.replicas}: "
+                             "every API worker routes to at least one replica")
+    ctx = mp.get_context("spawn")
+    procs = {}
+    restarts = [0] * workers
+
+    def start(i):
+        p = ctx.Process(target=_api_worker, args=(i, workers, host, port, access_log, http),
+                        name=f"mcp-api-{i}")
+        p.start()
+        procs[i] = p
+
+    stopping = []
+
+    def stop(signum, frame):
+        stopping.append(signum)
+
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
+    for i in range(workers):
+        start(i)
+    rc = 0
+    while not stopping:
+        time.sleep(0.2)
+        for i, p in list(procs.items()):
+            if not p.is_alive() and not stopping:
+                if restarts[i] >= max_restarts:
+                    stopping.append("dead")
+                    rc = 1
+                    break
+                restarts[i] += 1
+                start(i)
+    for p in procs.values():
+        if p.is_alive():
+            p.terminate()
+    for p in procs.values():
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    return rc
+
+
 def main():  # pragma: no cover - CLI entry (reference :155-157)
     import argparse
-
-    import uvicorn
+    import os
     ap = argparse.ArgumentParser(description="MI355X MCP control plane")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--workers", type=int, default=int(os.environ.get("MCP_API_WORKERS", "1")),
+                    help="API worker processes on one SO_REUSEPORT port (MCP_API_WORKERS)")
+    ap.add_argument("--http", choices=["fast", "uvicorn"], default=os.environ.get("MCP_HTTP", "fast"),
+                    help="front end: the lean HTTP/1.1 server (api/fasthttp.py) or uvicorn")
     ap.add_argument("--no-access-log", action="store_true",
                     help="skip uvicorn's per-request access log line")
     args = ap.parse_args()
-    uvicorn.run(create_app(settle_gc=True), host=args.host, port=args.port, access_log=not args.no_access_log)
+    raise SystemExit(serve(args.host, args.port, args.workers, not args.no_access_log,
+                           http=args.http))
 
 
 if __name__ == "__main__":  # pragma: no cover

@@ -42,6 +42,9 @@ class Settings:
     tp: int = 1                              # >1: this process is TP rank 0, workers spawned (parallel.tp_serve)
     replicas: int = 1
     router: bool = False                     # DP router + replica processes even at replicas == 1
+    api_workers: int = 1                     # >1: API worker processes on one SO_REUSEPORT port,
+                                             # each routing to its own slice of the replicas
+    replica_slice: Optional[str] = None      # "w/n": this API worker's slice (set by the supervisor)
     max_batch: int = 256
     max_step_tokens: int = 8192
     kv_blocks: int = 0                       # 0 -> size from free HBM
@@ -79,6 +82,8 @@ class Settings:
             tp=_env("MCP_TP", 1, int),
             replicas=_env("MCP_REPLICAS", 1, int),
             router=_env("MCP_ROUTER", False, bool),
+            api_workers=_env("MCP_API_WORKERS", 1, int),
+            replica_slice=_env("MCP_REPLICA_SLICE", None),
             max_batch=_env("MCP_MAX_BATCH", 256, int),
             max_step_tokens=_env("MCP_MAX_STEP_TOKENS", 8192, int),
             kv_blocks=_env("MCP_KV_BLOCKS", 0, int),

@@ -708,6 +708,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1 if an AGPR GEMM of this shape and tile count runs the persistent form");
   m.def("gemm_persist_force", &gemm_persist_force,
         "persistent AGPR GEMM: -1 plan / MCP_GEMM_PERSIST, 0 off, 1 when tiles > CUs, 2 always");
+  m.def("gemm_wide_force", &gemm_wide_force,
+        "AGPR GEMM epilogue: -1 MCP_GEMM_WIDE_EPI, 0 LDS-staged, 1 wide direct (permlane16 + 16-B stores)");
   m.def("gemm_plan_clear", &gemm_plan_clear);
   m.def("gemm_flex_count", &gemm_flex_count, "flex tile candidates (gemm(..., algo=16 + i))");
   m.def("gemm_flex_silu_ok", &gemm_flex_silu_ok, "1 if flex candidate i has the SwiGLU epilogue");

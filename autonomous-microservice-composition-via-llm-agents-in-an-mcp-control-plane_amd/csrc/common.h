@@ -98,6 +98,24 @@ DEV float norm_row_scale(const NE& ne, int m) {
   const float ss = (float)ne.ss_in[m] * (1.f / SS_FIX);
   return rsqrtf(ss * ne.inv_h + ne.eps);
 }
+// the row scales of N rows at once: the wave-uniform "no norm" test is hoisted
+// out and every load issued before the first use (norm_row_scale in an
+// unrolled loop makes hipcc branch around each load and wait vmcnt(0) per
+// row - N dependent round trips, and a drain of every DMA still in flight:
+// cdna_hip_programming.md §5 item 4(c), T20)
+template <int N, class NE>
+DEV void norm_row_scales(const NE& ne, const int (&m)[N], float (&out)[N]) {
+  if (!ne.ss_in) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = 1.f;
+    return;
+  }
+  unsigned long long v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = ne.ss_in[m[i]];
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = rsqrtf((float)v[i] * (1.f / SS_FIX) * ne.inv_h + ne.eps);
+}
 // sum of squares of the bf16-rounded values a residual epilogue stores
 DEV float sumsq_bf16x4(const bf16x4& v) {
   float s = 0.f;
@@ -154,6 +172,88 @@ DEV void store_direct(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y,
         *reinterpret_cast<bf16x4*>(Y + (size_t)m * N + n) = o;
         if (EPI == 1) ss += sumsq_bf16x4(o);
       }
+    }
+    if (EPI == 1 && ne.ss_out) {
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (fq == 0 && m < M) ss_atomic_add(ne.ss_out + m, ss);
+    }
+  }
+}
+
+// Wide direct epilogue of a wave's 16x16x32 accumulator grid, 8 column tiles
+// (128 columns) per wave: lane (fr = lane & 15, fq = lane >> 4) holds rows
+// mb + 16 mt + fr, columns 16 nt + 4 fq .. +3.  Column-tile pairs (2p, 2p+1)
+// are exchanged across lane rows by v_permlane16_swap (odd 16-lane rows of the
+// first operand <-> even rows of the second), after which lane fq holds the 8
+// consecutive columns 32 p + 16 (fq & 1) + 8 (fq >> 1) .. +7: one 16-B store
+// per lane, 64 contiguous bytes per row per instruction, no LDS staging and no
+// barrier (cdna_hip_programming.md T21, here for the 16x16 layout).
+DEV void swap_col_pairs(u32x2& a, u32x2& b) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  a.x = r0[0];
+  b.x = r0[1];
+  a.y = r1[0];
+  b.y = r1[1];
+}
+
+// EPI 0 plain, 1 residual (bf16 product + R, as the staged epilogue rounds it;
+// with ne.ss_out each stored row's sum of squares), 2 SwiGLU of interleaved
+// gate | up 16-column groups (64 output columns per wave; rsc = the fused
+// RMSNorm row scales of the wave's MT row tiles).  Y / R rows have ``ldy``
+// elements; the wave's first output column is ``col0``.  Stores go through a
+// range-checked buffer descriptor (rows >= M dropped, no branch); R rows are
+// clamped and all loaded up front.
+template <int EPI, int MT, class RS, class NE>
+DEV void store_wide(const f32x4 (&acc)[MT][8], RS rsY, const bf16* __restrict__ R, int M, int ldy,
+                    int mb, int col0, int fr, int fq, const float* rsc, const NE& ne) {
+  constexpr int NPAIR = EPI == 2 ? 2 : 4;
+  const int lcol = 16 * (fq & 1) + 8 * (fq >> 1);
+  bf16x8 rres[EPI == 1 ? MT * NPAIR : 1];
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p) {
+        const int m = min(mb + mt * 16 + fr, M - 1);
+        rres[mt * NPAIR + p] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldy + col0 + 32 * p + lcol);
+      }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mb + mt * 16 + fr;
+    float ss = 0.f;
+#pragma unroll
+    for (int p = 0; p < NPAIR; ++p) {
+      bf16x4 oa, ob;
+      if constexpr (EPI == 2) {
+        const float s = rsc[mt];
+        const f32x4 ga = acc[mt][4 * p] * s, ua = acc[mt][4 * p + 1] * s;
+        const f32x4 gb = acc[mt][4 * p + 2] * s, ub = acc[mt][4 * p + 3] * s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          oa[e] = (bf16)(ga[e] / (1.f + __expf(-ga[e])) * ua[e]);
+          ob[e] = (bf16)(gb[e] / (1.f + __expf(-gb[e])) * ub[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          oa[e] = (bf16)acc[mt][2 * p][e];
+          ob[e] = (bf16)acc[mt][2 * p + 1][e];
+        }
+      }
+      u32x2 a = __builtin_bit_cast(u32x2, oa), b = __builtin_bit_cast(u32x2, ob);
+      swap_col_pairs(a, b);
+      bf16x8 v = __builtin_bit_cast(bf16x8, u32x4{a.x, a.y, b.x, b.y});
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rres[mt * NPAIR + p][e]);
+        if (ne.ss_out) ss += m < M ? sumsq_bf16x8(v) : 0.f;
+      }
+      const unsigned off = (unsigned)(((size_t)m * ldy + col0 + 32 * p + lcol) * 2);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsY,
+                                             m < M ? off : 0x80000000u, 0, 0);
     }
     if (EPI == 1 && ne.ss_out) {
       ss += __shfl_xor(ss, 16, 64);

@@ -85,7 +85,7 @@ constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 
 // The epilogue goes through LDS (row-contiguous 16-B stores); the direct
 // MFMA-layout store measured 10-15 % slower (profiles/gemm_tuning.md).
-template <int EPI, int BMT>
+template <int EPI, int BMT, bool WIDE = false>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
@@ -121,16 +121,13 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((size_t)N * K * 2),
                                                      0x00020000);
   // The buffer range check covers voffset (+ the instruction offset) but NOT
-  // soffset, so rows that can fall past the end of X (the last M-tile) are
-  // clamped in per-lane offsets; W rows are always in range (N % 256 == 0,
-  // launcher) and step through soffset.
+  // soffset: X rows past M (the last M-tile) go in voffset, so they fall
+  // outside the descriptor and read nothing (their outputs are never stored);
+  // instruction q reads rows 8 q further, + 16 q K bytes - a wave-uniform
+  // addend, one VALU add per DMA instead of QA live offsets.  W rows are
+  // always in range (N % 256 == 0, launcher) and step through soffset.
   const int chunk = (lane & 7) ^ (lane >> 3);
-  // (sized 8, not QA: an array sized by a local constexpr and captured by the
-  // DMA lambda makes hipcc's host pass silently drop the kernel's stub)
-  unsigned offA[8];
-#pragma unroll
-  for (int q = 0; q < QA; ++q)
-    offA[q] = (unsigned)(((size_t)min(m0 + 8 * QA * wave + 8 * q + (lane >> 3), M - 1) * K + chunk * 8) * 2);
+  const unsigned offA0 = (unsigned)(((size_t)(m0 + 8 * QA * wave + (lane >> 3)) * K + chunk * 8) * 2);
   const unsigned offB = (unsigned)(((lane >> 3) * K + chunk * 8) * 2);
   const int rowB0 = n0 + 64 * wave;                  // first W row of this wave's instructions
   // k-tile t of the trailing (unconsumed) DMAs is clamped to the last one:
@@ -146,7 +143,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     if (b)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, offB, (rowB0 + 8 * q) * K * 2 + kb, 0, 0);
     else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA[q], kb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA0 + q * 16 * K, kb, 0, 0);
   };
 
   // ---- fragment reads: wave (wm, wn) owns rows wm*WROWS.., cols wn*128..;
@@ -254,7 +251,20 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // and pad MFMA results -> VALU reads (inline asm is not padded)
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
-  {
+  if constexpr (WIDE && EPI != 3) {
+    // ---- wide direct epilogue (common.h store_wide): straight from the
+    //      accumulators, 16-B stores after a permlane16 exchange, no LDS
+    const int ldy = EPI == 2 ? N / 2 : N;
+    const int col0 = EPI == 2 ? (n0 + wn * 128) / 2 : n0 + wn * 128;
+    float rsc[MTW];
+    int rrow[MTW];
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) rrow[mt] = min(m0 + wm * WROWS + mt * 16 + fr, M - 1);
+    if constexpr (EPI == 2) norm_row_scales(ne, rrow, rsc);
+    const auto rsY = __builtin_amdgcn_make_buffer_rsrc((void*)Y, (short)0, (int)((size_t)M * ldy * 2),
+                                                       0x00020000);
+    store_wide<EPI, MTW>(acc, rsY, R, M, ldy, m0 + wm * WROWS, col0, fr, fq, rsc, ne);
+  } else {
     // ---- staged epilogue.  The direct one below stores 8 B per lane in
     //      32-B row pieces (the MFMA layout: lane = 4 columns of one row); at
     //      one workgroup per CU nothing hides those stores and they cost
@@ -303,8 +313,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     // EPI 2 / 3: fused RMSNorm of the input rows (1 when none), loaded up front
     float rsc[EPI >= 2 ? MTW : 1];
     if constexpr (EPI >= 2) {
+      int rrow[MTW];
 #pragma unroll
-      for (int mt = 0; mt < MTW; ++mt) rsc[mt] = norm_row_scale(ne, min(m0 + wm * WROWS + mt * 16 + fr, M - 1));
+      for (int mt = 0; mt < MTW; ++mt) rrow[mt] = min(m0 + wm * WROWS + mt * 16 + fr, M - 1);
+      norm_row_scales(ne, rrow, rsc);
     }
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt) {
@@ -515,6 +527,17 @@ int gemm256d_group(int M, int N, int K) {
   return g > 0 ? g : 4;
 }
 
+// Wide direct epilogue (store_wide) instead of the LDS-staged one:
+// MCP_GEMM_WIDE_EPI=1 / gemm_wide_force (tools); needs the output < 2 GiB
+// (buffer descriptor)
+static int g_wide_force = -1;
+void gemm_wide_force(int w) { g_wide_force = w; }
+bool gemm_wide_on(int M, int N, int epi) {
+  static const int env = getenv("MCP_GEMM_WIDE_EPI") ? atoi(getenv("MCP_GEMM_WIDE_EPI")) : 0;
+  const int on = g_wide_force >= 0 ? g_wide_force : env;
+  return on && epi >= 0 && epi <= 2 && (size_t)M * (epi == 2 ? N / 2 : N) * 2 < (1ull << 31);
+}
+
 template <int BMT>
 static int launch_height(const void* X, const void* W, void* Y, const void* R, int M, int N,
                          int K, int epi, dim3 grid, int group, const RopeArgs& ra, hipStream_t s) {
@@ -522,6 +545,14 @@ static int launch_height(const void* X, const void* W, void* Y, const void* R, i
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
+  if (gemm_wide_on(M, N, epi)) {
+    switch (epi) {
+      case 0: gemm_tn_256d<0, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+      case 1: gemm_tn_256d<1, BMT, true><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;
+      case 2: gemm_tn_256d<2, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+      default: return 2;
+    }
+  }
   switch (epi) {
     case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
     case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;

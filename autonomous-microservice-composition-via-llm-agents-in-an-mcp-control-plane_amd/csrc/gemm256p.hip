@@ -65,7 +65,7 @@ DEV void tile_coords(int t, int nm, int nn, int bm, int group, int& m0, int& n0)
 constexpr int ops_at(int j, int n, int P) { return ((j + 1) * n) / P - (j * n) / P; }
 constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 
-template <int EPI, int BMT>
+template <int EPI, int BMT, bool WIDE = false>
 struct Geo {
   static constexpr int MTW = BMT / 32;              // 16-row MFMA tiles per wave
   static constexpr int WROWS = BMT / 2;             // rows per wave
@@ -85,7 +85,10 @@ struct Geo {
   // VMEM instructions every wave's epilogue issues for sure (range-checked
   // buffer stores; EPI 1 also its residual loads): the next tile's first
   // barrier leaves that many younger than the DMAs it waits for in flight
-  static constexpr int NEPI_RAW = EPI == 3 ? 0 : (WROWS / RPS) * (EPI == 1 ? 2 : 1);
+  // (the wide epilogue: MTW x 4 (EPI 2: x 2) stores, EPI 1 as many residual loads)
+  static constexpr int NEPI_RAW = EPI == 3 ? 0
+                                  : WIDE ? MTW * (EPI == 2 ? 2 : 4) * (EPI == 1 ? 2 : 1)
+                                         : (WROWS / RPS) * (EPI == 1 ? 2 : 1);
   static constexpr int NEPI = NEPI_RAW > 63 ? 63 : NEPI_RAW;
 };
 
@@ -101,20 +104,19 @@ DEV void waitcnt_vm_lgkm0() {
 // select could take goes to scratch).  At namespace scope: a class local to
 // the kernel, used by the kernel's lambdas, leaves hipcc's host pass without
 // the kernel's launch stub (undefined symbol at load time).
-typedef __attribute__((ext_vector_type(8))) unsigned u32x8;
 struct TileDma {
-  u32x8 offA;
+  unsigned offA0;                                   // this lane's X row of A instruction 0
   int rowB0;
 };
 
-template <int EPI, int BMT>
+template <int EPI, int BMT, bool WIDE = false>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
                                                        int K, int group, const RopeArgs ra,
                                                        const NormEpi ne) {
-  using G_ = Geo<EPI, BMT>;
+  using G_ = Geo<EPI, BMT, WIDE>;
   constexpr int MTW = G_::MTW, WROWS = G_::WROWS, PIECE_A = G_::PIECE_A, SLOT_B = G_::SLOT_B;
   constexpr int QA = G_::QA, NDMA = G_::NDMA, NRD = G_::NRD, NP = G_::NP;
   constexpr int OUTW = G_::OUTW, RB = G_::RB, NCH = G_::NCH, RPS = G_::RPS;
@@ -140,11 +142,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
   const unsigned offB = (unsigned)(((lane >> 3) * K + chunk * 8) * 2);
   const int nt = K / BK;                             // >= 2, even (launcher)
 
+  // X rows past M fall outside the buffer descriptor (voffset range check):
+  // their LDS rows are never stored, so no clamp; instruction q reads the rows
+  // 8 q further: + 16 q K bytes, a wave-uniform addend (one VALU add per DMA
+  // instead of 8 live offsets, which spilled at 256 rows)
   auto tile_dma = [&](int m0, int n0, TileDma& d) {
-#pragma unroll
-    for (int q = 0; q < QA; ++q)
-      d.offA[q] = (unsigned)(((size_t)min(m0 + 8 * QA * wave + 8 * q + (lane >> 3), M - 1) * K +
-                              chunk * 8) * 2);
+    d.offA0 = (unsigned)(((size_t)(m0 + 8 * QA * wave + (lane >> 3)) * K + chunk * 8) * 2);
     d.rowB0 = n0 + 64 * wave;
   };
   TileDma dstate;
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
     if (b)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, dst, 16, offB, (dstate.rowB0 + 8 * q) * K * 2 + kb, 0, 0);
     else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, dstate.offA[q], kb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, dstate.offA0 + q * 16 * K, kb, 0, 0);
   };
 
   const int wm = wave >> 1, wn = wave & 1;
@@ -286,8 +289,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
     const int head = (n0 + wn * 128) >> 7;
     const bool rotate = EPI == 3 && head < ra.Hq + ra.Hkv;
     constexpr int NST = WROWS / RPS;                 // store rows per lane, whole tile
-    bf16x8 rres[EPI == 1 ? NST : 1];
-    if constexpr (EPI == 1) {
+    bf16x8 rres[EPI == 1 && !WIDE ? NST : 1];
+    if constexpr (EPI == 1 && !WIDE) {
 #pragma unroll
       for (int i = 0; i < NST; ++i) {
         const int m = min(m0 + wm * WROWS + i * RPS + lr, M - 1);
@@ -301,8 +304,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
     }
     float rsc[EPI >= 2 ? MTW : 1];
     if constexpr (EPI >= 2) {
+      int rrow[MTW];
 #pragma unroll
-      for (int mt = 0; mt < MTW; ++mt) rsc[mt] = norm_row_scale(ne, min(m0 + wm * WROWS + mt * 16 + fr, M - 1));
+      for (int mt = 0; mt < MTW; ++mt) rrow[mt] = min(m0 + wm * WROWS + mt * 16 + fr, M - 1);
+      norm_row_scales(ne, rrow, rsc);
     }
     int rslot[EPI == 3 ? NST : 1];
     if (EPI == 3 && head >= ra.Hq) {
@@ -310,6 +315,17 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
       for (int i = 0; i < NST; ++i)
         rslot[i] = ra.slots[min(m0 + wm * WROWS + i * RPS + lr, M - 1)];
     }
+    if constexpr (WIDE && EPI != 3) {
+      // wide direct epilogue (common.h store_wide): no staging passes, no
+      // barrier; the stores drain under the next tile's first k-tiles
+      float rsc2[MTW];
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) {
+        if constexpr (EPI == 2) rsc2[mt] = rsc[mt];
+        else rsc2[mt] = 1.f;
+      }
+      store_wide<EPI, MTW>(acc, rsY, R, M, ldy, m0 + wm * WROWS, col0, fr, fq, rsc2, ne);
+    } else {
     auto put = [&](int row, int col, const bf16x4& v) __attribute__((always_inline)) {
       const int byte = col * 2;
       *reinterpret_cast<bf16x4*>(stg + row * RB + (((byte >> 4) ^ (row & (NCH - 1))) << 4) +
@@ -412,6 +428,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256p(const bf16* __restrict__ 
         }
       }
     }
+    }
     if (!has_next) break;
     // ---- next tile: its k-tiles 0 / 1 are in slots 0 / 1 (or in flight), its
     //      first fragments in F[0]
@@ -440,6 +457,14 @@ static int launch_p_height(const void* X, const void* W, void* Y, const void* R,
   auto w = (const bf16*)W;
   auto y = (bf16*)Y;
   auto r = (const bf16*)R;
+  if (gemm_wide_on(M, N, epi)) {
+    switch (epi) {
+      case 0: gemm_tn_256p<0, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+      case 1: gemm_tn_256p<1, BMT, true><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;
+      case 2: gemm_tn_256p<2, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+      default: return 2;
+    }
+  }
   switch (epi) {
     case 0: gemm_tn_256p<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
     case 1: gemm_tn_256p<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;

@@ -55,6 +55,8 @@ void gemm_group_force(int g);               // AGPR kernel tile group: 0 = plan 
 int gemm256d_group(int M, int N, int K);
 void gemm_plan_set_persist(int N, int K, const int* persist, int n);
 int gemm_plan_persist(int M, int N, int K);  // 1 = the persistent AGPR kernel measured faster
+void gemm_wide_force(int w);                // AGPR kernel epilogue: -1 env, 0 staged, 1 wide direct
+bool gemm_wide_on(int M, int N, int epi);   // that choice for one shape (EPI 0-2)
 void gemm_persist_force(int p);             // -1 plan / env, 0 off, 1 multi-wave, 2 always
 int gemm256d_persist(int M, int N, int K, int tiles);
 struct RopeArgs;
