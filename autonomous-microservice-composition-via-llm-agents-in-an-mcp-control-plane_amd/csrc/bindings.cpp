@@ -600,11 +600,24 @@ void car_connect(int64_t h, const at::Tensor& all_handles) {
   TORCH_CHECK(rc == 0, "custom all-reduce: hipIpcOpenMemHandle failed (", rc, ")");
 }
 
-void car_run(int64_t h, const at::Tensor& inp, at::Tensor& out, int64_t mode, int64_t blocks) {
+// ss (optional, int64 [>= rows]): also add each output row's fixed-point sum
+// of squares (the fused RMSNorm statistic of the next layer); rows are the
+// last dimension of inp
+void car_run(int64_t h, const at::Tensor& inp, at::Tensor& out, int64_t mode, int64_t blocks,
+             const c10::optional<at::Tensor>& ss) {
   CHECK_BF16_TENSOR(inp); CHECK_BF16_TENSOR(out);
   TORCH_CHECK(inp.numel() == out.numel(), "all-reduce shapes");
+  unsigned long long* ssp = nullptr;
+  int row_len = 0;
+  if (ss && ss->defined()) {
+    TORCH_CHECK(ss->is_cuda() && ss->scalar_type() == at::kLong && ss->is_contiguous(),
+                "ss: int64 cuda contiguous");
+    row_len = (int)inp.size(-1);
+    TORCH_CHECK(ss->numel() >= inp.numel() / row_len, "ss: one entry per row");
+    ssp = (unsigned long long*)ss->data_ptr();
+  }
   const int rc = car_allreduce((void*)(intptr_t)h, inp.data_ptr(), out.data_ptr(), inp.numel(),
-                               (int)mode, (int)blocks, stream());
+                               (int)mode, (int)blocks, stream(), ssp, row_len);
   TORCH_CHECK(rc == 0, "custom all-reduce launch failed (", rc, ")");
   check_launch("car_run");
 }
@@ -772,7 +785,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("car_handle_bytes", []() { return (int64_t)car_handle_bytes(); });
   m.def("car_init", &car_init);
   m.def("car_connect", &car_connect);
-  m.def("car_run", &car_run);
+  m.def("car_run", &car_run, py::arg("h"), py::arg("inp"), py::arg("out"), py::arg("mode"),
+        py::arg("blocks"), py::arg("ss") = py::none());
   m.def("car_error", [](int64_t h) { return car_error((void*)(intptr_t)h); });
   m.def("car_destroy", [](int64_t h) { car_destroy((void*)(intptr_t)h); });
   m.def("nccl_unique_id", &nccl_unique_id);

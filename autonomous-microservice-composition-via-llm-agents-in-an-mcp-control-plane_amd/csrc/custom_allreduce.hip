@@ -30,6 +30,15 @@
 // coherent host memory, so ``car_error`` is a plain host read (no HIP call,
 // no sync) that the engine makes after every step: a timed-out step is a hard
 // failure, never silently reduced stale data (parallel/comm.py).
+//
+// Fused RMSNorm statistic (TP > 1, VERDICT r4 #3b): with ``ss`` set, every
+// rank also adds the sums of squares of the bf16 rows it writes to ``ss``
+// (int64 fixed point, as the TP = 1 GEMM epilogues do: common.h), so the next
+// layer's QKV / gate|up GEMM scales its accumulators by the row rsqrt and no
+// standalone RMSNorm pass runs between the all-reduce and the next layer.
+// A wave writes 64 consecutive 16-B vectors per iteration; rows are at least
+// 64 vectors long (H >= 512), so those span at most two rows: two wave sums,
+// at most two atomics per 512 elements.
 #include <string.h>
 
 #include "common.h"
@@ -50,6 +59,8 @@ struct CarArgs {
   unsigned* sigs[CAR_MAX_RANKS];     // signal arrays of every rank
   int* err;
   unsigned* ctr;                     // device: [0] completed calls, [1] blocks done this call
+  unsigned long long* ss;            // fused-norm row statistics (nullptr: none)
+  int vpr;                           // 16-byte vectors per row (ss only; >= 64)
   long long nvec;                    // message length in 16-byte vectors
   long long par_vecs;                // staging buffer size per parity, 16-byte vectors
   int rank, world;
@@ -125,28 +136,76 @@ DEV bf16x8 pack8(const float (&s)[8]) {
   return r;
 }
 
-template <int W>
-DEV void sum_range(const CarArgs& a, long long v0, long long v1, bf16x8* dst) {
-  for (long long v = v0 + threadIdx.x; v < v1; v += CAR_THREADS) {
-    bf16x8 x[W];
-#pragma unroll
-    for (int p = 0; p < W; ++p) x[p] = a.bufs[p][v];      // W loads in flight
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < W; ++p) acc8(s, x[p]);
-    dst[v] = pack8(s);
+// the sums of squares of one wave-iteration's 64 vectors (v = base + lane,
+// valid lanes only) into their rows' statistics
+DEV void ss_wave_add(const CarArgs& a, long long v, bool valid, float s) {
+  const int row = valid ? (int)(v / a.vpr) : -1;
+  const int r0 = __shfl(row, 0, 64);                 // lane 0 is always valid
+  const float s0 = wave_sum(row == r0 ? s : 0.f);
+  const bool two = __ballot(row > r0) != 0ull;
+  const float s1 = two ? wave_sum(row > r0 ? s : 0.f) : 0.f;
+  if ((threadIdx.x & 63) == 0) {
+    ss_atomic_add(a.ss + r0, s0);
+    if (two) ss_atomic_add(a.ss + r0 + 1, s1);
   }
 }
 
-DEV void sum_range_dyn(const CarArgs& a, long long v0, long long v1, bf16x8* dst) {
+// dst[v] = sum over the W ranks' staging buffers, v in [v0, v1); every wave
+// runs the same iteration count (the loop steps by wave-uniform bases), so
+// the fused statistic's wave reductions see every lane
+template <int W, bool SS>
+DEV void sum_range(const CarArgs& a, long long v0, long long v1, bf16x8* dst) {
+  const int lane = threadIdx.x & 63;
+  for (long long b = v0 + (threadIdx.x & ~63); b < v1; b += CAR_THREADS) {
+    const long long v = b + lane;
+    const bool valid = v < v1;
+    float ssq = 0.f;
+    if (valid) {
+      bf16x8 x[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) x[p] = a.bufs[p][v];      // W loads in flight
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < W; ++p) acc8(s, x[p]);
+      const bf16x8 r = pack8(s);
+      dst[v] = r;
+      if (SS) ssq = sumsq_bf16x8(r);
+    }
+    if (SS) ss_wave_add(a, v, valid, ssq);
+  }
+}
+
+template <bool SS>
+DEV void sum_range_w(const CarArgs& a, long long v0, long long v1, bf16x8* dst) {
   switch (a.world) {
-    case 2: sum_range<2>(a, v0, v1, dst); break;
-    case 3: sum_range<3>(a, v0, v1, dst); break;
-    case 4: sum_range<4>(a, v0, v1, dst); break;
-    case 5: sum_range<5>(a, v0, v1, dst); break;
-    case 6: sum_range<6>(a, v0, v1, dst); break;
-    case 7: sum_range<7>(a, v0, v1, dst); break;
-    default: sum_range<8>(a, v0, v1, dst); break;
+    case 2: sum_range<2, SS>(a, v0, v1, dst); break;
+    case 3: sum_range<3, SS>(a, v0, v1, dst); break;
+    case 4: sum_range<4, SS>(a, v0, v1, dst); break;
+    case 5: sum_range<5, SS>(a, v0, v1, dst); break;
+    case 6: sum_range<6, SS>(a, v0, v1, dst); break;
+    case 7: sum_range<7, SS>(a, v0, v1, dst); break;
+    default: sum_range<8, SS>(a, v0, v1, dst); break;
+  }
+}
+
+DEV void sum_range_dyn(const CarArgs& a, long long v0, long long v1, bf16x8* dst, bool ss) {
+  if (ss) sum_range_w<true>(a, v0, v1, dst);
+  else sum_range_w<false>(a, v0, v1, dst);
+}
+
+// all-gather copy of src[t0, t1) -> out, with the fused statistic
+DEV void copy_range_ss(const CarArgs& a, const bf16x8* src, long long t0, long long t1) {
+  const int lane = threadIdx.x & 63;
+  for (long long b = t0 + (threadIdx.x & ~63); b < t1; b += CAR_THREADS) {
+    const long long v = b + lane;
+    const bool valid = v < t1;
+    float ssq = 0.f;
+    if (valid) {
+      const bf16x8 r = src[v];
+      a.out[v] = r;
+      ssq = sumsq_bf16x8(r);
+    }
+    ss_wave_add(a, v, valid, ssq);
   }
 }
 
@@ -163,7 +222,7 @@ __global__ __launch_bounds__(CAR_THREADS) void car_one_shot(CarArgs a) {
   bf16x8* mine = a.bufs[a.rank];
   for (long long v = v0 + threadIdx.x; v < v1; v += CAR_THREADS) mine[v] = a.inp[v];
   block_barrier(a, 0);
-  sum_range_dyn(a, v0, v1, a.out);
+  sum_range_dyn(a, v0, v1, a.out, a.ss != nullptr);
   car_end(a);
 }
 
@@ -177,14 +236,18 @@ __global__ __launch_bounds__(CAR_THREADS) void car_two_shot(CarArgs a) {
   // reduce-scatter: my slice of this block's range, summed into my own buffer
   const long long n = v1 - v0, per = (n + a.world - 1) / a.world;
   const long long s0 = v0 + min(n, per * a.rank), s1 = v0 + min(n, per * (a.rank + 1));
-  sum_range_dyn(a, s0, s1, mine);
+  sum_range_dyn(a, s0, s1, mine, false);
   block_barrier(a, 1);
   // all-gather: every rank's reduced slice
   for (int q = 0; q < a.world; ++q) {
     const int p = (a.rank + q) % a.world;            // stagger peers across ranks
     const long long t0 = v0 + min(n, per * p), t1 = v0 + min(n, per * (p + 1));
     const bf16x8* src = a.bufs[p];
-    for (long long v = t0 + threadIdx.x; v < t1; v += CAR_THREADS) a.out[v] = src[v];
+    if (a.ss) {
+      copy_range_ss(a, src, t0, t1);
+    } else {
+      for (long long v = t0 + threadIdx.x; v < t1; v += CAR_THREADS) a.out[v] = src[v];
+    }
   }
   car_end(a);
 }
@@ -261,11 +324,14 @@ int car_open(void* state, const void* all_handles) {
 
 // in-place allowed (inp == out).  mode: 1 one-shot, 2 two-shot.  Returns 0 on
 // success (the launch is asynchronous; check car_error for peer timeouts).
+// ss / row_len: the fused-norm statistic of rows of ``row_len`` elements
+// (row_len % 8 == 0, >= 512; nullptr: none); -4 if the rows do not qualify
 int car_allreduce(void* state, const void* inp, void* out, long long n_elems, int mode,
-                  int blocks, hipStream_t s) {
+                  int blocks, hipStream_t s, unsigned long long* ss, int row_len) {
   CarState* st = (CarState*)state;
   if (!st->opened) return -1;
   if (n_elems % 8 || (size_t)n_elems * 2 > st->buf_bytes) return -2;
+  if (ss && (row_len % 8 || row_len < 512 || n_elems % row_len)) return -4;
   CarArgs a;
   a.inp = (const bf16x8*)inp;
   a.out = (bf16x8*)out;
@@ -275,6 +341,8 @@ int car_allreduce(void* state, const void* inp, void* out, long long n_elems, in
   }
   a.err = st->err;
   a.ctr = st->ctr;
+  a.ss = ss;
+  a.vpr = ss ? row_len / 8 : 0;
   a.nvec = n_elems / 8;
   a.par_vecs = (long long)(st->buf_bytes / 16);
   a.rank = st->rank;

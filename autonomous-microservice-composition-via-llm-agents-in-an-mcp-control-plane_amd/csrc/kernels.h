@@ -194,7 +194,7 @@ size_t car_handle_bytes();
 void* car_create(int rank, int world, size_t buf_bytes, void* handles_out);
 int car_open(void* state, const void* all_handles);
 int car_allreduce(void* state, const void* inp, void* out, long long n_elems, int mode,
-                  int blocks, hipStream_t s);
+                  int blocks, hipStream_t s, unsigned long long* ss = nullptr, int row_len = 0);
 int car_error(void* state);
 void car_destroy(void* state);
 

@@ -164,6 +164,8 @@ CONFIGS = {
     "llama3-1b-ish": LlamaConfig("llama3-1b-ish", hidden=2048, layers=16, heads=16, kv_heads=4, ffn=8192),
     "tiny": LlamaConfig("tiny", hidden=256, layers=2, heads=2, kv_heads=1, ffn=512),
     "tiny-tp": LlamaConfig("tiny-tp", hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024),
+    # 8 KV heads: shards to TP = 8 like the 70B (one KV head per rank)
+    "tiny-tp8": LlamaConfig("tiny-tp8", hidden=2048, layers=2, heads=16, kv_heads=8, ffn=4096),
 }
 
 
@@ -315,7 +317,9 @@ class LlamaModel:
         if seq_parallel is None:
             seq_parallel = os.environ.get("MCP_SEQ_PARALLEL", "0") == "1"
         self.seq_parallel = bool(seq_parallel) and tp > 1
-        self.fused_norm = (tp == 1 and not self.seq_parallel
+        # at TP > 1 the statistic comes out of the all-reduce (K12 adds it as
+        # it writes the summed rows; RCCL / gloo: a row_sumsq pass after it)
+        self.fused_norm = (not self.seq_parallel
                            and os.environ.get("MCP_FUSED_NORM", "1") == "1")
         self._sp = sp_collectives          # (reduce_scatter, all_gather), injectable
         if self.seq_parallel and sp_collectives is None:
@@ -426,9 +430,26 @@ class LlamaModel:
                 h = ops.rmsnorm(x, self.w.layers[l + 1].attn_norm, cfg.eps)
         return ops.rmsnorm(x, self.w.final_norm, cfg.eps)
 
+    def _residual_gemm_ss(self, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor,
+                          ss_out: torch.Tensor) -> torch.Tensor:
+        """x + a w^T with the output rows' fused-norm statistic: in the GEMM
+        epilogue at TP = 1; at TP > 1 the row-parallel partials (rank 0 adds
+        the residual) are all-reduced and the collective adds the statistic
+        (``AllReduce(ss_out=)``; an injected all-reduce without it gets a
+        ``row_sumsq`` pass)."""
+        if self.tp == 1:
+            return ops.gemm(a, w, R=x, out=x, ss_out=ss_out)
+        y = ops.gemm(a, w, R=x if self.tp_rank == 0 else None)
+        if getattr(self._allreduce, "supports_ss", False):
+            self._allreduce(y, ss_out=ss_out)
+        else:
+            self._allreduce(y)
+            ops.row_sumsq(y, ss_out)
+        return y
+
     def _forward_fused_norm(self, step, kv, x) -> torch.Tensor:
-        """TP = 1 forward with every RMSNorm but the final one fused into the
-        GEMM epilogues (no normed copy of the residual stream is written):
+        """Forward with every RMSNorm but the final one fused into the
+        GEMM epilogues (TP > 1: into the all-reduce) (no normed copy of the residual stream is written):
         ``ss[l, 0]`` / ``ss[l, 1]`` are the fixed-point row sums of squares of
         layer l's attention / MLP input, produced by the previous residual
         GEMM (the embedding: ``row_sumsq``) and consumed by QKV + RoPE /
@@ -472,9 +493,9 @@ class LlamaModel:
                 x = x.index_select(0, ri)
                 a = a.view(T, self.hq * D).index_select(0, ri)
                 T = ri.numel()
-            x = ops.gemm(a.view(T, self.hq * D), lw.wo, R=x, out=x, ss_out=ss[l, 1])
+            x = self._residual_gemm_ss(a.view(T, self.hq * D), lw.wo, x, ss[l, 1])
             act = ops.gemm_silu(x, lw.w_gate_up, ss_in=ss[l, 1], eps=eps)
-            x = ops.gemm(act, lw.w_down, R=x, out=x, ss_out=ss[l + 1, 0])
+            x = self._residual_gemm_ss(act, lw.w_down, x, ss[l + 1, 0])
             if side is not None:
                 torch.cuda.current_stream(x.device).wait_stream(side)
         return ops.rmsnorm(x, self.w.final_norm, eps)

@@ -85,13 +85,20 @@ class NativeComm:
             self._comm = 0
 
 
+K12_MAX_BYTES = 64 << 20       # K12 staging buffer per epoch parity (2 per rank)
+
+
 class AllReduce:
     """In-place sum over the TP group for the row-parallel projections (C1, C2).
 
-    GPU: K12 (``parallel.custom_allreduce``, xGMI peer reads) for messages up
-    to ``MCP_CAR_MAX_BYTES`` (default 8 MiB: decode steps of up to 512 tokens
-    at H = 8192), the native RCCL communicator above that (``MCP_COMM=native``,
-    default) or torch.distributed's (``MCP_COMM=torch``).  ``MCP_CUSTOM_ALLREDUCE``
+    GPU: the path the xGMI cost model (``parallel/xgmi_model.py``) prices
+    lowest - K12 (``parallel.custom_allreduce``, peer reads on all links at
+    once; one-shot below the model's crossover, two-shot above) for every
+    message its staging buffer holds, ``MCP_CAR_MAX_BYTES`` (default 64 MiB:
+    prefill steps of up to 4096 tokens at H = 8192; the model prices K12
+    two-shot under RCCL at every size), the native RCCL communicator above
+    that (``MCP_COMM=native``, default) or torch.distributed's
+    (``MCP_COMM=torch``).  ``MCP_CUSTOM_ALLREDUCE``
     = auto (default: on for GPU groups of 2-8 ranks) | 1 | 0.
     CPU: gloo in fp32.
 
@@ -123,7 +130,20 @@ class AllReduce:
             from .custom_allreduce import CustomAllReduce
             self.custom = CustomAllReduce(group, self.device,
                                           max_bytes=int(os.environ.get("MCP_CAR_MAX_BYTES",
-                                                                       str(8 << 20))))
+                                                                       str(K12_MAX_BYTES))))
+            # the largest message the model still sends through K12 (RCCL
+            # above it; at the default constants: the whole staging buffer)
+            from .xgmi_model import best
+            m = self.custom.max_bytes
+            if best(m, world, m)[0] == "rccl":
+                lo, hi = 0, m
+                while hi - lo > 4096:
+                    mid = (lo + hi) // 2
+                    if best(mid, world, m)[0] == "rccl":
+                        hi = mid
+                    else:
+                        lo = mid
+                self.custom.max_bytes = lo
         if os.environ.get("MCP_COMM", "native") == "native":
             self.native = NativeComm(group, self.device)
         if self.custom is not None and os.environ.get("MCP_CAR_SELFCHECK", "1") == "1":
@@ -158,17 +178,29 @@ class AllReduce:
             self.custom = None
             self.custom_disabled = verdict["why"]
 
-    def __call__(self, t: torch.Tensor) -> None:
+    # accepts ``ss_out`` (the fused RMSNorm statistic of the summed rows)
+    supports_ss = True
+
+    def __call__(self, t: torch.Tensor, ss_out: Optional[torch.Tensor] = None) -> None:
+        """In-place sum; with ``ss_out`` (int64, zeroed) also the summed rows'
+        fixed-point sums of squares - inside K12 when it takes the message
+        (no extra pass), else one ``row_sumsq`` pass after the collective."""
         if self.device.type != "cuda":
             tf = t.float()
             dist.all_reduce(tf, group=self.group)
             t.copy_(tf.to(t.dtype))
         elif self.custom is not None and self.custom.eligible(t):
+            if ss_out is not None and self.custom.ss_eligible(t):
+                self.custom(t, ss_out=ss_out)
+                return
             self.custom(t)
         elif self.native is not None:
             self.native.all_reduce(t)
         else:
             dist.all_reduce(t, group=self.group)
+        if ss_out is not None:
+            from .. import ops
+            ops.row_sumsq(t.view(-1, t.shape[-1]), ss_out)
 
     def check(self) -> None:
         if self.custom is not None:

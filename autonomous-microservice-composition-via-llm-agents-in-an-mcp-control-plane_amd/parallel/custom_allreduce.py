@@ -23,7 +23,14 @@ import torch.distributed as dist
 
 from .. import ops
 
-ONE_SHOT_MAX = int(os.environ.get("MCP_CAR_ONE_SHOT_MAX", str(256 * 1024)))
+# one-shot / two-shot crossover: MCP_CAR_ONE_SHOT_MAX, else the xGMI cost
+# model's at this world size (parallel/xgmi_model.py: ~307 KB at 8 ranks)
+_ONE_SHOT_ENV = os.environ.get("MCP_CAR_ONE_SHOT_MAX")
+# workgroups per call (0: one per 4 x 512 16-B vectors, at most 128).  Every
+# rank's blocks spin on flags the peers' blocks raise, so all ranks' blocks
+# must be resident at once: on a node each rank has its own GPU, but ranks
+# sharing one device (the 8-process tests) must cap it (MCP_CAR_BLOCKS=16)
+MAX_BLOCKS = int(os.environ.get("MCP_CAR_BLOCKS", "0"))
 
 
 class CustomAllReduce:
@@ -33,6 +40,8 @@ class CustomAllReduce:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.max_bytes = max_bytes
+        from .xgmi_model import one_shot_max_bytes
+        self.one_shot_max = int(_ONE_SHOT_ENV) if _ONE_SHOT_ENV else one_shot_max_bytes(self.world)
         lib = ops.lib()
         self._lib = lib
         hb = lib.car_handle_bytes()
@@ -50,14 +59,22 @@ class CustomAllReduce:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()
                 and t.numel() % 8 == 0 and 0 < t.numel() * 2 <= self.max_bytes)
 
+    @staticmethod
+    def ss_eligible(t: torch.Tensor) -> bool:
+        """Rows the kernel can add the fused-norm statistic of (H >= 512, % 8)."""
+        h = t.shape[-1]
+        return h % 8 == 0 and h >= 512
+
     def __call__(self, t: torch.Tensor, out: torch.Tensor = None, mode: int = 0,
-                 blocks: int = 0) -> torch.Tensor:
+                 blocks: int = 0, ss_out: torch.Tensor = None) -> torch.Tensor:
         """Sum ``t`` over the group (in place unless ``out`` is given).
-        mode: 0 auto, 1 one-shot, 2 two-shot."""
+        mode: 0 auto, 1 one-shot, 2 two-shot.  ``ss_out`` (int64, zeroed):
+        also add every summed row's fixed-point sum of squares (the next
+        layer's fused RMSNorm statistic; ``ss_eligible`` rows)."""
         out = t if out is None else out
         if mode == 0:
-            mode = 1 if t.numel() * 2 <= ONE_SHOT_MAX else 2
-        self._lib.car_run(self._h, t, out, mode, blocks)
+            mode = 1 if t.numel() * 2 <= self.one_shot_max else 2
+        self._lib.car_run(self._h, t, out, mode, blocks or MAX_BLOCKS, ss_out)
         return out
 
     def check(self) -> None:

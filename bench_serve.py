@@ -91,7 +91,8 @@ def run_qps(planner, engine, qps, duration, seed, rank):
 
 def run_via_api(args):
     """Config 5 through the deployment path: ``python -m mcp_amd.api.server``
-    (uvicorn + FastAPI, ``create_app`` from the environment) in a child
+    (``--http fast``: the lean HTTP/1.1 front end, or uvicorn + FastAPI;
+    ``create_app`` from the environment; ``--api-workers``) in a child
     process with the local planner - ``--replicas N`` DP replica processes
     behind the router (``MCP_REPLICAS`` / ``MCP_ROUTER``), or with
     ``--replicas 0`` the in-process engine thread of a one-GPU server - and
@@ -116,7 +117,8 @@ def run_via_api(args):
         env["MCP_GRAPHS"] = "0"
     log_path = os.environ.get("MCP_SERVER_LOG", "/tmp/mcp_api_server.log")
     srv = subprocess.Popen([sys.executable, "-m", "mcp_amd.api.server", "--host", "127.0.0.1",
-                            "--port", str(port), "--no-access-log"],
+                            "--port", str(port), "--no-access-log", "--http", args.http,
+                            "--workers", str(args.api_workers)],
                            env=env, stdout=open(log_path, "w"), stderr=subprocess.STDOUT,
                            cwd=os.path.dirname(os.path.abspath(__file__)))
     base = f"http://127.0.0.1:{port}"
@@ -181,7 +183,9 @@ def run_via_api(args):
     for d in dags:
         validate_dag(d, names)
     out = {"metric": "plans/sec at fixed QPS through the API (config 5, deployment path)",
-           "path": f"uvicorn + FastAPI + {'router -> %d replica process(es)' % nrep if nrep else 'in-process engine thread'}",
+           "path": (f"{'fast HTTP/1.1 front end' if args.http == 'fast' else 'uvicorn + FastAPI'}"
+                    f" x {args.api_workers} API worker(s) + "
+                    f"{'router -> %d replica process(es)' % nrep if nrep else 'in-process engine thread'}"),
            "model": args.model, "services": args.services, "dtype": "bf16",
            "data": "synthetic intents, random-init weights", "replicas": nrep,
            "nodes_per_plan": [args.min_nodes, args.max_nodes], "offered_qps": args.qps * max(1, nrep),
@@ -209,6 +213,10 @@ def main():
                     help="qps: drive the HTTP API server (child process) instead of the engine")
     ap.add_argument("--replicas", type=int, default=1,
                     help="--via-api: DP replica processes behind the router (0: in-process engine)")
+    ap.add_argument("--http", choices=["fast", "uvicorn"], default="fast",
+                    help="--via-api: the server's front end")
+    ap.add_argument("--api-workers", type=int, default=1,
+                    help="--via-api: API worker processes (each routes to its slice of the replicas)")
     args = ap.parse_args()
     if args.via_api:
         return run_via_api(args)

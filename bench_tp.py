@@ -38,14 +38,8 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# xGMI / RCCL assumptions of the TP prediction (--simulate-rank), not
-# measurements: 7 links x ~153 GB/s per MI355X (one direction), RCCL
-# all-reduce bus bandwidth for large messages, and a per-call launch +
-# hand-off latency for RCCL; K12's latency floor IS measured (two processes
-# on this GPU), its xGMI read time is added from the link model
-XGMI_LINK_GBS = float(os.environ.get("MCP_SIM_XGMI_GBS", "153"))
-RCCL_BUSBW_GBS = float(os.environ.get("MCP_SIM_RCCL_BUSBW_GBS", "300"))
-RCCL_LAT_US = float(os.environ.get("MCP_SIM_RCCL_LAT_US", "25"))
+# xGMI / RCCL assumptions of the TP prediction (--simulate-rank): the cost
+# model of the run-time dispatch, parallel/xgmi_model.py (MCP_XGMI_* overrides)
 
 
 class _SimAllReduce:
@@ -103,10 +97,10 @@ def simulate_rank(args):
     with the all-reduces replaced by no-ops, so the timed batches give the
     rank's compute time.  Every all-reduce the steps would issue (2 per layer
     of [T, H] bf16, the last layer on the sampled rows) is then priced: K12
-    sizes (<= MCP_CAR_MAX_BYTES) at max(measured two-process K12 call on this
-    GPU, link-model xGMI read time), larger ones at the RCCL model
-    (assumptions above, reported in the JSON).  No overlap of communication
-    with compute is assumed."""
+    path and price come from the xGMI cost model the run-time dispatch uses
+    (parallel/xgmi_model.py: K12 one-/two-shot vs RCCL); a pessimistic
+    variant prices K12 calls at the two-process time on this one GPU where
+    that is higher.  No overlap of communication with compute is assumed."""
     import torch.multiprocessing as mp
     from mcp_amd.engine.engine import LLMEngine
     from mcp_amd.engine.kv_cache import KVCache
@@ -175,11 +169,16 @@ def simulate_rank(args):
     msgs = []
     for T, ns in steps:
         msgs += [T * H * 2] * (2 * (cfg.layers - 1)) + ([ns * H * 2] * 2 if ns else [])
-    car_max = int(os.environ.get("MCP_CAR_MAX_BYTES", str(8 << 20)))
-    # K12 sizes measured on a grid (64-token steps of [T, H] bf16, up to the K12 limit)
+    from mcp_amd.parallel import xgmi_model as xm
+    from mcp_amd.parallel.comm import K12_MAX_BYTES
+    car_max = int(os.environ.get("MCP_CAR_MAX_BYTES", str(K12_MAX_BYTES)))
+    # K12 sizes measured on a grid (64-token steps of [T, H] bf16, up to the K12
+    # limit): two processes on this ONE GPU - what that times is mostly the
+    # two contexts' time-slicing on one device, not links, so it only backs
+    # the pessimistic variant below
     grid = sorted({min(car_max, -(-m // (64 * H * 2)) * 64 * H * 2) for m in msgs if m <= car_max})
     k12 = {b: 0.0 for b in grid}              # CPU dry run: the link model alone
-    if grid and cuda:
+    if grid and cuda and not args.no_k12_timing:
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         port = free_port()
@@ -199,23 +198,21 @@ def simulate_rank(args):
         if any(isinstance(v, str) for v in got.values()):
             raise RuntimeError(f"K12 timing failed: {got}")
         k12 = {nbytes: max(got[0][nbytes], got[1][nbytes]) for nbytes in grid}
-    one_shot_max = int(os.environ.get("MCP_CAR_ONE_SHOT_MAX", str(256 * 1024)))
 
-    def price_us(m):
-        if m <= car_max:
-            b = min(car_max, -(-m // (64 * H * 2)) * 64 * H * 2)
-            # xGMI reads: one-shot pulls every peer's whole buffer (7 links in
-            # parallel), two-shot a 1/tp slice twice
-            read = m / (XGMI_LINK_GBS * 1e3) if m <= one_shot_max else 2 * m / tp / (XGMI_LINK_GBS * 1e3)
-            return max(k12[b], read + k12[b] * 0.5), "k12"
-        return RCCL_LAT_US + m * 2 * (tp - 1) / tp / (RCCL_BUSBW_GBS * 1e3), "rccl"
-    comm = {"k12": 0.0, "rccl": 0.0}
-    ncalls = {"k12": 0, "rccl": 0}
+    # the xGMI cost model (parallel/xgmi_model.py) picks and prices each call:
+    # the same rule the AllReduce dispatch follows at run time
+    comm = {"k12-1": 0.0, "k12-2": 0.0, "rccl": 0.0}
+    ncalls = {"k12-1": 0, "k12-2": 0, "rccl": 0}
+    pess_s = 0.0
     for m in msgs:
-        us, kind = price_us(m)
-        comm[kind] += us * 1e-6
-        ncalls[kind] += 1
-    comm_s = comm["k12"] + comm["rccl"]
+        path, us = xm.best(m, tp, car_max)
+        comm[path] += us * 1e-6
+        ncalls[path] += 1
+        if path.startswith("k12"):
+            b = min(car_max, -(-m // (64 * H * 2)) * 64 * H * 2)
+            us = max(us, k12.get(b, 0.0))
+        pess_s += us * 1e-6
+    comm_s = sum(comm.values())
     plans = len(seqs_all)
     pred_s = compute_s + comm_s
     print(json.dumps({
@@ -226,14 +223,20 @@ def simulate_rank(args):
         "rank_compute_s": round(compute_s, 3),
         "rank_compute_plans_per_s": round(plans / compute_s, 2),
         "allreduce_calls": ncalls, "allreduce_s": {k: round(v, 3) for k, v in comm.items()},
-        "k12_measured_us": {str(k): round(v, 1) for k, v in k12.items()},
         "predicted_step_s": round(pred_s / args.steps, 3),
         "predicted_plans_per_s": round(plans / pred_s, 2),
         "predicted_p50_latency_ms_upper": round(lats[len(lats) // 2] * pred_s / compute_s * 1e3, 1),
-        "measured": "rank-0 compute (GEMM shards, attention on its KV heads, norms, sampling, "
-                    "scheduler, hipGraphs) and K12 call time (two processes on one GPU)",
-        "modelled": {"xgmi_link_GBps": XGMI_LINK_GBS, "rccl_busbw_GBps": RCCL_BUSBW_GBS,
-                     "rccl_latency_us": RCCL_LAT_US, "overlap": "none"},
+        "pessimistic_plans_per_s": round(plans / (compute_s + pess_s), 2),
+        "pessimistic_allreduce_s": round(pess_s, 3),
+        "k12_one_gpu_two_process_us": {str(k): round(v, 1) for k, v in k12.items()},
+        "measured": "rank-0 compute (GEMM shards, attention on its KV heads, fused-norm "
+                    "statistics, sampling, scheduler, hipGraphs)",
+        "modelled": {"allreduce": "parallel/xgmi_model.py (K12 one-/two-shot vs RCCL per message)",
+                     "xgmi_link_GBps_per_direction": xm.LINK_GBS, "barrier_us": xm.BARRIER_US,
+                     "rccl_busbw_GBps": xm.RCCL_BUSBW_GBS, "rccl_latency_us": xm.RCCL_LAT_US,
+                     "k12_max_bytes": car_max,
+                     "overlap": "none: every all-reduce serialised after its GEMM (pessimistic "
+                                "variant: K12 calls at max(model, the one-GPU two-process time))"},
         "data": "synthetic intents, random-init weights",
     }), flush=True)
 
@@ -254,6 +257,8 @@ def main():
     ap.add_argument("--seq-parallel", action="store_true",
                     help="Megatron sequence parallelism (reduce-scatter / all-gather) for TP > 1")
     ap.add_argument("--gpus", type=int, default=1, help="TP degree = ranks (one per GPU); N > 1 self-launches")
+    ap.add_argument("--no-k12-timing", action="store_true",
+                    help="--simulate-rank: skip the two-process K12 timing on this GPU")
     ap.add_argument("--simulate-rank", type=int, default=0, metavar="TP",
                     help="predict config 4 at TP=N from one rank's shards on one GPU (simulate_rank)")
     args = ap.parse_args()
