@@ -193,6 +193,13 @@ class LLMEngine:
         self.alloc = self.kv.allocator
         self.max_batch = max_batch
         self.max_step_tokens = max_step_tokens
+        # chunked prefill (MCP_PREFILL_CHUNK tokens per step, 0 = off): while
+        # any request is past its first sample (decoding: one decision + its
+        # forced span per step), requests still in their prompt take at most
+        # this many prompt tokens per step between them, so a long
+        # (retrieval-sized) prompt no longer stretches every running
+        # request's decision step to a whole-prompt forward (config 3)
+        self.prefill_chunk = int(os.environ.get("MCP_PREFILL_CHUNK", "0"))
         self.temperature = temperature
         self.seed = seed
         self.running: List[Sequence] = []
@@ -683,6 +690,11 @@ class LLMEngine:
         casc_keys = (casc.length // BLOCK_SIZE) * BLOCK_SIZE if casc is not None else 0
         alloc, pool_free = self.alloc.alloc, self.alloc
         blocked = None
+        # chunked prefill: the prompt-token budget of this step, when decoding
+        # requests share it (None: no cap)
+        pf_left = None
+        if self.prefill_chunk > 0 and any(q.n_samples > 0 for q in order):
+            pf_left = self.prefill_chunk
         add_entry, add_batch, add_sample = entries.append, batch_seqs.append, sample_seqs.append
         # the per-request loop of every step (host critical path): locals bound,
         # _ensure_blocks / wants_sample inlined
@@ -698,6 +710,12 @@ class LLMEngine:
                 break
             if n < take:
                 take = n
+            if pf_left is not None and seq.n_samples == 0 and seq.decoder is not None:
+                if pf_left <= 0:
+                    continue                   # its prompt goes on next step
+                if take > pf_left:
+                    take = pf_left
+                pf_left -= take
             start = seq.num_cached
             blocks = seq.blocks
             need = (start + take + BLOCK_SIZE - 1) // BLOCK_SIZE - len(blocks)

@@ -114,7 +114,7 @@ def main():
             torch.cuda.synchronize()
 
     from mcp_amd.engine.engine import LLMEngine
-    from mcp_amd.models.llama import LlamaModel
+    from mcp_amd.models.llama import LlamaModel, get_config
     from mcp_amd.orchestrator import validate_dag
     from mcp_amd.planner.local import LocalPlanner
     from mcp_amd.planner.prompt import synthetic_intent
@@ -227,6 +227,13 @@ def main():
     p50 = statistics.median(all_lats) if all_lats else float("nan")
     ms_per_step = elapsed_max / args.steps * 1e3
     value = plans_total / elapsed_max
+    # workload-invariant throughput: the decoder layers' projection FLOPs per
+    # token (qkv, o, gate|up, down; no attention, embedding or LM head) at the
+    # measured token rate - moves with engine speed, not with the plan view
+    mc = get_config(args.model)
+    layer_params = mc.layers * (mc.hidden * (mc.heads + 2 * mc.kv_heads) * mc.head_dim
+                                + mc.heads * mc.head_dim * mc.hidden
+                                + 3 * mc.hidden * mc.ffn)
     if rank == 0:
         print(json.dumps({
             "metric": METRIC, "value": round(value, 3), "unit": "plans/s",
@@ -238,6 +245,7 @@ def main():
             "p99_latency_ms": round(statistics.quantiles(all_lats, n=100)[98] * 1e3, 2)
             if len(all_lats) >= 2 else None,
             "tokens_per_s": round(tokens_total / elapsed_max, 1),
+            "projection_pflops": round(2 * layer_params * tokens_total / elapsed_max / 1e15, 4),
             "batching": "continuous" if args.overlap > 0 else "closed",
             "device": args.device,
             "config": {"model": args.model, "global_batch": args.batch * world,

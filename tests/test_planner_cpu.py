@@ -630,3 +630,45 @@ def test_block_level_prefix_reuse_across_different_prefixes():
         eng.drop_prefixes()
         assert eng.alloc.num_free == eng.kv.num_blocks
     assert out[0] == out[1]
+
+
+def test_chunked_prefill_caps_prompt_tokens_beside_decoding_requests(monkeypatch):
+    """with MCP_PREFILL_CHUNK, requests still in their
+    prompt take at most that many prompt tokens per step while other requests
+    are decoding; the plans are the same greedy plans as unchunked."""
+    reg = MemoryRegistry(synthetic_registry(12, seed=5))
+    first = [synthetic_intent(i) for i in range(3)]
+    late = [synthetic_intent(100 + i) for i in range(3)]
+    out, steps, worst = [], [], []
+    for chunk in ("0", "24"):
+        monkeypatch.setenv("MCP_PREFILL_CHUNK", chunk)
+        torch.manual_seed(0)
+        model = LlamaModel.random("tiny", "cpu", seed=1)
+        eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, graphs=False)
+        assert eng.prefill_chunk == int(chunk)
+        planner = LocalPlanner(eng, reg, max_nodes=3)
+        seqs = planner.submit_many(first)
+        while not all(q.n_samples > 0 for q in seqs):
+            eng.step()
+        seen = []
+        real = eng._schedule_launch_inner
+
+        def rec(cohort, real=real, seen=seen):
+            before = {id(q): (q.n_samples, len(q.pending)) for q in eng.running}
+            L = real(cohort)
+            if L is not None:
+                decoding = any(q.n_samples > 0 for q in eng.running)
+                pre = sum(t for q, t in L.batch_seqs
+                          if q.decoder is not None and before.get(id(q), (1, 0))[0] == 0)
+                seen.append((decoding, pre))
+            return L
+        eng._schedule_launch_inner = rec
+        seqs += planner.submit_many(late)
+        eng.run()
+        assert all(q.done and q.error is None for q in seqs)
+        out.append([q.result for q in seqs])
+        steps.append(eng.stats["steps"])
+        worst.append(max((pre for dec, pre in seen if dec), default=0))
+    assert out[0] == out[1]
+    assert worst[0] > 24 >= worst[1], worst
+    assert steps[1] > steps[0]
