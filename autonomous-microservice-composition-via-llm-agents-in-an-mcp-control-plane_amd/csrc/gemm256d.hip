@@ -527,15 +527,19 @@ int gemm256d_group(int M, int N, int K) {
   return g > 0 ? g : 4;
 }
 
-// Wide direct epilogue (store_wide) instead of the LDS-staged one:
-// MCP_GEMM_WIDE_EPI=1 / gemm_wide_force (tools); needs the output < 2 GiB
-// (buffer descriptor)
+// Wide direct epilogue (store_wide) instead of the LDS-staged one.  Bitwise
+// the same outputs; over the headline's GEMM mix (cold weights, one process,
+// profiles/gemm_tuning.md round 5) gate|up + SwiGLU +1.6 %, o +0.1 %, down
+// -0.8 %: default (-1) = SwiGLU only; MCP_GEMM_WIDE_EPI / gemm_wide_force
+// 0 = never, 1 = every plain / residual / SwiGLU epilogue.  The output must
+// be < 2 GiB (buffer descriptor).
 static int g_wide_force = -1;
 void gemm_wide_force(int w) { g_wide_force = w; }
 bool gemm_wide_on(int M, int N, int epi) {
-  static const int env = getenv("MCP_GEMM_WIDE_EPI") ? atoi(getenv("MCP_GEMM_WIDE_EPI")) : 0;
+  static const int env = getenv("MCP_GEMM_WIDE_EPI") ? atoi(getenv("MCP_GEMM_WIDE_EPI")) : -1;
   const int on = g_wide_force >= 0 ? g_wide_force : env;
-  return on && epi >= 0 && epi <= 2 && (size_t)M * (epi == 2 ? N / 2 : N) * 2 < (1ull << 31);
+  if (epi < 0 || epi > 2 || (size_t)M * (epi == 2 ? N / 2 : N) * 2 >= (1ull << 31)) return false;
+  return on < 0 ? epi == 2 : on != 0;
 }
 
 template <int BMT>

@@ -126,3 +126,39 @@ def test_persistent_dispatch_rule(persist):
     assert L.gemm256d_persist(4096, 4096, 4096, 16 * 16) == 0
     L.gemm_persist_force(0)
     assert L.gemm256d_persist(4096, 28672, 4096, 16 * 112) == 0
+
+
+@pytest.mark.parametrize("persist_mode", [0, 2])
+@pytest.mark.parametrize("M,N,K", [(1000, 4096, 1024), (300, 2048, 4096)])
+def test_wide_direct_epilogue_equals_staged(M, N, K, persist_mode):
+    """The wide direct epilogue (permlane16 exchange + 16-B stores from the
+    accumulators, common.h store_wide) writes the same bytes as the LDS-staged
+    one at every tile height, one-tile and persistent: plain, residual in
+    place with the fused statistic, SwiGLU with the fused norm scale."""
+    L = ops.lib()
+    torch.manual_seed(43)
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    W = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    R = torch.randn(M, N, device=DEV).bfloat16()
+    ss_in = (X.float().pow(2).sum(-1) * 0.5 * ref.SS_FIX).round().to(torch.int64)
+    L.gemm_persist_force(persist_mode)
+    try:
+        for code in CODES:
+            L.gemm_plan_set(N, K, [code] * 128)
+            got = {}
+            for wide in (0, 1):
+                L.gemm_wide_force(wide)
+                y = R.clone()
+                ss = torch.zeros(M, dtype=torch.int64, device=DEV)
+                ops.gemm(X, W, R=y, out=y, ss_out=ss)
+                got[wide] = (ops.gemm(X, W), y, ss,
+                             ops.gemm_silu(X, W, ss_in=ss_in, eps=1e-5))
+            for a, b in zip(got[0], got[1]):
+                assert torch.equal(a, b), code
+            assert rel_err(got[1][0], ref.gemm(X, W)) < 1e-2, code
+            assert rel_err(got[1][3], ref.gemm_silu(X, W, ss_in=ss_in, eps=1e-5)) < 1e-2, code
+    finally:
+        L.gemm_wide_force(-1)
+        L.gemm_persist_force(-1)
+        L.gemm_plan_clear()
+        ops._load_gemm_plan(L)
