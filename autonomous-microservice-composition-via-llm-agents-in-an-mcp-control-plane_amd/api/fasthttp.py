@@ -77,6 +77,7 @@ class FastHTTP(asyncio.Protocol):
         self.queue: asyncio.Queue = None
         self.worker = None
         self.closing = False
+        self.continued = False                 # 100 Continue sent for the request being read
 
     # ------------------------------------------------------------ transport
     def connection_made(self, transport):
@@ -118,6 +119,7 @@ class FastHTTP(asyncio.Protocol):
         clen = 0
         chunked = False
         conn = b""
+        expect = False
         for ln in lines[1:]:
             k, sep, v = ln.partition(b":")
             if not sep:
@@ -136,6 +138,13 @@ class FastHTTP(asyncio.Protocol):
                 chunked = b"chunked" in v.lower()
             elif k == b"connection":
                 conn = v.lower()
+            elif k == b"expect":
+                expect = v.lower() == b"100-continue"
+        if expect and not self.continued:
+            # the client waits for this before it sends the body (curl does
+            # for bodies over 1 KiB)
+            self.continued = True
+            self.transport.write(b"HTTP/1.1 100 Continue\r\n\r\n")
         start = end + 4
         if chunked:
             body, used = self._dechunk(buf, start)
@@ -149,6 +158,7 @@ class FastHTTP(asyncio.Protocol):
                 return None
             body, used = bytes(buf[start:start + clen]), start + clen
         del buf[:used]
+        self.continued = False
         req.headers = headers
         req.body = body
         req.keep_alive = (conn != b"close") if req.version == b"HTTP/1.1" else (conn == b"keep-alive")

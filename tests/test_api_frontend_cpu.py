@@ -246,3 +246,23 @@ def test_uvicorn_workers_share_the_port():
             assert c.post("/plan", json={}).status_code == 422
     finally:
         _stop_server(p)
+
+
+def test_fast_front_end_expect_100_continue():
+    """A client that sends ``Expect: 100-continue`` (curl, bodies over 1 KiB)
+    gets the interim response before it sends the body."""
+    srv = _FastThread(_make_app())
+    try:
+        body = json.dumps({"intent": "x" * 2000}).encode()
+        s = socket.create_connection(("127.0.0.1", srv.port), timeout=10)
+        s.sendall(b"POST /plan HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+                  b"Expect: 100-continue\r\nContent-Length: " + str(len(body)).encode() + b"\r\n\r\n")
+        assert s.recv(100).startswith(b"HTTP/1.1 100 Continue")
+        s.sendall(body)
+        got = b""
+        while b"\r\n\r\n" not in got:
+            got += s.recv(65536)
+        assert got.startswith(b"HTTP/1.1 200")
+        s.close()
+    finally:
+        srv.close()
