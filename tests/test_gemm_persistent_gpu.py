@@ -153,8 +153,13 @@ def test_wide_direct_epilogue_equals_staged(M, N, K, persist_mode):
                 ops.gemm(X, W, R=y, out=y, ss_out=ss)
                 got[wide] = (ops.gemm(X, W), y, ss,
                              ops.gemm_silu(X, W, ss_in=ss_in, eps=1e-5))
-            for a, b in zip(got[0], got[1]):
+            # outputs bitwise; the fused statistic up to fp32 summation order
+            # (the wide epilogue sums a row's 128 columns in another order
+            # before its one fixed-point add per wave)
+            for a, b in zip(got[0][:2] + got[0][3:], got[1][:2] + got[1][3:]):
                 assert torch.equal(a, b), code
+            d = (got[0][2] - got[1][2]).abs().double() / got[0][2].double().clamp(min=1)
+            assert d.max().item() < 1e-6, code
             assert rel_err(got[1][0], ref.gemm(X, W)) < 1e-2, code
             assert rel_err(got[1][3], ref.gemm_silu(X, W, ss_in=ss_in, eps=1e-5)) < 1e-2, code
     finally:
