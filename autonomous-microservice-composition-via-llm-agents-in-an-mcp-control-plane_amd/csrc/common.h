@@ -181,6 +181,39 @@ DEV void store_direct(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y,
   }
 }
 
+// SwiGLU epilogue of a wave's MT x NT 16x16x32 accumulator tiles (W rows
+// interleaved [gate 16 | up 16] per 32-row group, so column tiles 2p / 2p + 1
+// hold gate / up of the same 4 features in the same lane); Y is [M, N / 2],
+// the fused RMSNorm row scale of the input applied first.  The rows' scale
+// loads are issued together before any store (norm_row_scales), not behind
+// a per-row guard (cdna_hip_programming.md §5 item 4(c)).
+template <int MT, int NT, class NE>
+DEV void store_silu(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y, int M, int N, int mb,
+                    int nb, int fr, int fq, const NE& ne) {
+  static_assert(NT % 2 == 0, "gate / up tile pairs");
+  const int F = N >> 1;
+  int rows[MT];
+  float rs[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) rows[mt] = min(mb + mt * 16 + fr, M - 1);
+  norm_row_scales(ne, rows, rs);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mb + mt * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int p = 0; p < NT / 2; ++p) {
+      const int f = (nb >> 1) + p * 16 + fq * 4;
+      if (f >= F) continue;
+      const f32x4 gv = acc[mt][2 * p] * rs[mt], uv = acc[mt][2 * p + 1] * rs[mt];
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
+      *reinterpret_cast<bf16x4*>(Y + (size_t)m * F + f) = o;
+    }
+  }
+}
+
 // Wide direct epilogue of a wave's 16x16x32 accumulator grid, 8 column tiles
 // (128 columns) per wave: lane (fr = lane & 15, fq = lane >> 4) holds rows
 // mb + 16 mt + fr, columns 16 nt + 4 fq .. +3.  Column-tile pairs (2p, 2p+1)

@@ -119,25 +119,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_128(const bf16* __restrict__ X
     store_direct<EPI>(acc, (bf16*)Y, R, M, N, m0 + wm * 64, n0 + wn * 64, fr, fq, ne);
     return;
   }
+  if constexpr (EPI == 2) {                          // row scales hoisted (common.h)
+    store_silu<4, 4>(acc, (bf16*)Y, M, N, m0 + wm * 64, n0 + wn * 64, fr, fq, ne);
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     const int m = m0 + wm * 64 + mt * 16 + fr;
     if (m >= M) continue;
-    if constexpr (EPI == 2) {
-      const int F = N >> 1;
-      const float rs = norm_row_scale(ne, m);        // fused RMSNorm of the input row
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int f = ((n0 + wn * 64) >> 1) + p * 16 + fq * 4;
-        if (f >= F) continue;
-        const f32x4 gv = acc[mt][2 * p] * rs, uv = acc[mt][2 * p + 1] * rs;
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
-        *reinterpret_cast<bf16x4*>((bf16*)Y + (size_t)m * F + f) = o;
-      }
-      continue;
-    }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int n = n0 + wn * 64 + nt * 16 + fq * 4;

@@ -57,32 +57,50 @@ DEV void tile_coords(int t, int nm, int nn, int& m0, int& n0) {
   n0 = ((t % per_group) / gsz) * BN;
 }
 
+// The epilogue inputs of one accumulator row mt, loaded before the slab sums
+// that precede its stores (clamped rows, no branch: loads issued behind a
+// per-row guard serialise, cdna_hip_programming.md §5 item 4(c)): the fused
+// RMSNorm scale (EPI 2) or the residual row piece (EPI 1)
+struct RowIn {
+  float rs;
+  bf16x4 rr[8];
+};
+template <int EPI>
+DEV void load_row_in(RowIn& in, const bf16* __restrict__ R, int M, int N, int m0, int n0, int wm,
+                     int wn, int fr, int fq, int mt, const NormEpi& ne) {
+  const int m = min(m0 + wm * 128 + mt * 16 + fr, M - 1);
+  if constexpr (EPI == 2) {
+    int rows[1] = {m};
+    float rs[1];
+    norm_row_scales(ne, rows, rs);
+    in.rs = rs[0];
+  }
+  if constexpr (EPI == 1) {                          // N % 256 == 0
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+      in.rr[nt] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n0 + wn * 128 + nt * 16 + fq * 4);
+  }
+}
+
 // the epilogue for one accumulator row mt from per-element values v(nt)
 template <int EPI, class V>
-DEV void store_row(bf16* __restrict__ Y, const bf16* __restrict__ R, int M, int N, int m0, int n0,
-                   int wm, int wn, int fr, int fq, int mt, const NormEpi& ne, V&& v) {
+DEV void store_row(bf16* __restrict__ Y, int M, int N, int m0, int n0, int wm, int wn, int fr,
+                   int fq, int mt, const NormEpi& ne, const RowIn& in, V&& v) {
   const int m = m0 + wm * 128 + mt * 16 + fr;
   if (m >= M) return;                                // the 4 fq lanes of the row together
   if constexpr (EPI == 2) {
     const int F2 = N >> 1;
-    const float rs = norm_row_scale(ne, m);          // fused RMSNorm of the input row
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int f = ((n0 + wn * 128) >> 1) + p * 16 + fq * 4;
       if (f >= F2) continue;
-      const f32x4 gv = v(2 * p) * rs, uv = v(2 * p + 1) * rs;
+      const f32x4 gv = v(2 * p) * in.rs, uv = v(2 * p + 1) * in.rs;
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
       *reinterpret_cast<bf16x4*>(Y + (size_t)m * F2 + f) = o;
     }
     return;
-  }
-  bf16x4 rr[8];
-  if (EPI == 1) {                                    // residual up front (N % 256 == 0)
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt)
-      rr[nt] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n0 + wn * 128 + nt * 16 + fq * 4);
   }
   float ss = 0.f;
 #pragma unroll
@@ -91,7 +109,7 @@ DEV void store_row(bf16* __restrict__ Y, const bf16* __restrict__ R, int M, int 
     f32x4 x = v(nt);
     if (EPI == 1) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] += (float)rr[nt][j];
+      for (int j = 0; j < 4; ++j) x[j] += (float)in.rr[nt][j];
     }
     bf16x4 o;
 #pragma unroll
@@ -273,6 +291,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256sk(const bf16* __restrict__
         //      then every later workgroup's first), two accumulator rows per batch
         const int w_first = owner_of(tile * U), w_last = owner_of(tile * U + U - 1);
         for (int rb = 0; rb < 4; ++rb) {
+          RowIn in[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            load_row_in<EPI>(in[h], R, M, N, m0, n0, wm, wn, fr, fq, 2 * rb + h, ne);
           f32x4 P[16];
 #pragma unroll
           for (int i = 0; i < 16; ++i) P[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -288,7 +310,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256sk(const bf16* __restrict__
           }
 #pragma unroll
           for (int h = 0; h < 2; ++h)
-            store_row<EPI>(Y, R, M, N, m0, n0, wm, wn, fr, fq, 2 * rb + h, ne,
+            store_row<EPI>(Y, M, N, m0, n0, wm, wn, fr, fq, 2 * rb + h, ne, in[h],
                            [&](int nt) { return P[h * 8 + nt]; });
         }
       }

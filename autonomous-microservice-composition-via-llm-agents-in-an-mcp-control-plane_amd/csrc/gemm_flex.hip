@@ -23,33 +23,7 @@ namespace {
 
 constexpr int FBK = 64;
 
-// SwiGLU epilogue (EPI 2): W rows interleaved [gate 16 | up 16] per 32-row
-// group, so a wave's column tiles 2p / 2p + 1 hold gate / up of the same 4
-// features in the same lane (as gemm.hip's 128^2 kernel); Y is [M, N / 2],
-// the fused RMSNorm row scale of the input applied first
-template <int MT, int NT>
-DEV void store_silu(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y, int M, int N, int mb,
-                    int nb, int fr, int fq, const NormEpi& ne) {
-  static_assert(NT % 2 == 0, "gate / up tile pairs");
-  const int F = N >> 1;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int m = mb + mt * 16 + fr;
-    if (m >= M) continue;
-    const float rs = norm_row_scale(ne, m);
-#pragma unroll
-    for (int p = 0; p < NT / 2; ++p) {
-      const int f = (nb >> 1) + p * 16 + fq * 4;
-      if (f >= F) continue;
-      const f32x4 gv = acc[mt][2 * p] * rs, uv = acc[mt][2 * p + 1] * rs;
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (bf16)(gv[j] / (1.f + __expf(-gv[j])) * uv[j]);
-      *reinterpret_cast<bf16x4*>(Y + (size_t)m * F + f) = o;
-    }
-  }
-}
-
+// SwiGLU epilogue (EPI 2): common.h store_silu (row scales hoisted)
 template <int EPI, int MT, int NT>
 DEV void flex_store(const f32x4 (&acc)[MT][NT], bf16* __restrict__ Y, const bf16* __restrict__ R,
                     int M, int N, int mb, int nb, int fr, int fq, const NormEpi& ne) {
