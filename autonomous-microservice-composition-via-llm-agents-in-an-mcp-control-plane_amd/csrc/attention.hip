@@ -133,8 +133,16 @@ DEV void split_fused_epilogue(const AttnArgs& a, f32x4 (&o)[8], float m_run, flo
   float lse = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
   const bool merge_pre = a.pre_o != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0;
   float wa = 0.f, wb = 1.f;
+  // the prefix partial's LSE and 8 row pieces, loaded together before any
+  // store (a load per dt behind a runtime test waits vmcnt(0) after each)
+  bf16x4 pa[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) pa[dt] = bf16x4{};
   if (z == 0 && merge_pre && qvalid) {
+    const bf16* pp = a.pre_o + row * D + 4 * fq;
     const float lse_a = a.pre_lse[row];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) pa[dt] = *reinterpret_cast<const bf16x4*>(pp + dt * 16);
     const float mx = fmaxf(lse_a, lse);
     const float ea = fexp2(lse_a - mx), eb = lse == -INFINITY ? 0.f : fexp2(lse - mx);
     wa = ea / (ea + eb);
@@ -144,17 +152,11 @@ DEV void split_fused_epilogue(const AttnArgs& a, f32x4 (&o)[8], float m_run, flo
   const auto rso = __builtin_amdgcn_make_buffer_rsrc(a.split_o, (short)0, 0x7FFFFFFF, 0x00020000);
   const auto rsl = __builtin_amdgcn_make_buffer_rsrc(a.split_lse, (short)0, 0x7FFFFFFF, 0x00020000);
   if (qvalid) {
-    const bf16* pp = (z == 0 && merge_pre) ? a.pre_o + row * D + 4 * fq : nullptr;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       f32x4 w;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = o[dt][r] * inv * wb;
-      if (pp) {
-        const bf16x4 pa = *reinterpret_cast<const bf16x4*>(pp + dt * 16);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) w[r] += (float)pa[r] * wa;
-      }
+      for (int r = 0; r < 4; ++r) w[r] = o[dt][r] * inv * wb + (float)pa[dt][r] * wa;
       o[dt] = w;                                      // this split's partial, kept for the merge
       __builtin_amdgcn_raw_buffer_store_b128(
           __builtin_bit_cast(u32x4, w), rso,
@@ -421,60 +423,70 @@ void attn_kernel(const AttnArgs a) {
   const size_t row = (size_t)(qs + tok) * Hq + head;
   float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if constexpr (KSPLIT) {
-    // normalised partial + its LSE; split 0 also carries the cascade prefix
+    // normalised partial + its LSE; split 0 also carries the cascade prefix.
+    // The prefix partial's LSE and its 8 row pieces are loaded together, in
+    // one branch, before any store: a load per dt behind the `pp` test made
+    // hipcc wait vmcnt(0) after each (8 dependent round trips per item)
     float lse = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
     float wa = 0.f, wb = 1.f;
-    const bf16* pp = nullptr;
-    if (blockIdx.z == 0 && a.pre_o != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
+    const bool merge = blockIdx.z == 0 && a.pre_o != nullptr && a.kv_begin != nullptr &&
+                       a.kv_begin[s] > 0;
+    bf16x4 pa[8];
+    if (merge) {
+      const bf16* pp = a.pre_o + row * D + 4 * fq;
       const float lse_a = a.pre_lse[row];
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) pa[dt] = *reinterpret_cast<const bf16x4*>(pp + dt * 16);
       const float mx = fmaxf(lse_a, lse);
       const float ea = fexp2(lse_a - mx), eb = lse == -INFINITY ? 0.f : fexp2(lse - mx);
       wa = ea / (ea + eb);
       wb = eb / (ea + eb);
       lse = mx + __log2f(ea + eb);
-      pp = a.pre_o + row * D + 4 * fq;
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) pa[dt] = bf16x4{};
     }
     float* po32 = a.split_o + ((size_t)blockIdx.z * a.rows + row) * D + 4 * fq;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       f32x4 w;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = o[dt][r] * inv * wb;
-      if (pp) {
-        const bf16x4 pa = *reinterpret_cast<const bf16x4*>(pp + dt * 16);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) w[r] += (float)pa[r] * wa;
-      }
+      for (int r = 0; r < 4; ++r) w[r] = o[dt][r] * inv * wb + (float)pa[dt][r] * wa;
       *reinterpret_cast<f32x4*>(po32 + dt * 16) = w;
     }
     if (fq == 0) a.split_lse[(size_t)blockIdx.z * a.rows + row] = lse;
     return;
   }
   float wa = 0.f, wb = 1.f;
-  const bf16* po = nullptr;
+  bool merge = false;
+  bf16x4 pa[8];
   if (MODE == 0 && a.own_lse != nullptr && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
     if (fq == 0) a.own_lse[row] = l_tot > 0.f ? m_run + __log2f(l_tot) : -INFINITY;
   } else if (MODE == 0 && a.kv_begin != nullptr && a.kv_begin[s] > 0) {
-    // merge with the shared-prefix partial: weights from the two log2-sum-exps
-    const float lse_b = m_run + __log2f(l_tot);
+    // merge with the shared-prefix partial: weights from the two log2-sum-exps.
+    // Its LSE and all 8 row pieces are loaded together before any store (a
+    // load per dt behind a runtime test waited vmcnt(0) after each one)
+    merge = true;
+    const bf16* po = a.pre_o + row * D + 4 * fq;
     const float lse_a = a.pre_lse[row];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) pa[dt] = *reinterpret_cast<const bf16x4*>(po + dt * 16);
+    const float lse_b = m_run + __log2f(l_tot);
     const float mx = fmaxf(lse_a, lse_b);
     wa = fexp2(lse_a - mx);
     wb = fexp2(lse_b - mx);
     const float den = 1.f / (wa + wb);
     wa *= den;
     wb *= den;
-    po = a.pre_o + row * D + 4 * fq;
   }
   if (MODE == 1 && fq == 0) a.lse_out[row] = m_run + __log2f(l_tot);
   bf16* op = a.out + row * D + 4 * fq;
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) {
     bf16x4 w;
-    if (po) {
-      const bf16x4 pa = *reinterpret_cast<const bf16x4*>(po + dt * 16);
+    if (merge) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv * wb + (float)pa[r] * wa);
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv * wb + (float)pa[dt][r] * wa);
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(o[dt][r] * inv);

@@ -227,6 +227,10 @@ def simulate_rank(args):
         "predicted_plans_per_s": round(plans / pred_s, 2),
         "predicted_p50_latency_ms_upper": round(lats[len(lats) // 2] * pred_s / compute_s * 1e3, 1),
         "pessimistic_plans_per_s": round(plans / (compute_s + pess_s), 2),
+        # NOT implemented - the bound a two-micro-batch schedule could reach
+        # (each half's all-reduces under the other half's GEMMs), charging the
+        # half-size GEMMs 5 % for their lower efficiency
+        "two_microbatch_overlap_bound_plans_per_s": round(plans / max(1.05 * compute_s, comm_s), 2),
         "pessimistic_allreduce_s": round(pess_s, 3),
         "k12_one_gpu_two_process_us": {str(k): round(v, 1) for k, v in k12.items()},
         "measured": "rank-0 compute (GEMM shards, attention on its KV heads, fused-norm "
