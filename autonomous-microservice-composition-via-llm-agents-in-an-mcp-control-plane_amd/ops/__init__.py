@@ -30,6 +30,8 @@ def lib():
     global _LIB
     if _LIB is None:
         cands = sorted(glob.glob(os.path.join(_HERE, "_kernels*.so")))
+        if os.environ.get("MCP_KERNELS_SO"):           # A/B of two builds (tools/gpu_run.sh ab)
+            cands = [os.environ["MCP_KERNELS_SO"]]
         if not cands:
             raise KernelLibraryMissing(
                 "HIP kernel library not built: run `python csrc/build.py` "
@@ -81,6 +83,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
 
 
 def library_path() -> Optional[str]:
+    if os.environ.get("MCP_KERNELS_SO"):
+        return os.environ["MCP_KERNELS_SO"]
     c = sorted(glob.glob(os.path.join(_HERE, "_kernels*.so")))
     return c[0] if c else None
 
