@@ -87,6 +87,26 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) acc[rb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the epilogue's row inputs, loaded before the weight stream (after it they
+  // are one more dependent round trip at the end of a ~20-50 us decode kernel):
+  // the fused-norm statistic (SwiGLU), the residual piece (EPI 1)
+  unsigned long long pre_ss[MB];
+  bf16x4 pre_rr[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    pre_ss[mb] = 0;
+    const int m = min(m0 + mb * 16 + r, M - 1);
+    if constexpr (EPI == 1)
+      pre_rr[mb] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + min(n0 + 4 * g, N - 4));
+  }
+  if (EPI == 2 && ne.ss_in) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) pre_ss[mb] = ne.ss_in[min(m0 + mb * 16 + r, M - 1)];
+  }
+  auto pre_rs = [&](int mb) -> float {
+    return ne.ss_in ? rsqrtf((float)pre_ss[mb] * (1.f / SS_FIX) * ne.inv_h + ne.eps) : 1.f;
+  };
+
   const int nsteps = K / SK_STEP;
   const int count = nsteps > wave ? (nsteps - wave + WV - 1) / WV : 0;
   bf16x8 wr[DEPTH][RB][4];
@@ -141,7 +161,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
 #pragma unroll
       for (int q = 0; q < 4; ++q) up[q] = __shfl_xor(tot[0][q], 32, 64);
       if (m >= M || g >= 2) continue;
-      const float rs = norm_row_scale(ne, m);
+      const float rs = pre_rs(mb);
       bf16x4 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -154,7 +174,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
     if (m >= M) continue;                            // all four g lanes of token r together
     if constexpr (EPI == 2) {
       const int F = N >> 1, f = (n0 >> 1) + 4 * g;   // f < F: N % 32 == 0 (skinny_ok)
-      const float rs = norm_row_scale(ne, m);
+      const float rs = pre_rs(mb);
       bf16x4 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -166,9 +186,8 @@ __global__ __launch_bounds__(64 * WV) void gemm_skinny(const bf16* __restrict__ 
       const int n = n0 + 4 * g;                      // n < N: N % 16 == 0 (skinny_ok)
       f32x4 v = tot[0];
       if (EPI == 1) {
-        const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] += (float)rr[q];
+        for (int q = 0; q < 4; ++q) v[q] += (float)pre_rr[mb][q];
       }
       bf16x4 o;
 #pragma unroll

@@ -98,6 +98,48 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
 #pragma unroll
     for (int mm = 0; mm < MF; ++mm) acc[f][mm] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // ---- the epilogue's per-row inputs, loaded before the weight stream: the
+  //      fused-norm statistic (EPI 2 / 3), the RoPE position and cache slot
+  //      (EPI 3), the residual piece (EPI 1).  Issued after the mainloop they
+  //      cost the kernel's critical path one to three dependent round trips
+  //      at its very end (decode steps: ~1 us each, 4 kernels per layer)
+  constexpr int UPW_ = (NQ / ((EPI >= 2) ? 2 : 1) + SW_WAVES - 1) / SW_WAVES;
+  constexpr int FPU_ = (EPI >= 2) ? 2 : 1;
+  unsigned long long pre_ss[UPW_];
+  int pre_pos[UPW_], pre_slot[UPW_];
+  bf16x4 pre_rr[UPW_][FPU_];
+#pragma unroll
+  for (int a = 0; a < UPW_; ++a) {
+    pre_ss[a] = 0;
+    pre_pos[a] = 0;
+    pre_slot[a] = -1;
+  }
+  {
+#pragma unroll
+    for (int a = 0; a < UPW_; ++a) {
+      const int u = min(wave + a * SW_WAVES, NQ / FPU_ - 1);
+      const int mm = u % MF;
+      const int m = min(16 * MF * mh + 16 * mm + r, M - 1);
+      if constexpr (EPI == 3) {
+        pre_pos[a] = ra.pos[m];
+        pre_slot[a] = ra.slots[m];
+      }
+      if constexpr (EPI == 1) {
+        const int f0 = u / MF;
+#pragma unroll
+        for (int j = 0; j < FPU_; ++j)
+          pre_rr[a][j] = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n0 + 16 * (f0 + j) + 4 * g);
+      }
+    }
+    if (EPI >= 2 && ne.ss_in) {
+#pragma unroll
+      for (int a = 0; a < UPW_; ++a) {
+        const int u = min(wave + a * SW_WAVES, NQ / FPU_ - 1);
+        pre_ss[a] = ne.ss_in[min(16 * MF * mh + 16 * (u % MF) + r, M - 1)];
+      }
+    }
+  }
+
   bf16x8 wr[DEPTH][NF][2], xr[DEPTH][MF][2];
   auto load = [&](int slot_i, int i) {
     const int k = (s0 + wave + i * SW_WAVES) * SW_STEP;
@@ -218,7 +260,22 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
   }
 
   // ---- epilogue: fragment (f, mm) lane holds rows n = 16 f + 4 g + i (i < 4)
-  //      of token m = 16 mm + r
+  //      of token m = 16 mm + r.  Its row inputs were loaded at kernel entry;
+  //      EPI 3's (cos, sin) pairs (they need the position) go out together here
+  static_assert(UPW_ == UPW && FPU_ == FPU, "prefetch geometry");
+  f32x4 pre_cs[EPI == 3 ? UPW : 1][2];
+  if constexpr (EPI == 3) {
+    if ((tile >> 1) < ra.Hq + ra.Hkv) {              // q / k heads rotate (v heads do not)
+#pragma unroll
+      for (int a = 0; a < UPW; ++a) {
+        const int u = min(wave + a * SW_WAVES, NU - 1);
+        const int d = 32 * (tile & 1) + 16 * ((2 * (u / MF)) >> 1) + 4 * g;
+        const f32x4* cs = reinterpret_cast<const f32x4*>(ra.cos_sin) + (size_t)pre_pos[a] * 32 + d / 2;
+        pre_cs[a][0] = cs[0];
+        pre_cs[a][1] = cs[1];
+      }
+    }
+  }
 #pragma unroll
   for (int a = 0; a < UPW; ++a) {
     const int u = wave + a * SW_WAVES;
@@ -227,7 +284,9 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
     const int mm = u % MF;
     const int m = 16 * MF * mh + 16 * mm + r;
     if (m >= M) continue;                            // the four g lanes of token r together
-    const float rs = EPI >= 2 ? norm_row_scale(ne, m) : 1.f;   // fused RMSNorm of the input row
+    // fused RMSNorm of the input row (1 when none), from the entry prefetch
+    const float rs = (EPI >= 2 && ne.ss_in)
+                         ? rsqrtf((float)pre_ss[a] * (1.f / SS_FIX) * ne.inv_h + ne.eps) : 1.f;
     if constexpr (EPI == 2) {
       // gate fragment f0, up fragment f0 + 1: output features n0/2 + 8 f0 + 4 g + i
       const f32x4 gv = sum[a][0] * rs, uv = sum[a][1] * rs;
@@ -248,8 +307,7 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
           o2[i] = (bf16)x2[i];
         }
       } else {
-        const f32x4* cs = reinterpret_cast<const f32x4*>(ra.cos_sin) + (size_t)ra.pos[m] * 32 + d / 2;
-        const f32x4 c01 = cs[0], c23 = cs[1];
+        const f32x4 c01 = pre_cs[EPI == 3 ? a : 0][0], c23 = pre_cs[EPI == 3 ? a : 0][1];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const f32x4 cc = i < 2 ? c01 : c23;
@@ -262,7 +320,7 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
       if (head < ra.Hq) {
         dst = reinterpret_cast<bf16*>(ra.q_out) + ((size_t)m * ra.Hq + head) * 128;
       } else {
-        const int slot = ra.slots[m];
+        const int slot = pre_slot[a];
         if (slot < 0) continue;
         const int hk = head - ra.Hq - (is_v ? ra.Hkv : 0);
         dst = reinterpret_cast<bf16*>(is_v ? ra.v_cache : ra.k_cache) +
@@ -276,9 +334,8 @@ __global__ __launch_bounds__(256 * MH, MH == 1 ? 2 : 1) void gemm_stream(const b
         const int n = n0 + 16 * (f0 + j) + 4 * g;
         f32x4 v = sum[a][j];
         if constexpr (EPI == 1) {
-          const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (size_t)m * N + n);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] += (float)rr[i];
+          for (int i = 0; i < 4; ++i) v[i] += (float)pre_rr[a][j][i];
         }
         bf16x4 o;
 #pragma unroll
