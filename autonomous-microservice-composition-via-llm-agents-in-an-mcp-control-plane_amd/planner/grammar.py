@@ -58,28 +58,28 @@ class Trie:
 
 
 def build_trie(token_seqs: Sequence[Sequence[int]]) -> Trie:
+    """Prefix-freeness is checked on insertion: an earlier alternative that is
+    a prefix of this one is a leaf on its path, one that this one prefixes
+    gives its end node children."""
     root = Trie()
     for i, seq in enumerate(token_seqs):
         if not seq:
             raise ValueError("empty alternative")
         node = root
-        node.mask |= 1 << i
+        bit = 1 << i
+        node.mask |= bit
         for t in seq:
-            node = node.children.setdefault(t, Trie())
-            node.mask |= 1 << i
+            if node.leaf >= 0:
+                raise ValueError("alternatives are not prefix-free")
+            nxt = node.children.get(t)
+            if nxt is None:
+                nxt = node.children[t] = Trie()
+            node = nxt
+            node.mask |= bit
         if node.leaf >= 0 or node.children:
             raise ValueError("alternatives are not prefix-free")
         node.leaf = i
-    for n in _walk(root):
-        if n.leaf >= 0 and n.children:
-            raise ValueError("alternatives are not prefix-free")
     return root
-
-
-def _walk(n: Trie):
-    yield n
-    for c in n.children.values():
-        yield from _walk(c)
 
 
 class GrammarSpec:
@@ -103,7 +103,6 @@ class GrammarSpec:
         self._chain_cache: Dict[tuple, tuple] = {}       # (trie node, live mask) -> forced walk
         self._kids_cache: Dict[tuple, List[int]] = {}    # (trie node, live mask) -> allowed tokens
         self.jnames = tuple(json.dumps(n) for n in self.names)
-        self.name_trie = self.trie(self.jnames)
         # input sources of key k: the payload key itself, then any earlier node.
         # ONE trie per key over every candidate; the live mask selects the key
         # plus the nodes chosen so far (a trie restricted by a mask is the trie
@@ -156,13 +155,20 @@ class GrammarSpec:
                 self._chain_cache[key] = r
         return r
 
+    @property
+    def name_trie(self) -> Trie:
+        return self.trie(self.jnames)
+
     def sources(self, key: str):
-        """(source names, their JSON alternatives, trie) for input ``key``."""
+        """(source names, their JSON alternatives, name -> position) for input
+        ``key``; the Python decoder's trie of the alternatives is
+        ``trie(alts)`` (built on first use: the native decoder never needs
+        it, and the tries were most of a retrieved request's host time)."""
         r = self._src_cache.get(key)
         if r is None:
             srcs = (key,) + tuple(n for n in self.names if n != key)
-            alts = tuple(json.dumps(x) for x in srcs)
-            r = (srcs, alts, self.trie(alts), {x: i for i, x in enumerate(srcs)})
+            alts = (json.dumps(key),) + tuple(j for n, j in zip(self.names, self.jnames) if n != key)
+            r = (srcs, alts, {x: i for i, x in enumerate(srcs)})
             self._src_cache[key] = r
         return r
 
@@ -221,7 +227,7 @@ class GrammarSpec:
             return (text, self.encode(text))
 
         def alts(a):
-            return (list(a), [list(self.tok.encode(x)) for x in a])
+            return (list(a), [self.tok.encode(x) for x in a])
 
         names = self.names
         name_idx = {}
@@ -233,7 +239,7 @@ class GrammarSpec:
             for k in ks:
                 if k not in key_ids:
                     key_ids[k] = len(keys)
-                    srcs, a_s, _, pos = self.sources(k)
+                    srcs, a_s, pos = self.sources(k)
                     keys.append({
                         "first": chunk(json.dumps(k) + ":"),
                         "rest": chunk("," + json.dumps(k) + ":"),
@@ -313,7 +319,7 @@ class DagDecoder:
             prev_names = [sp.names[j] for j in chosen]
             for ki, key in enumerate(sp.keys[idx]):
                 yield (("," if ki else "") + json.dumps(key) + ":", None)
-                srcs, alts_s, trie_s, pos = sp.sources(key)
+                srcs, alts_s, pos = sp.sources(key)
                 live_s = 1
                 for n in prev_names:
                     if n != key:
@@ -322,7 +328,7 @@ class DagDecoder:
                     yield (alts_s[0], None)
                     inputs[key] = srcs[0]
                 else:
-                    si = yield (None, (alts_s, trie_s, live_s))
+                    si = yield (None, (alts_s, sp.trie(alts_s), live_s))
                     inputs[key] = srcs[si]
             if sp.allow_retries:
                 yield ('},"retries":', None)

@@ -121,6 +121,7 @@ class SchemaIndex:
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self.stats = {"embedded": 0, "applied": 0, "full_builds": 0}
+        self._by_memo = None                            # see _by_name
 
     # ---------------------------------------------------------- bulk load
     def set_vectors(self, names: Sequence[str], vectors) -> None:
@@ -376,5 +377,18 @@ class SchemaIndex:
                 or self.n != len(services):
             self.refresh(services)
         names, _ = self.search_names([intent], k)
-        by = {s["name"]: s for s in services}
-        return [by[n] for n in names[0] if n in by]
+        return [s for s in map(self._by_name(services).get, names[0]) if s is not None]
+
+    def _by_name(self, services: Sequence[dict]) -> dict:
+        """name -> record of ``services``, memoised on the list's identity:
+        its length, its first and last records (held here, so their ids stay
+        theirs) and the registry version.  The registry hands out the same
+        record objects until it changes, so a 10k-service registry is indexed
+        once per version instead of once per request."""
+        key = (len(services), id(services[0]) if services else 0,
+               id(services[-1]) if services else 0, getattr(self.registry, "version", None))
+        memo = self._by_memo
+        if memo is None or memo[0] != key:
+            memo = self._by_memo = (key, {s["name"]: s for s in services},
+                                    (services[0], services[-1]) if services else ())
+        return memo[1]
