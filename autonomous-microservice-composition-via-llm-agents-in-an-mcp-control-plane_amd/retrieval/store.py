@@ -24,6 +24,7 @@ updates - an ``index_copy`` of the changed rows - so a registration into a
 """
 from __future__ import annotations
 
+import contextlib
 import re
 import threading
 import time
@@ -122,6 +123,14 @@ class SchemaIndex:
         self._stop = threading.Event()
         self.stats = {"embedded": 0, "applied": 0, "full_builds": 0}
         self._by_memo = None                            # see _by_name
+        # the index's own GPU stream (non-blocking w.r.t. the default stream
+        # the engine's forwards run on): every write and every query of the
+        # corpus is ordered on it, and a query's host read-back waits for the
+        # top-k kernels only, not behind the engine step queued ahead of it
+        self._stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+
+    def _on_stream(self):
+        return torch.cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
 
     # ---------------------------------------------------------- bulk load
     def set_vectors(self, names: Sequence[str], vectors) -> None:
@@ -129,6 +138,10 @@ class SchemaIndex:
         padded to a multiple of 4 here (zero rows, never returned: ``n_valid``)
         so no query ever copies the corpus (the unfused scoring GEMM writes
         16-B column groups)."""
+        with self._on_stream():
+            self._set_vectors(names, vectors)
+
+    def _set_vectors(self, names, vectors) -> None:
         v = torch.as_tensor(vectors).to(self.device, torch.bfloat16)
         n = v.shape[0]
         if n % 4:
@@ -240,6 +253,10 @@ class SchemaIndex:
     def _apply(self, u: _Update) -> None:
         """GPU side (the thread that owns the device): grow the padded
         corpus when needed and write the changed rows."""
+        with self._on_stream():
+            self._apply_rows(u)
+
+    def _apply_rows(self, u: _Update) -> None:
         cap = 0 if self.vectors is None else self.vectors.shape[0]
         need = -(-max(u.n, 1) // 4) * 4
         if need > cap:
@@ -361,10 +378,12 @@ class SchemaIndex:
 
     def search_names(self, intents: Sequence[str], k: int):
         n_pad = -(-self.n // 4) * 4
-        vals, idx = ops.topk_cosine(self.embed_queries(intents), self.vectors[:n_pad], k,
-                                    n_valid=self.n)
-        idx = idx.cpu().tolist()
-        return [[self.names[i] for i in row if 0 <= i < len(self.names)] for row in idx], vals.cpu()
+        with self._on_stream():
+            vals, idx = ops.topk_cosine(self.embed_queries(intents), self.vectors[:n_pad], k,
+                                        n_valid=self.n)
+            idx = idx.cpu().tolist()
+            vals = vals.cpu()
+        return [[self.names[i] for i in row if 0 <= i < len(self.names)] for row in idx], vals
 
     def search(self, intent: str, k: int, services: Sequence[dict]) -> List[dict]:
         if self._thread is not None and self.vectors is not None:
