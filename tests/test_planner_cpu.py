@@ -170,6 +170,49 @@ def test_retrieval_cpu_prunes_prompt():
     assert np.allclose(e[0], e[1]) and abs(np.linalg.norm(e[0]) - 1) < 1e-5
 
 
+def _shared_block_fraction(planner, intents, svcs):
+    """Replay of the prompts' 64-token block chains (the engine's block-level
+    prefix cache keys): the fraction of blocks an earlier prompt computed."""
+    from mcp_amd.planner.prompt import build_prompt_parts
+    seen, hit, tot = set(), 0, 0
+    for it in intents:
+        prefix, _ = build_prompt_parts(planner.candidates(it, svcs), it, compact=True)
+        t = planner.tok.prompt_ids(prefix)
+        h = ()
+        for b in range(len(t) // 64):
+            h = hash((h, tuple(t[b * 64:(b + 1) * 64])))
+            tot += 1
+            hit += h in seen
+            seen.add(h)
+    return hit / tot
+
+
+def test_retrieval_popularity_order_shares_more_prefix_blocks(monkeypatch):
+    """MCP_RETRIEVAL_ORDER=popular (default): the same retrieved sets, ordered
+    most-retrieved first, share more prompt-prefix blocks than name or score
+    order; the order is a permutation of the retrieved set and is stable
+    between rank snapshots."""
+    reg = MemoryRegistry(synthetic_registry(2000, seed=3))
+    svcs = reg.list_services()
+    idx = SchemaIndex(reg, dim=512, device="cpu")
+    idx.refresh()
+    intents = [synthetic_intent(i) for i in range(96)]
+    frac = {}
+    for order in ("popular", "name", "score"):
+        monkeypatch.setattr(LocalPlanner, "ORDER", order)
+        pl = LocalPlanner(None, reg, retriever=idx, retrieval_threshold=48, topk=32)
+        frac[order] = _shared_block_fraction(pl, intents, svcs)
+    assert frac["popular"] > frac["name"] > frac["score"], frac
+    monkeypatch.setattr(LocalPlanner, "ORDER", "popular")
+    pl = LocalPlanner(None, reg, retriever=idx, retrieval_threshold=48, topk=32)
+    for it in intents[:70]:                      # snapshots at 16 and 64 requests
+        pl.candidates(it, svcs)
+    a = pl.candidates(intents[3], svcs)
+    b = pl.candidates(intents[3], svcs)          # no snapshot in between: same order
+    assert [s["name"] for s in a] == [s["name"] for s in b]
+    assert sorted(s["name"] for s in a) == sorted(s["name"] for s in idx.search(intents[3], 32, svcs))
+
+
 def test_gate_up_interleave_roundtrip():
     from mcp_amd.ops import reference as ref
     g, u = torch.randn(64, 8), torch.randn(64, 8)
