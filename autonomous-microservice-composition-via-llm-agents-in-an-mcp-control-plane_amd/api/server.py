@@ -313,7 +313,15 @@ def serve(host: str, port: int, workers: int = 1, access_log: bool = True,
                                                        flush=True)))
             return 0
         import uvicorn
-        uvicorn.run(create_app(settle_gc=True), host=host, port=port, access_log=access_log)
+
+        class _Server(uvicorn.Server):
+            async def startup(self, sockets=None):
+                await super().startup(sockets=sockets)
+                if self.started:         # the same ready line as the other modes
+                    print(f"mcp api ready on {host}:{port} (uvicorn)", flush=True)
+
+        _Server(uvicorn.Config(create_app(settle_gc=True), host=host, port=port,
+                               access_log=access_log)).run()
         return 0
     import multiprocessing as mp
     import signal
