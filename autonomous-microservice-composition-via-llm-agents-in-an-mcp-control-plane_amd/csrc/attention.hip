@@ -505,14 +505,26 @@ void attn_kernel(const AttnArgs a) {
 // no mask (pre_keys is a multiple of 64).  Same row layout, online softmax,
 // swizzled double-buffered LDS-DMA ring and outputs (normalised O + LSE) as
 // MODE 1; the key-split form for few tokens stays on attn_kernel.
-template <int NW, int G, int RT>
+//
+// PP (ping-pong, 8 waves): waves 0-3 and 4-7 - one of each per SIMD - run the
+// tile loop half a phase apart.  Group A does QK^T, softmax, PV of tile kt
+// between two barriers; group B does softmax + PV of tile kt - 1, then QK^T of
+// tile kt.  So while one wave of a SIMD issues MFMAs the other issues the
+// softmax VALU, instead of both waiting on the same unit (in lock step, the
+// two waves' MFMA, VALU and LDS-read phases each took ~1/3 of a tile step and
+// did not overlap; profiles/attention_tuning.md).  B reads the V tile of the
+// previous step while the next tile is staged, so the ring has 3 buffers
+// (96 KiB); every wave passes the same barriers.
+template <int NW, int G, int RT, bool PP = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(RT >= 4 ? 1 : 2)))
 void attn_prefix_kernel(const AttnArgs a) {
+  static_assert(!PP || NW == 8, "ping-pong: two groups of 4 waves");
   constexpr int TPT = 16 / G;                 // tokens per 16-row tile
   constexpr int QT = NW * RT * TPT;           // tokens per block
   constexpr int PIECES = 2 * TILE * 2 / 1024; // 1 KiB pieces of the K and V tiles (32)
+  constexpr int NB = PP ? 3 : 2;              // K|V ring depth
   static_assert(PIECES % NW == 0, "pieces split evenly");
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];   // [buf][K|V][64][128]
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * 2 * TILE];   // [buf][K|V][64][128]
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kvh = a.head_major ? blockIdx.x : blockIdx.y;
@@ -541,18 +553,42 @@ void attn_prefix_kernel(const AttnArgs a) {
 
   const int srow = lane >> 4;
   BtLanes bt_at(a.pre_bt, 0, ntiles);
+  // Piece pr of a K or V tile is rows 4 pr + srow, the lane's 16-B chunk at
+  // chunk ^ (row & 15).  The 8-wave lock-step form DMAs from 64-bit addresses
+  // (global_load_lds); the 4-wave and ping-pong forms through per-tile buffer
+  // resources with 4 per-lane offsets (the chunk depends on pr & 3 only, the
+  // row step goes in soffset): one 64-bit address per piece kept
+  // 2 x PIECES / NW VGPRs live across the loop and the 4-wave form spilled,
+  // while the buffer form measured ~3 % slower on the 8-wave one (r5c7)
+  constexpr bool BUF_DMA = NW == 4 || PP;
+  unsigned voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) voff[i] = (unsigned)((srow * D + (((lane & 15) ^ (4 * i + srow)) << 3)) * 2);
   auto stage = [&](int kt, int buf) {
     const size_t blk = (size_t)bt_at(kt);
-    const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
-    const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
+    const size_t off = (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
+    if constexpr (BUF_DMA) {
+      const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)(a.kc + off), (short)0, TILE * 2, 0x00020000);
+      const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(a.vc + off), (short)0, TILE * 2, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < PIECES / NW; ++i) {
-      const int p = wave * (PIECES / NW) + i;
-      const int tile = p >> 4, pr = p & 15;
-      const int row = pr * 4 + srow;
-      const int chunk = (lane & 15) ^ (row & 15);
-      glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
+      for (int i = 0; i < PIECES / NW; ++i) {
+        const int p = wave * (PIECES / NW) + i;
+        const int tile = p >> 4, pr = p & 15;
+        auto* dst = (__attribute__((address_space(3))) void*)(base + tile * TILE + pr * 512);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(tile ? rv : rk, dst, 16, voff[pr & 3], pr * 4 * D * 2, 0, 0);
+      }
+    } else {
+      const bf16* kb = a.kc + off;
+      const bf16* vb = a.vc + off;
+#pragma unroll
+      for (int i = 0; i < PIECES / NW; ++i) {
+        const int p = wave * (PIECES / NW) + i;
+        const int tile = p >> 4, pr = p & 15;
+        const int row = pr * 4 + srow;
+        const int chunk = (lane & 15) ^ (row & 15);
+        glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
+      }
     }
   };
 
@@ -566,17 +602,10 @@ void attn_prefix_kernel(const AttnArgs a) {
     l_part[r] = 0.f;
   }
 
-  if (ntiles > 0) stage(0, 0);
-  __syncthreads();
   const int tq = (lane & 15) >> 2, tp = lane & 3;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
-    const bf16* Kl = smem + cur * 2 * TILE;
-    const bf16* Vl = Kl + TILE;
-
-    // ---- S^T = K Q^T: each K fragment feeds the RT row tiles
-    f32x4 sacc[RT][4];
+  const float c = a.scale_log2;
+  // ---- S^T = K Q^T: each K fragment feeds the RT row tiles
+  auto qk = [&](const bf16* Kl, f32x4 (&sacc)[RT][4]) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
 #pragma unroll
@@ -584,17 +613,17 @@ void attn_prefix_kernel(const AttnArgs a) {
       const int row = nt * 16 + fr;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const int c = ks * 4 + fq;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * D + ((c ^ (row & 15)) << 3));
+        const int cc = ks * 4 + fq;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * D + ((cc ^ (row & 15)) << 3));
 #pragma unroll
         for (int r = 0; r < RT; ++r) sacc[r][nt] = mfma16x16x32(kf, qf[r][ks], sacc[r][nt]);
       }
     }
-    // ---- online softmax per row tile (lane: query row fr, keys 16nt + 4fq + r).
-    //      The scores stay unscaled: the max commutes with the positive scale,
-    //      and exp2(s c - m) is one fma + exp per score
-    const float c = a.scale_log2;
-    bf16x8 pf[RT][2];
+  };
+  // ---- online softmax per row tile (lane: query row fr, keys 16nt + 4fq + r).
+  //      The scores stay unscaled: the max commutes with the positive scale,
+  //      and exp2(s c - m) is one fma + exp per score
+  auto softmax = [&](f32x4 (&sacc)[RT][4], bf16x8 (&pf)[RT][2]) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       float tmax = -INFINITY;
@@ -620,7 +649,9 @@ void attn_prefix_kernel(const AttnArgs a) {
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
     }
-    // ---- O^T += V^T P^T: each transposed V fragment feeds the RT row tiles
+  };
+  // ---- O^T += V^T P^T: each transposed V fragment feeds the RT row tiles
+  auto pv = [&](const bf16* Vl, bf16x8 (&pf)[RT][2]) {
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       const int col = dt * 16 + tp * 4;
@@ -636,7 +667,48 @@ void attn_prefix_kernel(const AttnArgs a) {
         for (int r = 0; r < RT; ++r) o[r][dt] = mfma16x16x32(vf, pf[r][k2], o[r][dt]);
       }
     }
-    __syncthreads();             // its fence also drains the next tile's LDS-DMA
+  };
+
+  f32x4 sacc[RT][4];
+  bf16x8 pf[RT][2];
+  if (ntiles > 0) stage(0, 0);
+  __syncthreads();
+  if constexpr (!PP) {
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < ntiles) stage(kt + 1, cur ^ 1);
+      const bf16* Kl = smem + cur * 2 * TILE;
+      qk(Kl, sacc);
+      softmax(sacc, pf);
+      pv(Kl + TILE, pf);
+      __syncthreads();             // its fence also drains the next tile's LDS-DMA
+    }
+  } else {
+    const bool lag = wave >= NW / 2;          // group B: half a phase behind
+    int cur = 0, prev = 2;                    // ring slots of tiles kt and kt - 1
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const int nxt = cur == 2 ? 0 : cur + 1;
+      if (kt + 1 < ntiles) stage(kt + 1, nxt);   // slot of tile kt - 2: read by nobody now
+      const bf16* Kl = smem + cur * 2 * TILE;
+      if (!lag) {
+        qk(Kl, sacc);
+        softmax(sacc, pf);
+        pv(Kl + TILE, pf);
+      } else {
+        if (kt > 0) {
+          softmax(sacc, pf);                  // tile kt - 1's scores, from the last step
+          pv(smem + prev * 2 * TILE + TILE, pf);
+        }
+        qk(Kl, sacc);
+      }
+      __syncthreads();             // tile kt + 1 landed; slot prev free for the next stage
+      prev = cur;
+      cur = nxt;
+    }
+    if (lag && ntiles > 0) {       // group B's last tile (nothing is staged any more)
+      softmax(sacc, pf);
+      pv(smem + prev * 2 * TILE + TILE, pf);
+    }
   }
 
   // ---- normalise and store: lane holds O[row fr][d = 16dt + 4fq + e]
@@ -861,6 +933,13 @@ int prefix_nw(int tokens, int tok_per_block8, int hkv) {
   return blocks8 < gemm256_num_cus() ? 4 : 8;
 }
 
+// MCP_ATTN_PREFIX_PP=1: the ping-pong form of the 8-wave prefix pass (read
+// per launch: the GPU tests compare the forms in one process)
+static bool prefix_pp() {
+  const char* e = getenv("MCP_ATTN_PREFIX_PP");
+  return e && e[0] == '1';
+}
+
 // Shared-prefix pass: 8 waves per block (32 tokens x G heads) -> half the K/V
 // tile staging per query of the 4-wave item and 4 waves per SIMD at 2 blocks/CU
 template <int G>
@@ -890,6 +969,8 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
       attn_prefix_kernel<4, G, 4><<<grid_for(4 * 4 * (16 / G)), 256, 0, s>>>(a);
     else if (prefix_nw(a.pre_tokens, 8 * 2 * (16 / G), a.Hkv) == 4)
       attn_prefix_kernel<4, G, 2><<<grid_for(4 * 2 * (16 / G)), 256, 0, s>>>(a);
+    else if (prefix_pp())
+      attn_prefix_kernel<8, G, 2, true><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     else
       attn_prefix_kernel<8, G, 2><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     return;

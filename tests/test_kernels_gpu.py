@@ -493,13 +493,14 @@ def test_decode_kernel_cascade_fold(own_keys, q_lens, monkeypatch):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (16, 8)])
-@pytest.mark.parametrize("T", [1, 77, 300])
+@pytest.mark.parametrize("T", [1, 77, 300, 2100])
 @pytest.mark.parametrize("rt", ["1", "2", "4"])
 def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
     """The shared-prefix pass alone (normalised O and its log2-sum-exp over
     the prefix keys) in every row-tile form (1 = MODE 1 of attn_kernel, 2 / 4
     = attn_prefix_kernel: each LDS fragment feeds 2 / 4 row tiles) against
-    fp32 softmax attention; T covers partial row tiles and blocks."""
+    fp32 softmax attention; T covers partial row tiles and blocks, and 2100
+    tokens over 8 kv heads the 8-wave grid (the 4-wave one below a block per CU)."""
     monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
     torch.manual_seed(11)
     D, P = 128, 640
@@ -520,6 +521,38 @@ def test_prefix_pass_row_tile_forms(Hq, Hkv, T, rt, monkeypatch):
     exp_lse = (torch.logsumexp(s, -1) / math.log(2)).reshape(T, Hq)
     assert rel_err(out, exp_o) < 2e-2
     assert torch.allclose(lse, exp_lse, atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("T,P", [(2100, 640), (4096, 704), (2500, 64)])
+def test_prefix_pass_ping_pong_form(T, P, monkeypatch):
+    """MCP_ATTN_PREFIX_PP=1: the 8-wave prefix pass with its two wave groups
+    half a phase apart (3-slot K|V ring) gives the same bits as the lock-step
+    form - every lane runs the same operations in the same order - and
+    matches fp32 softmax attention.  T >= 2048 tokens over 8 kv heads takes
+    the 8-wave grid; P = 64 is a one-tile prefix (group B only in its tail)."""
+    monkeypatch.setenv("MCP_ATTN_PREFIX_RT", "2")
+    torch.manual_seed(13)
+    Hq, Hkv, D = 32, 8, 128
+    n_pre = P // 64
+    kc, vc = _cache(n_pre + 2, Hkv)
+    pre_bt = torch.randperm(n_pre + 2, device=DEV)[:n_pre].to(torch.int32)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    outs = []
+    for pp in ("0", "1"):
+        monkeypatch.setenv("MCP_ATTN_PREFIX_PP", pp)
+        out = torch.empty_like(q)
+        lse = torch.empty(T, Hq, device=DEV, dtype=torch.float32)
+        ops.lib().prefix_attention(q, kc, vc, out, lse, pre_bt, P, T, scale)
+        torch.cuda.synchronize()
+        outs.append((out, lse))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    G = Hq // Hkv
+    k = kc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    v = vc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    s = torch.einsum("thgd,hpd->thgp", q.float().view(T, Hkv, G, D), k) * scale
+    exp_o = torch.einsum("thgp,hpd->thgd", torch.softmax(s, -1), v).reshape(T, Hq, D)
+    assert rel_err(outs[1][0], exp_o) < 2e-2
 
 
 @pytest.mark.parametrize("rt", ["1", "2"])
