@@ -39,6 +39,7 @@ _REASONS = {200: b"OK", 201: b"Created", 204: b"No Content", 307: b"Temporary Re
             500: b"Internal Server Error", 502: b"Bad Gateway", 503: b"Service Unavailable"}
 MAX_HEADER = 64 * 1024
 MAX_BODY = 64 * 1024 * 1024
+MAX_PIPELINED = 64                   # parsed requests queued per connection before reading pauses
 
 
 class _Date:
@@ -78,6 +79,7 @@ class FastHTTP(asyncio.Protocol):
         self.worker = None
         self.closing = False
         self.continued = False                 # 100 Continue sent for the request being read
+        self.paused = False                    # reading paused: MAX_PIPELINED requests queued
 
     # ------------------------------------------------------------ transport
     def connection_made(self, transport):
@@ -99,6 +101,11 @@ class FastHTTP(asyncio.Protocol):
             if req is None:
                 break
             self.queue.put_nowait(req)
+            if self.queue.qsize() >= MAX_PIPELINED and not self.paused:
+                # a client pipelining faster than it reads its answers: stop
+                # reading until the queue drains (flow control, bounded memory)
+                self.paused = True
+                self.transport.pause_reading()
 
     # -------------------------------------------------------------- parsing
     def _parse(self) -> Optional[_Request]:
@@ -129,11 +136,11 @@ class FastHTTP(asyncio.Protocol):
             v = v.strip()
             headers.append((k, v))
             if k == b"content-length":
-                try:
-                    clen = int(v)
-                except ValueError:
+                # digits only: int() would take "-5", "+5" or " 5_0"
+                if not v.isdigit():
                     self._fail(400)
                     return None
+                clen = int(v)
             elif k == b"transfer-encoding":
                 chunked = b"chunked" in v.lower()
             elif k == b"connection":
@@ -201,6 +208,9 @@ class FastHTTP(asyncio.Protocol):
             req = await self.queue.get()
             if req is None:
                 return
+            if self.paused and self.queue.qsize() < MAX_PIPELINED // 2 and not self.closing:
+                self.paused = False
+                self.transport.resume_reading()
             try:
                 status, headers, body = await self.srv.handle(req)
             except Exception:   # noqa: BLE001 - as Starlette's ServerErrorMiddleware

@@ -184,6 +184,16 @@ def test_fast_front_end_http_framing():
         assert st == 200 and h.get(b"connection") == b"close"
         (st, _, _), = _raw(srv.port, b"BROKEN\r\n\r\n")
         assert st == 400
+        # a negative / signed Content-Length is malformed, not a zero-length body
+        for bad in (b"-5", b"+5", b"5 5"):
+            (st, _, _), = _raw(srv.port, b"POST /plan HTTP/1.1\r\nHost: t\r\nContent-Length: " + bad +
+                              b"\r\n\r\n{}")
+            assert st == 400, bad
+        # 300 pipelined requests (past the per-connection queue bound: reading
+        # pauses and resumes) all answered, in order
+        pipe = b"".join(_post(b"/plan", json.dumps({"intent": f"p{i}"}).encode()) for i in range(300))
+        rs = _raw(srv.port, pipe, n_responses=300, timeout=30.0)
+        assert [r[0] for r in rs] == [200] * 300
     finally:
         srv.close()
 
