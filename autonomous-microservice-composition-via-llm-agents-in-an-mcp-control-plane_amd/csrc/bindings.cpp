@@ -199,6 +199,31 @@ void gemm_silu(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y,
   check_launch("gemm_silu");
 }
 
+// tuning / tests: one SwiGLU path by code (launch_gemm_silu_algo); returns
+// nonzero (nothing launched) where the path does not take the shape
+int64_t gemm_silu_algo(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64_t algo,
+                       const c10::optional<at::Tensor>& ss_in, double norm_eps) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
+  const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && N % 64 == 0, "gemm_silu_algo: W [N, K], N % 64 == 0");
+  TORCH_CHECK(Y.numel() == (int64_t)M * (N / 2), "gemm_silu_algo: Y [M, N/2]");
+  TORCH_CHECK(gemm_tn_check(M, N, K) == 0, "gemm_silu_algo: unsupported shape");
+  NormEpiScope scope(make_norm_epi(M, K, c10::nullopt, ss_in, norm_eps));
+  const int rc = launch_gemm_silu_algo(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, (int)algo,
+                                       stream());
+  if (rc == 0) check_launch("gemm_silu_algo");
+  return rc;
+}
+
+void gemm_plan_set_silu_py(int64_t N, int64_t K, const std::vector<int64_t>& codes) {
+  std::vector<int> c(codes.begin(), codes.end());
+  for (int v : c)
+    TORCH_CHECK(v == -1 || (v >= 1 && v <= 5) || (v >= 101 && v <= 116) || v == 200 ||
+                    (v >= 300 && v < 364) || (v >= 1000 && v < 1000 + 16 * 16),
+                "gemm plan silu: -1 or a launch_gemm_silu_algo code");
+  gemm_plan_set_silu((int)N, (int)K, c.data(), (int)c.size());
+}
+
 void gemm_variant(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64_t v) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
   const int K = X.size(-1), M = X.numel() / K, N = W.size(0);
@@ -700,6 +725,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
+  m.def("gemm_plan_set_silu", &gemm_plan_set_silu_py,
+        "measured SwiGLU path per 64-row M bucket for one gate|up (N, K) (-1: the rule)");
+  m.def("gemm_silu_algo", &gemm_silu_algo, "one SwiGLU GEMM path by code (tuning / tests)",
+        py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("algo"), py::arg("ss_in") = py::none(),
+        py::arg("norm_eps") = 0.0);
   m.def("gemm_plan_set_splits", &gemm_plan_set_splits_py,
         "measured split-K of the 128^2 path for one (N, K): a count per 64-row M bucket (0 = rule)");
   m.def("gemm_plan_split", &gemm_plan_split);

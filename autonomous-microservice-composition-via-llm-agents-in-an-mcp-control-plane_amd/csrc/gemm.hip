@@ -242,6 +242,7 @@ struct GemmPlan {
   std::vector<signed char> group;    // measured tile group of the AGPR kernel (0: default)
   std::vector<signed char> persist;  // 1: the persistent AGPR kernel (gemm256p.hip) measured faster
   std::vector<short> fsplit;         // measured flex tile x split-K (16 cand + S) or -1
+  std::vector<short> silu;           // gate|up: measured SwiGLU path (launch_gemm_silu_algo) or -1
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -353,6 +354,33 @@ int gemm_plan_fsplit(int M, int N, int K) {
     if (p.N == N && p.K == K) {
       const size_t b = (size_t)((M + 63) / 64) - 1;
       return b < p.fsplit.size() ? p.fsplit[b] : -1;
+    }
+  return -1;
+}
+
+void gemm_plan_set_silu(int N, int K, const int* codes, int n) {
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.silu.assign(codes, codes + n);
+      return;
+    }
+  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}, {}};
+  q.silu.assign(codes, codes + n);
+  g_plans.push_back(std::move(q));
+}
+
+// gate|up with the SwiGLU epilogue: the path measured fastest WITH that
+// epilogue for this M bucket (tools/tune_gemm_plan.py --silu), -1 = none (the
+// rule).  The code plan above is timed with the plain epilogue, and its AGPR
+// heights were never reached below M = 256 (gemm_select).  MCP_GEMM_SILU_PLAN=0
+// disables.
+int gemm_plan_silu(int M, int N, int K) {
+  static const int on = getenv("MCP_GEMM_SILU_PLAN") ? atoi(getenv("MCP_GEMM_SILU_PLAN")) : 1;
+  if (!on) return -1;
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.silu.size() ? p.silu[b] : -1;
     }
   return -1;
 }
@@ -710,9 +738,56 @@ void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, i
 // SwiGLU-fused projection: W rows interleaved [gate 16 | up 16]; Y is [M, N/2]
 void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N, int K,
                              hipStream_t s);
+
+// One SwiGLU path by code (the tuner's candidates and the "silu" plan):
+//   1..5          AGPR kernel at the height of plan code c (gemm256d_code_height)
+//   100 + S       128^2 kernel, S-way split-K through the reduce (S = 1: none)
+//   200           weight-streaming kernel (M <= 128)
+//   300 + f       flex tile candidate f (+32: 4-stage) with the SwiGLU epilogue
+//   1000 + 16 c + S  flex tile c with S-way split-K, the reduce applies SwiGLU
+// nonzero: not supported for this shape (nothing launched)
+int launch_gemm_silu_algo(const void* X, const void* W, void* Y, int M, int N, int K, int algo,
+                          hipStream_t s) {
+  if (N % 64) return 1;
+  if (algo >= 1000)
+    return launch_gemm_flex_split(X, W, Y, nullptr, M, N, K, (algo - 1000) / 16, (algo - 1000) % 16, 2, s);
+  if (algo >= 300) {
+    if (!gemm_flex_silu_ok(algo - 300)) return 2;
+    return launch_gemm_flex_epi(X, W, Y, nullptr, M, N, K, algo - 300, 2, s);
+  }
+  if (algo == 200) return launch_gemm_stream(X, W, Y, nullptr, M, N, K, 2, RopeArgs{}, s);
+  if (algo >= 100) {
+    const int S = algo - 100;
+    if (S > 1) {
+      const int nkt = K / BK;
+      if (!g_splitk_ws || nkt % S || nkt / S < 4 || (size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes)
+        return 3;
+      const int saved = g_split_force;
+      g_split_force = S;
+      const bool split = launch_gemm_128_split(X, W, Y, nullptr, M, N, K, 2, s);
+      g_split_force = saved;
+      if (!split) return 3;
+      return 0;
+    }
+    const int nm = (M + BM - 1) / BM, nn = (N + BN - 1) / BN;
+    gemm_tn_128<2><<<dim3(nm * nn), 256, 0, s>>>((const bf16*)X, (const bf16*)W, (bf16*)Y,
+                                                 nullptr, M, N, K, norm_epi());
+    return 0;
+  }
+  if (algo >= 1 && algo <= 5) {
+    if (gemm256d_ok(M, N, K)) return 4;
+    return launch_gemm_tn_256d_bm(X, W, Y, nullptr, M, N, K, 2, gemm256d_code_height(algo), s);
+  }
+  return 5;
+}
+
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s) {
   if (N % 64) return 1;
   if (skinny_first(M, N, K) && launch_gemm_skinny(X, W, Y, nullptr, M, N, K, 2, s) == 0) return 0;
+  // a measured SwiGLU path for the bucket (timed at its top row: below 33
+  // rows the stream / skinny rules, measured per M, keep the decode sizes)
+  const int sp = M > 32 ? gemm_plan_silu(M, N, K) : -1;
+  if (sp >= 0 && launch_gemm_silu_algo(X, W, Y, M, N, K, sp, s) == 0) return 0;
   if (gemm_stream_enabled() && gemm_stream_pick(M, N, K, 2) &&
       launch_gemm_stream(X, W, Y, nullptr, M, N, K, 2, RopeArgs{}, s) == 0)
     return 0;

@@ -126,6 +126,11 @@ int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R,
                            int K, int epi, int bm, hipStream_t s);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]
 int launch_gemm_silu(const void* X, const void* W, void* Y, int M, int N, int K, hipStream_t s);
+// one SwiGLU path by code (gemm.hip: AGPR height, 128^2 x split, stream, flex, flex x split)
+int launch_gemm_silu_algo(const void* X, const void* W, void* Y, int M, int N, int K, int algo,
+                          hipStream_t s);
+void gemm_plan_set_silu(int N, int K, const int* codes, int n);
+int gemm_plan_silu(int M, int N, int K);
 int launch_gemm_tn_256_variant(const void* X, const void* W, void* Y, int M, int N, int K, int v,
                                hipStream_t s);
 void launch_gemm_tn_algo(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,

@@ -79,6 +79,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
             mod.gemm_plan_set_group(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["group"]])
         if "persist" in sh and hasattr(mod, "gemm_plan_set_persist"):
             mod.gemm_plan_set_persist(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["persist"]])
+        if "silu" in sh and hasattr(mod, "gemm_plan_set_silu"):
+            mod.gemm_plan_set_silu(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["silu"]])
     return len(plan["shapes"])
 
 

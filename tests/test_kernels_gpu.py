@@ -596,6 +596,36 @@ def test_gemm_silu_fused(M, F, K):
     assert rel_err(y, exp) < 2e-2
 
 
+@pytest.mark.parametrize("M", [100, 200, 330])
+def test_gemm_silu_every_path(M):
+    """Every SwiGLU path the "silu" plan can name (launch_gemm_silu_algo: AGPR
+    heights, 128^2 x split-K, stream, flex tiles, flex x split-K) against fp32,
+    with the fused-norm statistic applied (rows scaled by rsqrt(mean x^2 + eps))."""
+    torch.manual_seed(5)
+    L = ops.lib()
+    F, K = 1792, 4096
+    X = torch.randn(M, K, device=DEV).bfloat16()
+    g = (torch.randn(F, K, device=DEV) / math.sqrt(K)).bfloat16()
+    u = (torch.randn(F, K, device=DEV) / math.sqrt(K)).bfloat16()
+    W = ref.interleave_gate_up(g, u).contiguous()
+    eps = 1e-5
+    ss = (X.float().pow(2).sum(-1) * (1 << 20)).round().to(torch.int64)
+    rs = torch.rsqrt(ss.double() / (1 << 20) / K + eps).float()[:, None]
+    exp = torch.nn.functional.silu((X.float() @ g.float().t()) * rs) * ((X.float() @ u.float().t()) * rs)
+    algos = [1, 2, 3, 4, 5, 101, 102, 104, 200]
+    algos += [300 + f for f in range(L.gemm_flex_count()) if L.gemm_flex_silu_ok(f)]
+    algos += [1000 + 16 * c + S for c in (0, 6, 10) for S in (2, 4)]
+    ran = 0
+    for a in algos:
+        Y = torch.full((M, F), float("nan"), device=DEV, dtype=torch.bfloat16)
+        if L.gemm_silu_algo(X, W, Y, a, ss, eps):
+            continue                                   # path does not take this shape
+        torch.cuda.synchronize()
+        assert rel_err(Y, exp) < 2e-2, a
+        ran += 1
+    assert ran >= 10
+
+
 @pytest.mark.parametrize("M,N,K", [(3584, 6144, 4096), (3584, 4096, 14336), (1000, 1024, 4096),
                                    (700, 520, 320)])
 def test_gemm_stream_k(M, N, K):

@@ -122,6 +122,97 @@ def time_ms(fn, Ws, reps=10):
     return s_ev.elapsed_time(e_ev) / reps
 
 
+def tune_silu():
+    """MCP_TUNE_SILU=1: time every gate|up path WITH the SwiGLU epilogue and the
+    fused-norm statistic (as the TP=1 model runs it, launch_gemm_silu_algo
+    codes) against the production dispatch under the shipped plan, per 64-row
+    bucket up to m_max, cold weights; record the winner as the shape's "silu"
+    entry when it beats production by > 1 % (-1 otherwise), and write the
+    shipped plan with that key to out_path.  The code plan above is timed with
+    the plain epilogue, and below M = 256 its AGPR heights are never reached."""
+    with open(ops.GEMM_PLAN_FILE) as f:
+        plan = json.load(f)
+    ops._load_gemm_plan(L, ops.GEMM_PLAN_FILE)
+    eps = 1e-5
+    t0 = time.time()
+    for sh in plan["shapes"]:
+        N, K = int(sh["N"]), int(sh["K"])
+        if N not in SWIGLU_N or (N, K) not in SHAPES:
+            continue
+        nb = m_max // MSTEP
+        L.gemm_plan_set_silu(N, K, [-1] * nb)           # production = the rule
+        Xf = torch.randn(m_max, K, device=dev).bfloat16()
+        Wc = [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+              for _ in range(max(2, int(1.5e9 // (N * K * 2))))]
+        Yf = torch.empty(m_max, N // 2, device=dev, dtype=torch.bfloat16)
+        ssf = (Xf.float().pow(2).sum(-1) * (1 << 20)).to(torch.int64)   # fixed-point row sums (SS_FIX)
+        silu, ref = [], []
+        for b in range(nb):
+            M = (b + 1) * MSTEP
+            X, Y, ss = Xf[:M], Yf[:M], ssf[:M]
+            cands = [("prod", -1)]
+            if M >= 128:
+                cands += [("a", c) for c in (1, 2, 3, 4, 5)]
+            cands += [("a", 100 + S) for S in (1, 2, 4, 8)]
+            if M <= 128:
+                cands.append(("a", 200))
+            if 64 <= M <= FLEX_MAX:
+                fc = [f for f in range(NFLEX) if L.gemm_flex_silu_ok(f)]
+                cands += [("a", 300 + f) for f in fc + [32 + f for f in fc]]
+            if FS_MIN <= M <= FS_MAX:
+                for c, (tm, tn) in enumerate(FS_TILES):
+                    tiles = -(-M // tm) * -(-N // tn)
+                    for S in (2, 3, 4, 7, 8):
+                        if (K // 64) % S == 0 and 128 <= tiles * S <= 1024:
+                            cands.append(("a", 1000 + 16 * c + S))
+            cands.append(("lib", -1))
+
+            def fn(c, w):
+                if c[0] == "prod":
+                    L.gemm_silu(X, w, Y, ss, eps)
+                elif c[0] == "lib":
+                    torch.matmul(X, w.t())
+                elif L.gemm_silu_algo(X, w, Y, c[1], ss, eps):
+                    raise ValueError("unsupported")
+            ok = []
+            for c in cands:
+                try:
+                    fn(c, Wc[0])
+                    ok.append(c)
+                except (ValueError, RuntimeError):
+                    pass
+            torch.cuda.synchronize()
+            best = {c: float("inf") for c in ok}
+            for _ in range(3):
+                for c in ok:
+                    best[c] = min(best[c], time_ms(lambda w, c=c: fn(c, w), Wc))
+            lib_ms = best.pop(("lib", -1))
+            prod = best.pop(("prod", -1))
+            win = min(best, key=best.get) if best else None
+            take = win is not None and best[win] * 1.01 < prod
+            silu.append(win[1] if take else -1)
+            ours = min(prod, best[win]) if take else prod
+            ref.append([round(prod * 1e3, 1), round(ours * 1e3, 1), round(lib_ms * 1e3, 1)])
+            print(json.dumps({"N": N, "K": K, "M": M, "prod_us": round(prod * 1e3, 1),
+                              "best": win[1] if win else None,
+                              "best_us": round(best[win] * 1e3, 1) if win else None,
+                              "taken": bool(take), "hipblaslt_us": round(lib_ms * 1e3, 1),
+                              "s": round(time.time() - t0, 1)}), flush=True)
+        sh["silu"] = silu
+        sh["silu_us"] = ref
+        del Xf, Wc, Yf
+    plan["silu"] = ("gate|up SwiGLU path per bucket (launch_gemm_silu_algo code; -1 = the rule); "
+                    "silu_us: [production before, chosen, hipBLASLt plain GEMM] us")
+    with open(out_path, "w") as f:
+        json.dump(plan, f, indent=None, separators=(",", ":"))
+        f.write("\n")
+    print(json.dumps({"written": out_path, "s": round(time.time() - t0, 1)}), flush=True)
+
+
+if os.environ.get("MCP_TUNE_SILU") == "1":
+    tune_silu()
+    sys.exit(0)
+
 result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
           "mstep": MSTEP,
           "codes": "0=128x128, 1..5=AGPR 256/192/160/224/128-row tiles",
