@@ -117,10 +117,10 @@ void rope_kv(const at::Tensor& qkv, const at::Tensor& pos, const at::Tensor& slo
 
 // QKV projection + RoPE + paged K/V write: fused in the GEMM epilogue when the
 // AGPR kernel serves the shape, else GEMM into ``qkv`` (scratch) + rope_kv
-void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const at::Tensor& pos,
-              const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& q_out,
-              at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D,
-              const c10::optional<at::Tensor>& ss_in, double norm_eps) {
+int64_t qkv_rope_impl(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const at::Tensor& pos,
+                      const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& q_out,
+                      at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D,
+                      const c10::optional<at::Tensor>& ss_in, double norm_eps, int64_t algo) {
   CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(qkv);
   CHECK_I32_TENSOR(pos); CHECK_I32_TENSOR(slots);
   CHECK_BF16_TENSOR(q_out); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache);
@@ -141,8 +141,42 @@ void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const a
               q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), (int)Hq, (int)Hkv,
               (int)k_cache.size(2)};
   NormEpiScope scope(make_norm_epi(M, K, c10::nullopt, ss_in, norm_eps));
+  if (algo >= 0) {             // tuning / tests: one path by code, nonzero = not taken
+    const int rc = launch_qkv_rope_algo(X.data_ptr(), W.data_ptr(), qkv.data_ptr(), M, N, K, (int)D,
+                                        ra, (int)algo, stream());
+    if (rc == 0) check_launch("qkv_rope_algo");
+    return rc;
+  }
   launch_qkv_rope(X.data_ptr(), W.data_ptr(), qkv.data_ptr(), M, N, K, (int)D, ra, stream());
   check_launch("qkv_rope");
+  return 0;
+}
+
+void qkv_rope(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv, const at::Tensor& pos,
+              const at::Tensor& slots, const at::Tensor& cos_sin, at::Tensor& q_out,
+              at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t D,
+              const c10::optional<at::Tensor>& ss_in, double norm_eps) {
+  qkv_rope_impl(X, W, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, ss_in,
+                norm_eps, -1);
+}
+
+int64_t qkv_rope_algo(const at::Tensor& X, const at::Tensor& W, at::Tensor& qkv,
+                      const at::Tensor& pos, const at::Tensor& slots, const at::Tensor& cos_sin,
+                      at::Tensor& q_out, at::Tensor& k_cache, at::Tensor& v_cache, int64_t Hq,
+                      int64_t Hkv, int64_t D, int64_t algo, const c10::optional<at::Tensor>& ss_in,
+                      double norm_eps) {
+  TORCH_CHECK(algo >= 0, "qkv_rope_algo: algo >= 0");
+  return qkv_rope_impl(X, W, qkv, pos, slots, cos_sin, q_out, k_cache, v_cache, Hq, Hkv, D, ss_in,
+                       norm_eps, algo);
+}
+
+void gemm_plan_set_rope_py(int64_t N, int64_t K, const std::vector<int64_t>& codes) {
+  std::vector<int> c(codes.begin(), codes.end());
+  for (int v : c)
+    TORCH_CHECK(v == -1 || (v >= 1 && v <= 5) || v == 200 || v == 500 ||
+                    (v >= 1000 && v < 1000 + 16 * 16),
+                "gemm plan rope: -1 or a launch_qkv_rope_algo code");
+  gemm_plan_set_rope((int)N, (int)K, c.data(), (int)c.size());
 }
 
 void row_sumsq(const at::Tensor& x, at::Tensor& ss) {
@@ -725,6 +759,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm_plan_set", &gemm_plan_set_py, "measured tile plan for one (N, K): a code per 64-row M bucket");
+  m.def("qkv_rope_algo", &qkv_rope_algo, "one QKV + RoPE path by code (tuning / tests)",
+        py::arg("X"), py::arg("W"), py::arg("qkv"), py::arg("pos"), py::arg("slots"),
+        py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("algo"),
+        py::arg("ss_in") = py::none(), py::arg("norm_eps") = 0.0);
+  m.def("gemm_plan_set_rope", &gemm_plan_set_rope_py,
+        "measured QKV + RoPE path per 64-row M bucket for one qkv (N, K) (-1: the rule)");
   m.def("gemm_plan_set_silu", &gemm_plan_set_silu_py,
         "measured SwiGLU path per 64-row M bucket for one gate|up (N, K) (-1: the rule)");
   m.def("gemm_silu_algo", &gemm_silu_algo, "one SwiGLU GEMM path by code (tuning / tests)",

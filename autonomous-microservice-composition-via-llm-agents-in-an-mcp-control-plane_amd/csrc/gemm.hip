@@ -243,6 +243,7 @@ struct GemmPlan {
   std::vector<signed char> persist;  // 1: the persistent AGPR kernel (gemm256p.hip) measured faster
   std::vector<short> fsplit;         // measured flex tile x split-K (16 cand + S) or -1
   std::vector<short> silu;           // gate|up: measured SwiGLU path (launch_gemm_silu_algo) or -1
+  std::vector<short> rope;           // qkv: measured QKV + RoPE path (launch_qkv_rope_algo) or -1
 };
 std::vector<GemmPlan> g_plans;
 }  // namespace
@@ -340,7 +341,7 @@ void gemm_plan_set_fsplit(int N, int K, const int* fs, int n) {
       p.fsplit.assign(fs, fs + n);
       return;
     }
-  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}};
+  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}, {}, {}};
   q.fsplit.assign(fs, fs + n);
   g_plans.push_back(std::move(q));
 }
@@ -364,7 +365,7 @@ void gemm_plan_set_silu(int N, int K, const int* codes, int n) {
       p.silu.assign(codes, codes + n);
       return;
     }
-  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}, {}};
+  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}, {}, {}};
   q.silu.assign(codes, codes + n);
   g_plans.push_back(std::move(q));
 }
@@ -381,6 +382,31 @@ int gemm_plan_silu(int M, int N, int K) {
     if (p.N == N && p.K == K) {
       const size_t b = (size_t)((M + 63) / 64) - 1;
       return b < p.silu.size() ? p.silu[b] : -1;
+    }
+  return -1;
+}
+
+void gemm_plan_set_rope(int N, int K, const int* codes, int n) {
+  for (auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      p.rope.assign(codes, codes + n);
+      return;
+    }
+  GemmPlan q{N, K, {}, {}, {}, {}, {}, {}, {}, {}};
+  q.rope.assign(codes, codes + n);
+  g_plans.push_back(std::move(q));
+}
+
+// QKV + RoPE + K/V write: the path measured fastest with that epilogue for
+// this M bucket (tools/tune_gemm_plan.py MCP_TUNE_ROPE=1), -1 = none (the
+// rule).  MCP_GEMM_ROPE_PLAN=0 disables.
+int gemm_plan_rope(int M, int N, int K) {
+  static const int on = getenv("MCP_GEMM_ROPE_PLAN") ? atoi(getenv("MCP_GEMM_ROPE_PLAN")) : 1;
+  if (!on) return -1;
+  for (const auto& p : g_plans)
+    if (p.N == N && p.K == K) {
+      const size_t b = (size_t)((M + 63) / 64) - 1;
+      return b < p.rope.size() ? p.rope[b] : -1;
     }
   return -1;
 }
@@ -615,19 +641,25 @@ __global__ __launch_bounds__(256) void splitk_reduce_rope(const float* __restric
 
 // QKV + RoPE + K/V write through the plan's flex x split-K entry for this
 // bucket, the reduce doing the rope_kv work; nonzero: not taken
-int launch_qkv_rope_fsplit(const void* X, const void* W, int M, int N, int K, int D,
-                           const RopeArgs& ra, hipStream_t s) {
-  static const int on = getenv("MCP_QKV_ROPE_FSPLIT") ? atoi(getenv("MCP_QKV_ROPE_FSPLIT")) : 1;
-  if (!on || D != 128 || N != (ra.Hq + 2 * ra.Hkv) * D) return 1;
-  const int fs = gemm_plan_fsplit(M, N, K);
-  if (fs < 0) return 1;
-  const int S = fs % 16;
+// flex tile cand x S-way split-K, the reduce applying RoPE + the K/V write
+int launch_qkv_rope_flex_split(const void* X, const void* W, int M, int N, int K, int D,
+                               const RopeArgs& ra, int cand, int S, hipStream_t s) {
+  if (D != 128 || N != (ra.Hq + 2 * ra.Hkv) * D) return 1;
   if (!g_splitk_ws || (size_t)S * M * N * sizeof(float) > g_splitk_ws_bytes) return 4;
-  if (launch_gemm_flex_partials(X, W, g_splitk_ws, M, N, K, fs / 16, S, s)) return 2;
+  if (launch_gemm_flex_partials(X, W, g_splitk_ws, M, N, K, cand, S, s)) return 2;
   const size_t total = (size_t)M * (ra.Hq + 2 * ra.Hkv) * (D / 16);
   splitk_reduce_rope<128><<<(unsigned)((total + 255) / 256), 256, 0, s>>>(g_splitk_ws, S, M, ra,
                                                                             norm_epi());
   return 0;
+}
+
+int launch_qkv_rope_fsplit(const void* X, const void* W, int M, int N, int K, int D,
+                           const RopeArgs& ra, hipStream_t s) {
+  static const int on = getenv("MCP_QKV_ROPE_FSPLIT") ? atoi(getenv("MCP_QKV_ROPE_FSPLIT")) : 1;
+  if (!on) return 1;
+  const int fs = gemm_plan_fsplit(M, N, K);
+  if (fs < 0) return 1;
+  return launch_qkv_rope_flex_split(X, W, M, N, K, D, ra, fs / 16, fs % 16, s);
 }
 
 // flex tile cand, S-way split-K through the fp32 workspace + the reduce

@@ -621,11 +621,41 @@ int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R,
   return launch_256d_impl(X, W, Y, R, M, N, K, epi, bm, RopeArgs{}, s);
 }
 
+// One QKV + RoPE + K/V-write path by code (the tuner's candidates and the
+// "rope" plan):
+//   1..5            AGPR kernel, EPI 3, at the height of plan code c
+//   200             weight-streaming kernel, EPI 3 (M <= 128)
+//   500             the GEMM by the code / flex plan into qkv, then rope_kv
+//   1000 + 16 c + S flex tile c x S-way split-K, the reduce applies RoPE
+// nonzero: not supported for this shape (nothing launched)
+int launch_qkv_rope_algo(const void* X, const void* W, void* qkv, int M, int N, int K, int D,
+                         const RopeArgs& ra, int algo, hipStream_t s) {
+  if (D != 128 || N != (ra.Hq + 2 * ra.Hkv) * 128) return 1;
+  if (algo >= 1000)
+    return launch_qkv_rope_flex_split(X, W, M, N, K, D, ra, (algo - 1000) / 16, (algo - 1000) % 16, s);
+  if (algo == 500) {
+    launch_gemm_tn(X, W, qkv, nullptr, M, N, K, s);
+    launch_rope_kv(qkv, ra.pos, ra.slots, ra.cos_sin, ra.q_out, ra.k_cache, ra.v_cache, M, ra.Hq,
+                   ra.Hkv, D, ra.BS, s);
+    return 0;
+  }
+  if (algo == 200) return launch_gemm_stream(X, W, nullptr, nullptr, M, N, K, 3, ra, s);
+  if (algo >= 1 && algo <= 5) {
+    if (gemm256d_ok(M, N, K)) return 4;
+    return launch_256d_impl(X, W, nullptr, nullptr, M, N, K, 3, gemm256d_code_height(algo), ra, s);
+  }
+  return 5;
+}
+
 // QKV + RoPE + paged K/V write (EPI 3) on the AGPR kernel when the selector
 // picks it for this shape; otherwise the plain GEMM into qkv and rope_kv
 void launch_qkv_rope(const void* X, const void* W, void* qkv, int M, int N, int K, int D,
                      const RopeArgs& ra, hipStream_t s) {
   static const int fused = getenv("MCP_QKV_ROPE_FUSED") ? atoi(getenv("MCP_QKV_ROPE_FUSED")) : 1;
+  // a measured path for the bucket (timed at its top row; the decode sizes
+  // below 33 rows keep the stream kernel)
+  const int rp = (fused && M > 32) ? gemm_plan_rope(M, N, K) : -1;
+  if (rp >= 0 && launch_qkv_rope_algo(X, W, qkv, M, N, K, D, ra, rp, s) == 0) return;
   if (fused && gemm_stream_enabled() && gemm_stream_pick(M, N, K, 3) &&
       launch_gemm_stream(X, W, nullptr, nullptr, M, N, K, 3, ra, s) == 0)
     return;

@@ -229,3 +229,10 @@ int launch_gemm_flex_split(const void* X, const void* W, void* Y, const void* R,
                            int K, int cand, int S, int epi, hipStream_t s);
 int launch_qkv_rope_fsplit(const void* X, const void* W, int M, int N, int K, int D,
                            const RopeArgs& ra, hipStream_t s);
+int launch_qkv_rope_flex_split(const void* X, const void* W, int M, int N, int K, int D,
+                               const RopeArgs& ra, int cand, int S, hipStream_t s);
+// one QKV + RoPE path by code (gemm256d.hip: AGPR height, stream, unfused, flex x split)
+int launch_qkv_rope_algo(const void* X, const void* W, void* qkv, int M, int N, int K, int D,
+                         const RopeArgs& ra, int algo, hipStream_t s);
+void gemm_plan_set_rope(int N, int K, const int* codes, int n);
+int gemm_plan_rope(int M, int N, int K);

@@ -81,6 +81,8 @@ def _load_gemm_plan(mod, path: Optional[str] = None) -> int:
             mod.gemm_plan_set_persist(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["persist"]])
         if "silu" in sh and hasattr(mod, "gemm_plan_set_silu"):
             mod.gemm_plan_set_silu(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["silu"]])
+        if "rope" in sh and hasattr(mod, "gemm_plan_set_rope"):
+            mod.gemm_plan_set_rope(int(sh["N"]), int(sh["K"]), [int(c) for c in sh["rope"]])
     return len(plan["shapes"])
 
 

@@ -888,6 +888,39 @@ def test_qkv_rope_fused(M, long_ctx):
     assert kc.cpu().permute(0, 2, 1, 3).reshape(nb * BS, -1)[~used].abs().sum() == 0
 
 
+@pytest.mark.parametrize("M", [100, 200, 330])
+def test_qkv_rope_every_path(M):
+    """Every QKV + RoPE + K/V-write path the "rope" plan can name
+    (launch_qkv_rope_algo: AGPR heights, stream, unfused GEMM + rope_kv, flex x
+    split-K with the RoPE reduce) gives the fp32 reference's q / K / V rows."""
+    torch.manual_seed(14)
+    L = ops.lib()
+    Hq, Hkv, D, H, BS = 32, 8, 128, 4096, 64
+    N = (Hq + 2 * Hkv) * D
+    X = torch.randn(M, H, device=DEV).bfloat16()
+    W = (torch.randn(N, H, device=DEV) / math.sqrt(H)).bfloat16()
+    nb = (M + BS - 1) // BS + 1
+    pos = torch.randint(0, 8000, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * BS, device=DEV)[:M].to(torch.int32)
+    cs = ref.rope_cos_sin(8192, D, 500000.0, DEV)
+    qkv_ref = ref.gemm(X, W).cpu()
+    qr, kr, vr = (torch.zeros(M, Hq, D), torch.zeros(nb, Hkv, BS, D), torch.zeros(nb, Hkv, BS, D))
+    ref.rope_kv(qkv_ref, pos.cpu(), slots.cpu(), cs.cpu(), qr, kr, vr, Hq, Hkv, D)
+    ran = 0
+    for a in [1, 2, 3, 4, 5, 200, 500] + [1000 + 16 * c + S for c in (0, 6, 10) for S in (2, 4)]:
+        q = torch.zeros(M, Hq, D, device=DEV, dtype=torch.bfloat16)
+        kc = torch.zeros(nb, Hkv, BS, D, device=DEV, dtype=torch.bfloat16)
+        vc = torch.zeros_like(kc)
+        qkv = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        if L.qkv_rope_algo(X, W, qkv, pos, slots, cs, q, kc, vc, Hq, Hkv, D, a):
+            continue
+        torch.cuda.synchronize()
+        assert rel_err(q.cpu(), qr) < 1e-2, a
+        assert rel_err(kc.cpu(), kr) < 1e-2 and rel_err(vc.cpu(), vr) < 1e-2, a
+        ran += 1
+    assert ran >= 8
+
+
 @pytest.mark.parametrize("M,N,K", [(4352, 4096, 4096), (3000, 28672, 4096), (2304, 6144, 4096)])
 def test_gemm_hybrid_streamk_tail(M, N, K):
     """Hybrid launch (gemm256d.hip full waves + gemm256sk.hip stream-K tail when

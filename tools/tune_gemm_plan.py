@@ -72,6 +72,8 @@ if os.environ.get("MCP_TUNE_SHAPES") == "swiglu":
     SHAPES = [sh for sh in SHAPES if sh[0] in SWIGLU_N]
 elif os.environ.get("MCP_TUNE_SHAPES") == "narrow":     # all but gate|up
     SHAPES = [sh for sh in SHAPES if sh[0] not in SWIGLU_N]
+elif os.environ.get("MCP_TUNE_SHAPES") == "residual":   # o and down (with MCP_TUNE_SSOUT=1)
+    SHAPES = [sh for spec in MODEL.split("+") for i, sh in enumerate(shard_shapes(spec)) if i in (1, 3)]
 MSTEP = 64
 M_MIN = 256                                # below: 128^2 path only (gemm_select)
 M_SPLIT_MAX = 1024                         # split-K measured up to here
@@ -94,11 +96,28 @@ FS_MIN = int(os.environ.get("MCP_TUNE_FS_MIN", "65"))    # flex x split-K measur
 FS_MAX = int(os.environ.get("MCP_TUNE_FS_MAX", "512"))
 
 
+# MCP_TUNE_SSOUT=1: the residual projections are timed with the fused-norm
+# statistic too (ss_out, as the TP=1 model runs them: the epilogue's per-row
+# sum of squares and its atomic add cost differently on each path)
+SSOUT = os.environ.get("MCP_TUNE_SSOUT", "0") == "1"
+_SS = {}
+
+
+def _ss(R, M):
+    if not (SSOUT and R is not None):
+        return None
+    buf = _SS.get(R.device)
+    if buf is None or buf.numel() < M:
+        buf = _SS[R.device] = torch.zeros(max(M, 8192), dtype=torch.int64, device=R.device)
+    return buf[:M]
+
+
 def run(code, X, W, Y, split=-1, R=None):
+    ss = _ss(R, X.shape[0])
     if code == "fsplit":                   # flex tile x split-K, split = 16 cand + S
-        L.gemm(X, W, Y, R, 1000 + split)
+        L.gemm(X, W, Y, R, 1000 + split, ss)
     elif code == "flex":                   # flex tile, split = candidate
-        L.gemm(X, W, Y, R, 16 + split)
+        L.gemm(X, W, Y, R, 16 + split, ss)
     elif code == "lib":                    # hipBLASLt yardstick (never dispatched)
         if R is not None:
             Y.addmm_(X, W.t())
@@ -106,10 +125,10 @@ def run(code, X, W, Y, split=-1, R=None):
             torch.matmul(X, W.t(), out=Y)
     elif code == 0:
         L.gemm_splitk_force(split)
-        L.gemm(X, W, Y, R, 0)
+        L.gemm(X, W, Y, R, 0, ss)
         L.gemm_splitk_force(-1)
     else:                                  # AGPR kernel at the height of plan code 1..5
-        L.gemm(X, W, Y, R, 8 + code)
+        L.gemm(X, W, Y, R, 8 + code, ss)
 
 
 def time_ms(fn, Ws, reps=10):
@@ -209,8 +228,98 @@ def tune_silu():
     print(json.dumps({"written": out_path, "s": round(time.time() - t0, 1)}), flush=True)
 
 
+def tune_rope():
+    """MCP_TUNE_ROPE=1: the same for the qkv projection with its production
+    epilogue - RoPE on q / k, the paged K/V write, the fused-norm statistic
+    (launch_qkv_rope_algo codes) - recorded as the shape's "rope" entry."""
+    from mcp_amd.ops import reference as ref
+    with open(ops.GEMM_PLAN_FILE) as f:
+        plan = json.load(f)
+    ops._load_gemm_plan(L, ops.GEMM_PLAN_FILE)
+    eps, D, BS = 1e-5, 128, 64
+    t0 = time.time()
+    qkv_shapes = {shard_shapes(spec)[0] for spec in MODEL.split("+")}
+    for sh in plan["shapes"]:
+        N, K = int(sh["N"]), int(sh["K"])
+        if (N, K) not in qkv_shapes:
+            continue
+        name = next(spec for spec in MODEL.split("+") if shard_shapes(spec)[0] == (N, K))
+        arch, _, tp = name.partition("-tp")
+        Hq, Hkv = ARCH[arch][1] // int(tp or 1), max(1, ARCH[arch][2] // int(tp or 1))
+        if (Hq + 2 * Hkv) * D != N:
+            continue
+        nb = m_max // MSTEP
+        L.gemm_plan_set_rope(N, K, [-1] * nb)
+        Xf = torch.randn(m_max, K, device=dev).bfloat16()
+        Wc = [(torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+              for _ in range(max(2, int(1.5e9 // (N * K * 2))))]
+        qkvf = torch.empty(m_max, N, device=dev, dtype=torch.bfloat16)
+        qf = torch.empty(m_max, Hq, D, device=dev, dtype=torch.bfloat16)
+        nblk = m_max // BS + 2
+        kc = torch.zeros(nblk, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
+        vc = torch.zeros_like(kc)
+        posf = torch.randint(0, 8000, (m_max,), device=dev, dtype=torch.int32)
+        slotsf = torch.randperm(nblk * BS, device=dev)[:m_max].to(torch.int32)
+        cs = ref.rope_cos_sin(8192, D, 500000.0, dev)
+        ssf = (Xf.float().pow(2).sum(-1) * (1 << 20)).to(torch.int64)
+        rope, us = [], []
+        for b in range(nb):
+            M = (b + 1) * MSTEP
+            X, qkv, q, pos, slots, ss = Xf[:M], qkvf[:M], qf[:M], posf[:M], slotsf[:M], ssf[:M]
+            cands = [("prod", -1), ("a", 500)]
+            if M >= 128:
+                cands += [("a", c) for c in (1, 2, 3, 4, 5)]
+            if M <= 128:
+                cands.append(("a", 200))
+            if FS_MIN <= M <= FS_MAX:
+                for c, (tm, tn) in enumerate(FS_TILES):
+                    tiles = -(-M // tm) * -(-N // tn)
+                    for S in (2, 3, 4, 7, 8):
+                        if (K // 64) % S == 0 and 128 <= tiles * S <= 1024:
+                            cands.append(("a", 1000 + 16 * c + S))
+
+            def fn(c, w):
+                if c[0] == "prod":
+                    L.qkv_rope(X, w, qkv, pos, slots, cs, q, kc, vc, Hq, Hkv, D, ss, eps)
+                elif L.qkv_rope_algo(X, w, qkv, pos, slots, cs, q, kc, vc, Hq, Hkv, D, c[1], ss, eps):
+                    raise ValueError("unsupported")
+            ok = []
+            for c in cands:
+                try:
+                    fn(c, Wc[0])
+                    ok.append(c)
+                except (ValueError, RuntimeError):
+                    pass
+            torch.cuda.synchronize()
+            best = {c: float("inf") for c in ok}
+            for _ in range(3):
+                for c in ok:
+                    best[c] = min(best[c], time_ms(lambda w, c=c: fn(c, w), Wc))
+            prod = best.pop(("prod", -1))
+            win = min(best, key=best.get) if best else None
+            take = win is not None and best[win] * 1.01 < prod
+            rope.append(win[1] if take else -1)
+            us.append([round(prod * 1e3, 1), round(min(prod, best[win]) * 1e3 if take else prod * 1e3, 1)])
+            print(json.dumps({"N": N, "K": K, "M": M, "prod_us": round(prod * 1e3, 1),
+                              "best": win[1] if win else None,
+                              "best_us": round(best[win] * 1e3, 1) if win else None,
+                              "taken": bool(take), "s": round(time.time() - t0, 1)}), flush=True)
+        sh["rope"] = rope
+        sh["rope_us"] = us
+        del Xf, Wc, qkvf, qf, kc, vc
+    plan["rope"] = ("qkv + RoPE + K/V write path per bucket (launch_qkv_rope_algo code; -1 = the "
+                    "rule); rope_us: [production before, chosen] us")
+    with open(out_path, "w") as f:
+        json.dump(plan, f, indent=None, separators=(",", ":"))
+        f.write("\n")
+    print(json.dumps({"written": out_path, "s": round(time.time() - t0, 1)}), flush=True)
+
+
 if os.environ.get("MCP_TUNE_SILU") == "1":
     tune_silu()
+    sys.exit(0)
+if os.environ.get("MCP_TUNE_ROPE") == "1":
+    tune_rope()
     sys.exit(0)
 
 result = {"arch": torch.cuda.get_device_properties(0).gcnArchName.split(":")[0],
