@@ -662,6 +662,10 @@ void car_connect(int64_t h, const at::Tensor& all_handles) {
 // ss (optional, int64 [>= rows]): also add each output row's fixed-point sum
 // of squares (the fused RMSNorm statistic of the next layer); rows are the
 // last dimension of inp
+void comm_emulate(double us, int64_t nbytes, int64_t max_blocks) {
+  TORCH_CHECK(launch_comm_emulate(us, nbytes, (int)max_blocks, stream()) == 0, "comm_emulate failed");
+}
+
 void car_run(int64_t h, const at::Tensor& inp, at::Tensor& out, int64_t mode, int64_t blocks,
              const c10::optional<at::Tensor>& ss) {
   CHECK_BF16_TENSOR(inp); CHECK_BF16_TENSOR(out);
@@ -856,6 +860,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("car_handle_bytes", []() { return (int64_t)car_handle_bytes(); });
   m.def("car_init", &car_init);
   m.def("car_connect", &car_connect);
+  m.def("comm_emulate", &comm_emulate, "hold a K12 call's CUs for us microseconds (TP simulation)",
+        py::arg("us"), py::arg("nbytes"), py::arg("max_blocks") = 0);
   m.def("car_run", &car_run, py::arg("h"), py::arg("inp"), py::arg("out"), py::arg("mode"),
         py::arg("blocks"), py::arg("ss") = py::none());
   m.def("car_error", [](int64_t h) { return car_error((void*)(intptr_t)h); });

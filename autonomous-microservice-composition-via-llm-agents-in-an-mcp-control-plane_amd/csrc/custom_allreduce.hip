@@ -266,7 +266,37 @@ struct CarState {
 
 constexpr size_t SIG_BYTES = sizeof(unsigned) * 2 * CAR_MAX_BLOCKS * CAR_MAX_RANKS;
 
+// Emulated all-reduce (bench_tp.py --simulate-rank --emulate-comm): holds the
+// CUs a K12 call of the same size would hold (its block count, 512 threads,
+// every wave resident) for the modelled duration, then exits - so one GPU
+// running one TP rank's compute measures what a comm stream beside it costs
+// (CUs the GEMMs on the compute stream cannot use) and hides (time it runs
+// under them).  No memory is touched.
+__global__ __launch_bounds__(CAR_THREADS) void comm_emulate_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+
 }  // namespace
+
+int launch_comm_emulate(double us, long long nbytes, int max_blocks, hipStream_t s) {
+  static int rate_khz = 0;
+  if (rate_khz <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        rate_khz <= 0)
+      return -1;
+  }
+  if (us <= 0.0) return 0;
+  const long long nvec = (nbytes + 15) / 16;
+  const long long want = (nvec + CAR_THREADS * 4 - 1) / (CAR_THREADS * 4);
+  const int cap = max_blocks > 0 ? min(max_blocks, CAR_MAX_BLOCKS) : CAR_MAX_BLOCKS;
+  const int blocks = (int)max(1LL, min(want, (long long)cap));
+  const unsigned long long ticks = (unsigned long long)(us * rate_khz / 1000.0);
+  comm_emulate_kernel<<<blocks, CAR_THREADS, 0, s>>>(ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 size_t car_handle_bytes() { return 2 * sizeof(hipIpcMemHandle_t); }
 

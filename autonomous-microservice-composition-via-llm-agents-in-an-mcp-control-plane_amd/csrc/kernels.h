@@ -198,6 +198,8 @@ void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float
 size_t car_handle_bytes();
 void* car_create(int rank, int world, size_t buf_bytes, void* handles_out);
 int car_open(void* state, const void* all_handles);
+// emulated K12 call: its block count, resident for ``us`` (bench_tp --emulate-comm)
+int launch_comm_emulate(double us, long long nbytes, int max_blocks, hipStream_t s);
 int car_allreduce(void* state, const void* inp, void* out, long long n_elems, int mode,
                   int blocks, hipStream_t s, unsigned long long* ss = nullptr, int row_len = 0);
 int car_error(void* state);

@@ -45,9 +45,26 @@ def log(*a):
 class _SimAllReduce:
     """Stands in for the TP group's all-reduce on a simulated rank: no data
     moves (the rank's partial sums flow on unreduced - the arithmetic per
-    rank is unchanged), capturable in hipGraphs like K12."""
+    rank is unchanged), capturable in hipGraphs like K12.  ``emulate``: each
+    call launches a kernel that holds the CUs a K12 call of that size would
+    hold for the xGMI model's time (csrc/custom_allreduce.hip
+    comm_emulate_kernel), on the caller's stream - so the row-chunked MLP
+    block's comm stream (models/llama.py _mlp_block_overlapped) is measured
+    overlapping the GEMMs for real, CU contention included."""
+
+    def __init__(self, emulate: bool = False, tp: int = 1, car_max: int = 0):
+        self.emulate, self.tp, self.car_max = emulate, tp, car_max
+        self.calls = 0
 
     def __call__(self, t):
+        if self.emulate and t.is_cuda:
+            from mcp_amd import ops
+            from mcp_amd.parallel import xgmi_model as xm
+            nbytes = t.numel() * t.element_size()
+            # MCP_CAR_BLOCKS caps the blocks as it caps K12's
+            ops.lib().comm_emulate(xm.best(nbytes, self.tp, self.car_max)[1], nbytes,
+                                   int(os.environ.get("MCP_CAR_BLOCKS", "0")))
+            self.calls += 1
         return None
 
     def check(self):
@@ -118,8 +135,11 @@ def simulate_rank(args):
     cfg = get_config(args.model)
     H = cfg.hidden
     t0 = time.time()
+    from mcp_amd.parallel.comm import K12_MAX_BYTES
+    car_max = int(os.environ.get("MCP_CAR_MAX_BYTES", str(K12_MAX_BYTES)))
+    sim_ar = _SimAllReduce(emulate=args.emulate_comm and cuda, tp=tp, car_max=car_max)
     model = LlamaModel(cfg, random_weights(cfg, dev, seed=args.seed, tp_rank=0, tp=tp), dev,
-                       0, tp, None, allreduce=_SimAllReduce())
+                       0, tp, None, allreduce=sim_ar)
     sync()
     log(f"[sim rank 0 of TP={tp}] {args.model} shard ready in {time.time() - t0:.1f}s")
     per_block = KVCache.bytes_per_block(cfg.layers, model.hkv, cfg.head_dim)
@@ -170,8 +190,26 @@ def simulate_rank(args):
     for T, ns in steps:
         msgs += [T * H * 2] * (2 * (cfg.layers - 1)) + ([ns * H * 2] * 2 if ns else [])
     from mcp_amd.parallel import xgmi_model as xm
-    from mcp_amd.parallel.comm import K12_MAX_BYTES
-    car_max = int(os.environ.get("MCP_CAR_MAX_BYTES", str(K12_MAX_BYTES)))
+    if sim_ar.emulate:
+        # the timed steps ran every all-reduce as an emulated K12 call on the
+        # GPU: the measured time IS the prediction (overlap as the model ran it)
+        plans = len(seqs_all)
+        print(json.dumps({
+            "config": "llama3-70b TP planner, 50-service registry (config 4), one rank simulated "
+                      "on one GPU, all-reduces emulated on the GPU",
+            "model": args.model, "tp": tp, "services": args.services, "batch": args.batch,
+            "steps": args.steps, "engine_steps": len(steps), "plans": plans,
+            "emulated_allreduce_calls": sim_ar.calls,
+            "measured_step_s": round(compute_s / args.steps, 3),
+            "measured_plans_per_s": round(plans / compute_s, 2),
+            "p50_latency_ms": round(lats[len(lats) // 2] * 1e3, 1),
+            "tp_overlap_min_tokens": model._overlap_min_t if model._comm is not None else None,
+            "emulation": "each all-reduce = a kernel holding K12's CUs (its block count) for the "
+                         "xGMI model's time (parallel/xgmi_model.py), on the stream the model "
+                         "issues it on (the comm stream of the row-chunked MLP block at >= "
+                         "tp_overlap_min_tokens tokens, else in line)",
+            "data": "synthetic intents, random-init weights"}), flush=True)
+        return
     # K12 sizes measured on a grid (64-token steps of [T, H] bf16, up to the K12
     # limit): two processes on this ONE GPU - what that times is mostly the
     # two contexts' time-slicing on one device, not links, so it only backs
@@ -263,6 +301,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="TP degree = ranks (one per GPU); N > 1 self-launches")
     ap.add_argument("--no-k12-timing", action="store_true",
                     help="--simulate-rank: skip the two-process K12 timing on this GPU")
+    ap.add_argument("--emulate-comm", action="store_true",
+                    help="--simulate-rank: run every all-reduce as an emulated K12 call on the GPU "
+                         "(measured overlap) instead of pricing it after the run")
     ap.add_argument("--simulate-rank", type=int, default=0, metavar="TP",
                     help="predict config 4 at TP=N from one rank's shards on one GPU (simulate_rank)")
     args = ap.parse_args()

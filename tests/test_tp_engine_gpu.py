@@ -130,3 +130,66 @@ def test_tp8_eight_processes_one_gpu_matches_tp1(monkeypatch):
     lp = LocalPlanner(eng1, reg, max_nodes=4)
     dags_1 = lp.plan_many(intents) + lp.plan_many([synthetic_intent(7)])
     assert dags_tp == dags_1
+
+
+class _DoubleAR:
+    """Two identical ranks' all-reduce: every element doubles (no ss: the
+    model adds the statistic with row_sumsq)."""
+
+    def __init__(self):
+        self.streams = set()
+
+    def __call__(self, t):
+        self.streams.add(torch.cuda.current_stream(t.device).cuda_stream)
+        t.mul_(2)
+
+    def check(self):
+        return None
+
+    def graph_safe(self, nbytes):
+        return True
+
+
+@pytest.mark.parametrize("T", [300, 700])
+def test_tp_mlp_block_row_chunks_overlap_matches_unchunked(T, monkeypatch):
+    """TP > 1: the o-projection / MLP block as two row chunks with their
+    all-reduces on the comm stream (models/llama.py _mlp_block_overlapped)
+    gives the unchunked block's rows and fused-norm statistics, rank 0 (the
+    residual) and another rank alike, and the collectives ran on the comm
+    stream."""
+    from mcp_amd import ops
+    from mcp_amd.models.llama import LlamaModel, get_config, random_weights
+    monkeypatch.setenv("MCP_TP_OVERLAP_MIN_T", "64")
+    cfg = get_config("tiny-tp8")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    for rank in (0, 1):
+        ar = _DoubleAR()
+        m = LlamaModel(cfg, random_weights(cfg, dev, seed=9, tp_rank=rank, tp=2), dev, rank, 2, None,
+                       allreduce=ar)
+        assert m._comm is not None
+        lw = m.w.layers[0]
+        a = torch.randn(T, m.hq * cfg.head_dim, device=dev).bfloat16()
+        x = torch.randn(T, cfg.hidden, device=dev).bfloat16()
+        ss_mid = torch.zeros(T, dtype=torch.int64, device=dev)
+        ss_next = torch.zeros_like(ss_mid)
+        z = m._mlp_block_overlapped(a, lw, x, ss_mid, ss_next, 1e-5)
+        torch.cuda.synchronize()
+        assert m._comm.cuda_stream in ar.streams
+        # unchunked, in line
+        rs_mid = torch.zeros_like(ss_mid)
+        rs_next = torch.zeros_like(ss_mid)
+        y = ops.gemm(a, lw.wo, R=x if rank == 0 else None)
+        y.mul_(2)
+        ops.row_sumsq(y, rs_mid)
+        act = ops.gemm_silu(y, lw.w_gate_up, ss_in=rs_mid, eps=1e-5)
+        z_ref = ops.gemm(act, lw.w_down, R=y if rank == 0 else None)
+        z_ref.mul_(2)
+        ops.row_sumsq(z_ref, rs_next)
+        torch.cuda.synchronize()
+        err = ((z.float() - z_ref.float()).norm() / z_ref.float().norm()).item()
+        assert err < 1e-2, (rank, err)
+        # (the chunks' GEMMs may take other tiles than the whole block's: equal
+        # up to their rounding)
+        for got, want in ((ss_mid, rs_mid), (ss_next, rs_next)):
+            assert (got.double() - want.double()).abs().max() <= 1e-2 * want.double().abs().max()
