@@ -7,6 +7,7 @@ counted).  Also prints the schema of the marker table it used.
 
     python tools/gap_attribution.py run_results.db [last_ms] [min_us]
 """
+import json
 import sqlite3
 import sys
 from collections import defaultdict
@@ -27,7 +28,30 @@ def main(db, last_ms=None, min_us=200.0):
     # marker ranges: the first table / view with name + start + end besides kernels
     rng = []
     used = None
-    for o in objs:
+    if "regions" in objs:                  # rocpd views (rocprofv3 -f rocpd)
+        n_all = c.execute("select count(*) from regions").fetchone()[0]
+        names = [r[0] for r in c.execute("select distinct name from regions limit 20")]
+        print(f"# regions view: {n_all} rows, names {names}")
+        rows = list(c.execute("select name, start, end from regions where end >= ?", (t0,)))
+        # roctx ranges: the region is the API call (roctxThreadRangeA), the
+        # range's text is the "message" of its extdata JSON
+        try:
+            msg = []
+            for ext, s0, e0 in c.execute("select extdata, start, end from regions where end >= ?", (t0,)):
+                try:
+                    m = json.loads(ext).get("message") if ext else None
+                except (ValueError, AttributeError):
+                    m = None
+                if m:
+                    msg.append((m, s0, e0))
+            if msg:
+                rows = msg
+            print(f"# roctx messages: {len(msg)}")
+        except sqlite3.Error as e:
+            print(f"# extdata read failed: {e}")
+        if rows:
+            rng, used = rows, ("regions", ["name", "start", "end"])
+    for o in ([] if used else objs):
         if o in ("kernels",) or "kernel" in o.lower():
             continue
         try:
@@ -56,9 +80,14 @@ def main(db, last_ms=None, min_us=200.0):
             lo, hi = max(a, s), min(b, e)
             if hi > lo:
                 cover[name] += hi - lo
-    print("| host range | ms of gap covered | per gap us |\n|---|---|---|")
+    tot, cnt = defaultdict(float), defaultdict(int)
+    for name, s0, e0 in rng:
+        tot[name] += e0 - s0
+        cnt[name] += 1
+    print("| host range | ms of gap covered | per gap us | ms in window | calls | us per call |\n|---|---|---|---|---|---|")
     for name, t in sorted(cover.items(), key=lambda x: -x[1]):
-        print(f"| `{name}` | {t / 1e6:.1f} | {t / 1e3 / max(1, len(gaps)):.0f} |")
+        print(f"| `{name}` | {t / 1e6:.1f} | {t / 1e3 / max(1, len(gaps)):.0f} | "
+              f"{tot[name] / 1e6:.1f} | {cnt[name]} | {tot[name] / 1e3 / max(1, cnt[name]):.0f} |")
 
 
 if __name__ == "__main__":
