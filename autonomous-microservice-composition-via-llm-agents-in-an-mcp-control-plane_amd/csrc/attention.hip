@@ -248,6 +248,7 @@ void attn_kernel(const AttnArgs a) {
   const int Hq = a.Hq, Hkv = a.Hkv;
 
   int s = 0, qs, ql, cl, tok, qpos, kt0, ntiles;
+  int kv_stop = 1 << 30;                                  // MODE 0: the item's last key + 1
   bool qvalid;
   const int* bt;
   if (MODE == 1) {
@@ -289,6 +290,7 @@ void attn_kernel(const AttnArgs a) {
     qpos = cl - ql + tok;
     const int last_tok = min(q0 + item_waves * TPW, ql) - 1;
     const int kv_end = cl - ql + last_tok + 1;
+    kv_stop = kv_end;
     ntiles = (kv_end + KT - 1) / KT;
     kt0 = a.kv_begin ? a.kv_begin[s] / KT : 0;
     if constexpr (KSPLIT) {                               // this split's share of the tiles
@@ -310,7 +312,12 @@ void attn_kernel(const AttnArgs a) {
     }
   }
 
-  // staging: piece p covers rows 4p..4p+3 of the K (p<16) or V (p>=16) tile
+  // staging: piece p covers rows 4p..4p+3 of the K (p<16) or V (p>=16) tile.
+  // A sequence's last tile is read only up to its last key: pieces wholly
+  // past it are not fetched (HBM bytes the per-request pass - bandwidth
+  // bound - would otherwise spend on rows every query masks); their V rows
+  // are zeroed in LDS instead (P is 0 there, and 0 x stale LDS could be NaN),
+  // their K rows stay stale (those scores are masked before the softmax)
   const int srow = lane >> 4;
   BtLanes bt_at(bt, kt0, ntiles);
   auto stage = [&](int kt, int buf) {
@@ -318,10 +325,15 @@ void attn_kernel(const AttnArgs a) {
     const bf16* kb = a.kc + (blk * Hkv + kvh) * (size_t)TILE;
     const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
+    const int rows_valid = kv_stop - kt * KT;              // >= 1 for a staged tile
 #pragma unroll
     for (int i = 0; i < PIECES / NW; ++i) {
       const int p = wave * (PIECES / NW) + i;
       const int tile = p >> 4, pr = p & 15;
+      if (pr * 4 >= rows_valid) {                          // wave-uniform
+        if (tile) *reinterpret_cast<u32x4*>(base + TILE + pr * 512 + lane * 8) = u32x4{0, 0, 0, 0};
+        continue;
+      }
       const int row = pr * 4 + srow;
       const int chunk = (lane & 15) ^ (row & 15);
       const bf16* src = (tile ? vb : kb) + row * D + chunk * 8;
