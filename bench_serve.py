@@ -67,8 +67,13 @@ def run_qps(planner, engine, qps, duration, seed, rank):
     t0 = time.perf_counter()
     i = 0
     batch_sizes = []
+    next_log = 30.0            # a progress line every 30 s (long soak runs stay visibly alive)
     while i < n or engine.has_work():
         now = time.perf_counter() - t0
+        if now >= next_log:
+            log(f"[qps {qps}] {now:.0f} s: {i} of {n} submitted, {len(done_at)} done, "
+                f"{len(engine.running)} running")
+            next_log += 30.0
         while i < n and arrivals[i] <= now:
             dec, ptoks, stoks = planner.prepare(synthetic_intent(rank * 1_000_000 + i), services)
             arr = arrivals[i]
