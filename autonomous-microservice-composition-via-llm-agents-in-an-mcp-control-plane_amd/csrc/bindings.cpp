@@ -626,6 +626,27 @@ void sample_dense(const at::Tensor& logits, const at::Tensor& ctr, double temper
   check_launch("sample_dense");
 }
 
+// decision lookahead: the sampled outcome's tokens / sizes / allowed set into
+// the next step's device views (sampling.hip).  The caller (engine
+// _launch_branch) bounds every offset of ``tab`` against these views on the host.
+void branch_select(const at::Tensor& prev_tok, const at::Tensor& tab, int64_t n, at::Tensor& ids,
+                   at::Tensor& slots, at::Tensor& q_len, at::Tensor& ctx_len, at::Tensor& rows, at::Tensor& aptr,
+                   at::Tensor& aids, at::Tensor& err) {
+  CHECK_I32_TENSOR(prev_tok); CHECK_I32_TENSOR(tab); CHECK_I32_TENSOR(ids); CHECK_I32_TENSOR(slots);
+  TORCH_CHECK(slots.numel() == ids.numel(), "branch_select: slots / ids");
+  CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len); CHECK_I32_TENSOR(rows);
+  CHECK_I32_TENSOR(aptr); CHECK_I32_TENSOR(aids); CHECK_I32_TENSOR(err);
+  TORCH_CHECK(n >= 0 && q_len.numel() >= n && ctx_len.numel() >= n && rows.numel() >= n &&
+              aptr.numel() >= n + 1 && tab.numel() >= 2 + 6 * n, "branch_select sizes");
+  const int rc = launch_branch_select(prev_tok.data_ptr<int>(), tab.data_ptr<int>(), (int)n,
+                                      ids.data_ptr<int>(), slots.data_ptr<int>(), q_len.data_ptr<int>(),
+                                      ctx_len.data_ptr<int>(), rows.data_ptr<int>(),
+                                      aptr.data_ptr<int>(), (int)aptr.numel(),
+                                      aids.data_ptr<int>(), err.data_ptr<int>(), stream());
+  TORCH_CHECK(rc == 0, "branch_select: too many sequences");
+  check_launch("branch_select");
+}
+
 void copy_blocks(at::Tensor& data, const at::Tensor& src, const at::Tensor& dst) {
   CHECK_BF16_TENSOR(data); CHECK_I32_TENSOR(src); CHECK_I32_TENSOR(dst);
   TORCH_CHECK(data.dim() == 6, "kv data [L, 2, nb, Hkv, BS, D]");
@@ -846,6 +867,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("allow_ids"), py::arg("ctr"), py::arg("temperature"), py::arg("seed"),
         py::arg("out_tok"), py::arg("out_logit") = py::none());
   m.def("sample_dense", &sample_dense);
+  m.def("branch_select", &branch_select);
   m.def("add_inplace", &add_inplace);
   m.def("attn_decode_blocks", &attn_decode_blocks, "grid z of paged_attention_decode for a table width");
   m.def("paged_attention_decode", &paged_attention_decode, py::arg("q"), py::arg("k_cache"),

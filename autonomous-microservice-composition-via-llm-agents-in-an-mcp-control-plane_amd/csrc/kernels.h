@@ -193,6 +193,9 @@ void launch_sample_allowed(const void* hidden, const void* W, const int* allow_p
                            hipStream_t s);
 void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float temperature,
                          unsigned long long seed, int* out_tok, hipStream_t s);
+int launch_branch_select(const int* prev_tok, const int* tab, int n, int* ids, int* slots, int* q_len,
+                         int* ctx_len, int* rows, int* aptr, int aptr_len, int* aids, int* err,
+                         hipStream_t s);
 
 // custom_allreduce.hip (K12): opaque state handle, IPC handles exchanged by the caller
 size_t car_handle_bytes();

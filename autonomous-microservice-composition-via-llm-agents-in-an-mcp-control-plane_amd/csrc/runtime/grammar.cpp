@@ -475,6 +475,23 @@ void register_grammar(py::module_& m) {
       out[i] = py::cast(decs[i].cast<const NativeDecoder&>().allowed());
     return out;
   });
+  // decision lookahead (engine MCP_LOOKAHEAD): every outcome of a decoder's
+  // pending choice, each as (token, the tokens it appends - the token itself
+  // then its jump-forward span -, done, the next choice's allowed tokens, the
+  // decoder state after it).  The engine launches the next forward for all
+  // outcomes at once and the device picks the sampled one.
+  m.def("branches", [](const NativeDecoder& d) {
+    py::list out;
+    for (int tok : d.allowed()) {
+      NativeDecoder c(d);
+      c.feed(tok);
+      std::vector<int> toks = c.advance();
+      const bool fin = c.done();
+      std::vector<int> nxt = fin ? std::vector<int>{} : c.allowed();
+      out.append(py::make_tuple(tok, std::move(toks), fin, std::move(nxt), std::move(c)));
+    }
+    return out;
+  });
   m.def("feed_advance_many", [](const py::list& decs, const std::vector<int>& toks) {
     if ((size_t)py::len(decs) != toks.size()) throw py::value_error("decoders / tokens length");
     py::list out(toks.size());

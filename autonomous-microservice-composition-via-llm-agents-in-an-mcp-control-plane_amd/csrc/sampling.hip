@@ -110,3 +110,84 @@ void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float
   const float inv_t = temperature > 0.f ? 1.f / temperature : 0.f;
   sample_dense_kernel<<<S, 256, 0, s>>>((const bf16*)logits, V, ctr, inv_t, seed, out_tok);
 }
+
+// Decision lookahead (engine MCP_LOOKAHEAD): the next forward was launched
+// before the host read this step's sampled tokens, laid out for every outcome
+// of each sequence's pending choice (engine._launch_branch).  This kernel runs
+// between the step payload's H2D copy and the forward: per sequence it finds
+// the record of the token the previous step sampled and writes that outcome's
+// tokens (the token, then its jump-forward span), the sequence's new-token
+// count and context length, its logit row and the allowed set of the choice
+// after it into the step's device views.  The sequence's rows past the
+// outcome's span get KV slot -1: their K/V are never written (they sit past
+// the context, in the tile the next step's attention masks - a masked key
+// still multiplies its V row by 0, and these rows' values are undefined).
+//   tab[0] = n;  tab[2 + 6 i ..] = {prev_row, q_start, start, Lmax, n_branches, rec_off}
+//   record (4 + Lmax ints) = {token, q_len, allowed_off, allowed_len, ids[Lmax]}
+// One block: n <= 64 sequences, a few hundred ints of output.
+constexpr int BRANCH_MAX_SEQS = 64;
+
+__global__ __launch_bounds__(256) void branch_select_kernel(
+    const int* __restrict__ prev_tok, const int* __restrict__ tab, int* __restrict__ ids,
+    int* __restrict__ slots, int* __restrict__ q_len, int* __restrict__ ctx_len, int* __restrict__ rows,
+    int* __restrict__ aptr, int aptr_len, int* __restrict__ aids, int* __restrict__ err) {
+  __shared__ int s_rec[BRANCH_MAX_SEQS], s_aoff[BRANCH_MAX_SEQS + 1];
+  const int n = tab[0];
+  const int t = threadIdx.x;
+  if (t < n) {
+    const int* h = tab + 2 + 6 * t;
+    const int tok = prev_tok[h[0]];
+    const int L = h[3], nb = h[4];
+    int rec = h[5];
+    int found = -1;
+    for (int b = 0; b < nb; ++b)
+      if (tab[h[5] + b * (4 + L)] == tok) {
+        found = b;
+        break;
+      }
+    if (found < 0) {
+      err[0] = 1 + t;                                  // the host checks it with the tokens
+      found = 0;
+    }
+    rec += found * (4 + L);
+    s_rec[t] = rec;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int i = 0; i < n; ++i) {
+      s_aoff[i] = acc;
+      acc += tab[s_rec[i] + 3];
+    }
+    s_aoff[n] = acc;
+  }
+  __syncthreads();
+  if (t < n) {
+    const int* h = tab + 2 + 6 * t;
+    const int ql = tab[s_rec[t] + 1];
+    q_len[t] = ql;
+    ctx_len[t] = h[2] + ql;
+    rows[t] = h[1] + ql - 1;
+  }
+  for (int i = n + t; i < aptr_len; i += 256) aptr[i] = s_aoff[n];
+  if (t < n) aptr[t] = s_aoff[t];
+  for (int i = 0; i < n; ++i) {
+    const int* h = tab + 2 + 6 * i;
+    const int* rec = tab + s_rec[i];
+    for (int j = t; j < h[3]; j += 256) {
+      ids[h[1] + j] = rec[4 + j];
+      if (j >= rec[1]) slots[h[1] + j] = -1;
+    }
+    for (int j = t; j < rec[3]; j += 256) aids[s_aoff[i] + j] = tab[rec[2] + j];
+  }
+}
+
+int launch_branch_select(const int* prev_tok, const int* tab, int n, int* ids, int* slots, int* q_len,
+                         int* ctx_len, int* rows, int* aptr, int aptr_len, int* aids, int* err,
+                         hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > BRANCH_MAX_SEQS || aptr_len < n + 1) return 1;
+  branch_select_kernel<<<1, 256, 0, s>>>(prev_tok, tab, ids, slots, q_len, ctx_len, rows, aptr, aptr_len,
+                                         aids, err);
+  return 0;
+}

@@ -112,6 +112,12 @@ class _Launch:
     tokens: Optional[torch.Tensor]      # host (pinned) copy of the sampled tokens
     event: Optional[object]             # completion of the D2H copy
     T: int
+    booked: bool = False                # batch_seqs' launched tokens already counted
+    tok_dev: Optional[torch.Tensor] = None   # device sampled tokens (row i = sample i)
+    # decision lookahead (_launch_branch): the sequences in sample-row order and,
+    # per sequence, token -> (token, appended tokens, done, next allowed, decoder)
+    seqs: Optional[list] = None
+    branches: Optional[list] = None
 
 
 # MCP_SPIN_WAIT=1: busy-poll the sampled-token event (one host core per GPU
@@ -119,6 +125,17 @@ class _Launch:
 # Measured no faster (headline 216.6 / 215.6 vs 216.6 / 217.1 plans/s, 40
 # intents/s p50 171.1 vs 170.6 ms, same box): off by default
 _SPIN_WAIT = os.environ.get("MCP_SPIN_WAIT", "0") == "1"
+
+# MCP_LOOKAHEAD=1: decision lookahead for small batches (single intent /
+# low-QPS serving).  The next forward is launched before the host has read
+# this step's sampled tokens: laid out for every outcome of each sequence's
+# pending grammar choice (native decoder clones give each outcome's forced
+# span and next allowed set), the device picks the sampled outcome
+# (csrc/sampling.hip branch_select_kernel) between the step's H2D copy and its
+# forward.  The host's per-decision work (read-back, grammar, schedule, pack,
+# launch) then runs while the GPU is busy with the next step instead of
+# between steps.
+_LOOKAHEAD = os.environ.get("MCP_LOOKAHEAD", "0") == "1"
 
 
 def tp_graph_safe(model) -> bool:
@@ -154,7 +171,7 @@ class LLMEngine:
     def __init__(self, model, num_blocks: Optional[int] = None, kv_budget_bytes: Optional[int] = None,
                  max_batch: int = 256, max_step_tokens: int = 8192, temperature: float = 0.2,
                  seed: int = 0, bcast=None, cascade: bool = True, pipeline: Optional[bool] = None,
-                 graphs: Optional[bool] = None):
+                 graphs: Optional[bool] = None, lookahead: Optional[bool] = None):
         self.model = model
         cfg = model.cfg
         self.device = model.device
@@ -175,10 +192,14 @@ class LLMEngine:
             pipeline = False
         self.pipeline = pipeline
         self.inflight: Dict[int, _Launch] = {}
+        self.lookahead = (_LOOKAHEAD if lookahead is None else bool(lookahead)) and bcast is None
+        self._look: List[_Launch] = []          # [launch whose samples decide, branch launch]
+        self._look_err = None
         self.last_progress = time.perf_counter()   # watched by the planner's stall watchdog
         self._turn = 0
         self._next_cohort = 0
         self.stager = HostStager(self.device)
+        self._look_stager = HostStager(self.device)
         if graphs is None:
             graphs = self.device.type == "cuda" and os.environ.get("MCP_GRAPHS", "1") == "1"
             if graphs and getattr(model, "tp", 1) > 1:
@@ -222,7 +243,8 @@ class LLMEngine:
                                       bcast=bcast)
         self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "graph_cow_steps": 0,
                       "graph_split_steps": 0, "graph_cascade_steps": 0, "kv_split_steps": 0, "preemptions": 0,
-                      "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0}
+                      "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0,
+                      "lookahead_steps": 0}
 
     # ------------------------------------------------------------- prefixes
     def get_prefix(self, tokens: Seq[int]) -> Optional[PrefixEntry]:
@@ -473,10 +495,11 @@ class LLMEngine:
         allocator) and forget the prefix cache: the planner's recovery after a
         stalled step.  Launches still in flight are waited for first.  Returns
         the number of requests failed."""
-        for L in self.inflight.values():
+        for L in list(self.inflight.values()) + self._look:
             if L.event is not None:
                 L.event.synchronize()
         self.inflight.clear()
+        self._look = []
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         n = 0
@@ -510,7 +533,7 @@ class LLMEngine:
         Headline A/B (same box, interleaved): 217.3 / 215.6 plans/s with it,
         215.4 / 219.1 without - within run-to-run noise (the overlap is the
         ~10 ms suffix tokenisation of a 256-intent batch)."""
-        if self.pipeline or self.inflight or self.running or not self.waiting:
+        if self.pipeline or self.inflight or self._look or self.running or not self.waiting:
             return False
         L = self._schedule_launch(None)
         if L is None:
@@ -519,7 +542,7 @@ class LLMEngine:
         return True
 
     def has_work(self) -> bool:
-        return bool(self.running or self.waiting or self.inflight)
+        return bool(self.running or self.waiting or self.inflight or self._look)
 
     # ---------------------------------------------------------------- step
     def _admit(self):
@@ -585,6 +608,8 @@ class LLMEngine:
         Pipelined: cohort c's previous launch is retired (its sampled tokens
         fed to the grammar) while the GPU is still busy with cohort c^1's
         forward, then cohort c is scheduled and launched asynchronously."""
+        if self._look:
+            return self._step_look()
         if not self._pipelined_now() or self._big_step():
             while self.inflight:                  # drain the cohorts before a full-batch step
                 c, L = self.inflight.popitem()
@@ -593,6 +618,9 @@ class LLMEngine:
                 L = self._schedule_launch(None)
             if L is None:
                 return 0
+            if self.lookahead and self._look_start(L):
+                self.last_progress = time.perf_counter()
+                return L.T
             with span("engine.retire"):
                 self._retire(L)
             self.last_progress = time.perf_counter()
@@ -808,10 +836,12 @@ class LLMEngine:
             self.stats["graph_split_steps"] += kv_splits > 1
             self.stats["graph_cascade_steps"] += cascade
             self.stats["samples"] += len(sample_seqs)
-            tokens, event = self._fetch(tok_dev[:len(sample_seqs)])
+            with span("launch.fetch"):
+                tokens, event = self._fetch(tok_dev[:len(sample_seqs)])
         else:
             hidden, dstep = self._launch(host, layout)
-            tokens, event = self._sample(hidden, dstep, len(sample_seqs))
+            tok_dev = self._sample(hidden, dstep, len(sample_seqs))
+            tokens, event = self._fetch(tok_dev) if tok_dev is not None else (None, None)
         self.stats["launch_s"] += time.perf_counter() - t0
         if self.graphs is not None:
             self.stats["graph_captures"] = self.graphs.captures
@@ -819,7 +849,208 @@ class LLMEngine:
         self.stats["tokens"] += T
         self.stats["steps"] += 1
         self.steps += 1
-        return _Launch(batch_seqs, sample_seqs, tokens, event, T)
+        return _Launch(batch_seqs, sample_seqs, tokens, event, T, tok_dev=tok_dev)
+
+    # ------------------------------------------------------ decision lookahead
+    LOOKAHEAD_MAX_SEQS = 8
+
+    def _look_eligible(self, seqs) -> bool:
+        """Every running request is at a pending grammar choice (nothing else
+        to schedule), few of them, native decoders, nothing queued."""
+        if (not seqs or len(seqs) > self.LOOKAHEAD_MAX_SEQS or self.waiting or self.inflight
+                or len(seqs) != len(self.running)):
+            return False
+        fa = _native_feed_advance()
+        if fa is None:
+            return False
+        from . import native
+        if not hasattr(native._RT, "branches"):
+            return False
+        for q in seqs:
+            if (q.is_prefix_job or q.evicted or q.pending or q.done or type(q.decoder) is not fa[1]
+                    or q.decoder.done):
+                return False
+        return True
+
+    def _look_start(self, L: _Launch) -> bool:
+        """After a normal launch whose every sequence samples: count its
+        tokens now and launch the next step over the outcomes of its samples.
+        False: not eligible (the caller retires ``L`` as usual)."""
+        if (L.tok_dev is None or not L.sample_seqs or len(L.sample_seqs) != len(L.batch_seqs)
+                or len(L.sample_seqs) != len(self.running) or self.waiting or self.inflight):
+            return False
+        for q, take in L.batch_seqs:
+            if take != len(q.pending) or q.is_prefix_job:
+                return False
+        for q, take in L.batch_seqs:
+            q.num_cached += take
+            del q.pending[:take]
+        L.booked = True
+        nxt = None
+        if self._look_eligible(L.sample_seqs):
+            with span("engine.launch"):
+                nxt = self._launch_branch(L, list(L.sample_seqs))
+        if nxt is None:
+            with span("engine.retire"):
+                self._retire(L)
+            return True
+        self._look = [L, nxt]
+        return True
+
+    def _launch_branch(self, prev: _Launch, seqs) -> Optional[_Launch]:
+        """Launch the step after ``prev`` for every outcome of the choices
+        ``prev`` samples: sequence s gets 1 + (its longest forced span) token
+        rows at its next positions; the device writes the sampled outcome's
+        tokens, sizes, logit row and next allowed set (ops.branch_select).
+        None when the step does not fit (blocks, context, step budget)."""
+        from . import native
+        t_sched = time.perf_counter()
+        rt = native._RT
+        order = prev.seqs if prev.seqs is not None else prev.sample_seqs
+        row = {id(q): i for i, q in enumerate(order)}
+        max_pos = getattr(self.model.cfg, "max_pos", None)
+        entries, allowed, ctr, per = [], [], [], []
+        T = 0
+        for q in seqs:
+            brs = rt.branches(q.decoder)
+            if any(b[2] for b in brs):
+                # an outcome that ends the plan: a step launched for it would be
+                # wasted GPU work that the next request queues behind (the
+                # plan's last choice runs synchronously)
+                return None
+            Lm = max(len(b[1]) for b in brs)
+            start = q.num_cached
+            if max_pos is not None and start + Lm >= max_pos:
+                return None
+            need = (start + Lm + BLOCK_SIZE - 1) // BLOCK_SIZE - len(q.blocks)
+            if need > 0:
+                if need > self.alloc.num_free:
+                    return None
+                q.blocks += self.alloc.alloc(need)
+            entries.append(([0] * Lm, Lm, start, q.blocks, 0, True))
+            allowed.append([0] * max(1, max(len(b[3]) for b in brs)))
+            ctr.append((q.uid * 4096 + q.n_samples + 1) & 0x7FFFFFFF)
+            per.append((row[id(q)], T, start, Lm, brs))
+            T += Lm
+        if T > self.max_step_tokens:
+            return None
+        # the outcome table: header, per-outcome records, allowed-set pool
+        n = len(seqs)
+        off = 2 + 6 * n
+        tab = [n, 0] + [0] * (6 * n)
+        recs, pool = [], []
+        pool_base = off + sum(len(p[4]) * (4 + p[3]) for p in per)
+        for i, (prow, qs, start, Lm, brs) in enumerate(per):
+            tab[2 + 6 * i: 8 + 6 * i] = [prow, qs, start, Lm, len(brs), off + len(recs)]
+            for tok, ids, _, nxt, _ in brs:
+                recs += [tok, len(ids), pool_base + len(pool), len(nxt)] + list(ids) + [0] * (Lm - len(ids))
+                pool += nxt
+        tab += recs + pool
+        tab[1] = len(tab)
+        group = self.model.cfg.group
+        own_keys = [p[2] + p[3] for p in per]
+        kv_splits = choose_kv_splits([p[3] for p in per], own_keys, group, self.model.hkv,
+                                     hq=self.model.hq) if self.device.type == "cuda" else 1
+        host, layout = pack_step(entries, BLOCK_SIZE, group, [], None, 0, allowed, ctr)
+        own_tiles = -(-max(own_keys) // BLOCK_SIZE)
+        layout = list(layout) + [kv_splits, 0, own_tiles]
+        tab_dev = self._look_stager.to_device(np.asarray(tab, dtype=np.int32))
+        if self._look_err is None:
+            self._look_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        prev_tok, err = prev.tok_dev, self._look_err
+
+        def select(dstep):
+            ops.branch_select(prev_tok, tab_dev, n, dstep, err)
+
+        t0 = time.perf_counter()
+        self.stats["schedule_s"] += t0 - t_sched
+        use_graph = (self.graphs is not None and T <= self.graphs.buckets[-1] and T <= _GRAPH_MAX_T
+                     and self.temperature == self.graphs.temperature)
+        tok_dev = self.graphs.run(step_from_host(host, layout), (), kv_splits, pre=select) \
+            if use_graph else None
+        if tok_dev is not None:
+            self.stats["graph_steps"] += 1
+            self.stats["graph_split_steps"] += kv_splits > 1
+            self.stats["samples"] += n
+            tokens, event = self._fetch(tok_dev[:n])
+        else:
+            hidden, dstep = self._launch(host, layout, pre=select)
+            tok_dev = self._sample(hidden, dstep, n)
+            tokens, event = self._fetch(tok_dev)
+        self.stats["launch_s"] += time.perf_counter() - t0
+        self.stats["tokens"] += T
+        self.stats["steps"] += 1
+        self.stats["lookahead_steps"] += 1
+        self.steps += 1
+        return _Launch([], list(seqs), tokens, event, T, booked=True, tok_dev=tok_dev,
+                       seqs=list(seqs), branches=[{b[0]: b for b in p[4]} for p in per])
+
+    def _wait_tokens(self, L: _Launch) -> list:
+        t1 = time.perf_counter()
+        with span("retire.wait"):
+            if L.event is not None:
+                if _SPIN_WAIT:
+                    while not L.event.query():
+                        pass
+                else:
+                    L.event.synchronize()
+            toks = L.tokens.tolist() if L.tokens is not None else []
+        self.stats["sample_s"] += time.perf_counter() - t1
+        return toks
+
+    def _step_look(self) -> int:
+        """Lookahead steady state: read the older launch's samples, resolve
+        the branch launch's outcome per sequence (adopt that outcome's
+        decoder, count its tokens), then launch the next branch step before
+        the GPU finishes the current one - or leave lookahead, retiring the
+        branch launch the normal way."""
+        old, cur = self._look
+        toks = self._wait_tokens(old)
+        t2 = time.perf_counter()
+        order = old.seqs if old.seqs is not None else old.sample_seqs
+        row = {id(q): i for i, q in enumerate(order)}
+        now = None
+        finished = []
+        with span("retire.update"):
+            for q, brs in zip(cur.seqs, cur.branches):
+                t = toks[row[id(q)]]
+                br = brs.get(t)
+                if br is None:
+                    raise RuntimeError(f"decision lookahead: sampled token {t} is not an outcome "
+                                       f"of the pending choice")
+                tok, ids, fin, _, dec = br
+                if q.t_first is None:
+                    q.t_first = now = now or time.perf_counter()
+                q.n_samples += 1
+                q.decoder = dec
+                q.tokens += ids
+                if fin:
+                    finished.append(q)
+                else:
+                    q.num_cached += len(ids)
+            for q in finished:
+                self._finish(q)             # its blocks' later writers queue after this step
+            if finished:
+                self.running = [s for s in self.running if not s.done]
+        self.stats["update_s"] += time.perf_counter() - t2
+        live = [q for q in cur.seqs if not q.done]
+        nxt = None
+        if live and self._look_eligible(live):
+            with span("engine.launch"):
+                nxt = self._launch_branch(cur, live)
+        if nxt is not None:
+            self._look = [cur, nxt]
+        else:
+            self._look = []
+            ctoks = self._wait_tokens(cur)
+            rows = [i for i, q in enumerate(cur.seqs) if not q.done]
+            seqs = [cur.seqs[i] for i in rows]
+            t3 = time.perf_counter()
+            with span("retire.update"):
+                self._update([(q, 0) for q in seqs], seqs, [ctoks[i] for i in rows], booked=True)
+            self.stats["update_s"] += time.perf_counter() - t3
+        self.last_progress = time.perf_counter()
+        return old.T + 1
 
     def _retire(self, L: _Launch):
         """Wait for a launch's sampled tokens and advance its sequences."""
@@ -841,14 +1072,14 @@ class LLMEngine:
             self.model.comm_check()
         batch_seqs, sample_seqs = L.batch_seqs, L.sample_seqs
         with span("retire.update"):
-            self._update(batch_seqs, sample_seqs, new_tokens)
+            self._update(batch_seqs, sample_seqs, new_tokens, booked=L.booked)
         self.stats["update_s"] += time.perf_counter() - t2
         METRICS.set("batch_occupancy", len(self.running))
         METRICS.set("kv_block_utilization", self.alloc.utilization())
 
-    def _update(self, batch_seqs, sample_seqs, new_tokens):
-        # ---- bookkeeping
-        for seq, take in batch_seqs:
+    def _update(self, batch_seqs, sample_seqs, new_tokens, booked: bool = False):
+        # ---- bookkeeping (a lookahead launch counted its tokens at launch)
+        for seq, take in ([] if booked else batch_seqs):
             seq.num_cached += take
             del seq.pending[:take]
             if seq.is_prefix_job and not seq.pending:
@@ -883,13 +1114,16 @@ class LLMEngine:
                 self._finish(seq)
         self.running = [s for s in self.running if not s.done]
 
-    def _launch(self, host, layout):
-        """(packed step) -> (broadcast to TP workers) -> H2D -> KV copies -> forward."""
+    def _launch(self, host, layout, pre=None):
+        """(packed step) -> (broadcast to TP workers) -> H2D -> KV copies ->
+        (``pre``: the lookahead's outcome selection) -> forward."""
         with span("launch.h2d"):
             payload = self.stager.to_device(host)
         if self.bcast is not None:
             self.bcast.send(payload, layout)
         dstep, csrc, cdst = views(payload, layout)
+        if pre is not None:
+            pre(dstep)
         if csrc.numel():
             ops.copy_blocks(self.kv.data, csrc, cdst)
         if dstep.token_ids.numel() == 0:
@@ -901,17 +1135,17 @@ class LLMEngine:
         if self.bcast is not None:
             self.bcast.stop()
 
-    def _sample(self, hidden: torch.Tensor, dstep, n: int):
+    def _sample(self, hidden: torch.Tensor, dstep, n: int) -> Optional[torch.Tensor]:
         """Fused LM-head-rows + grammar mask + Gumbel-max sampling (K9) on the
         allowed sets that travelled with the step descriptor.  The RNG counter
         (request uid, sample index) makes every draw unique, so the seed is
         constant (the same kernel runs inside captured hipGraphs)."""
         if n == 0:
-            return None, None
+            return None
         tok = ops.sample_allowed(hidden, self.model.w.lm_head, dstep.allow_ptr, dstep.allow_ids,
                                  dstep.sample_ctr, self.temperature, self.seed)
         self.stats["samples"] += n
-        return self._fetch(tok)
+        return tok
 
     @staticmethod
     def _fetch(tok: torch.Tensor):
@@ -938,7 +1172,7 @@ class LLMEngine:
     def run(self, max_steps: int = 1_000_000):
         n = idle = 0
         while self.has_work() and n < max_steps:
-            if self.step() == 0 and not self.inflight:
+            if self.step() == 0 and not self.inflight and not self._look:
                 if not self.waiting:
                     # nothing runnable: sequences blocked on nothing -> bug guard
                     stuck = [s for s in self.running if not s.pending]

@@ -45,6 +45,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.tracing import span
 from .batch import BLOCK_SIZE, HostStager, StepInputs, build_work, tokens_per_item, views
 
 # token buckets: every 64 rows above 64 (the GEMM tile plan's M granularity,
@@ -94,6 +95,7 @@ class GraphRunner:
         self._pool = None
         self.stager = HostStager(self.device)
         self.replays = 0
+        self.replay_host_s = 0.0     # host time inside CUDAGraph.replay()
         self.captures = 0
         self.capture_s = 0.0
         self.warmed = False     # warm() ran: split keys are no longer captured lazily
@@ -318,11 +320,14 @@ class GraphRunner:
         self.warmed = True
         return self.captures - n0
 
-    def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1) -> Optional[torch.Tensor]:
+    def run(self, step: StepInputs, copies: Sequence = (), kv_splits: int = 1,
+            pre=None) -> Optional[torch.Tensor]:
         """Replays the graph for ``step`` (after the prefix copy-on-write
         ``copies``); returns the device tensor of sampled tokens (first
         ``len(step.logit_rows)`` entries valid), or None when the step does
-        not fit a bucket (the caller runs it eagerly)."""
+        not fit a bucket (the caller runs it eagerly).  ``pre(dstep)`` runs on
+        the bucket's views between the payload copy and the replay (the
+        engine's decision lookahead)."""
         bs = self.bucket_for(step, len(copies))
         if bs is None:
             return None
@@ -330,7 +335,8 @@ class GraphRunner:
         w = self.width_for(int(step.block_table.shape[1]))
         if w is None:
             return None
-        host = self.pack_static(step, b, w, copies, sb)
+        with span("graph.pack"):
+            host = self.pack_static(step, b, w, copies, sb)
         if host is None:
             return None
         casc = int(step.pre_tokens > 0 and step.pre_bt is not None and len(step.pre_bt) > 0)
@@ -338,11 +344,19 @@ class GraphRunner:
         if kv_splits > 1 and self.warmed and key not in self._b:
             return None        # an uncommon split key: eager, never a lazy capture mid-serving
         if self.bcast is not None:
+            if pre is not None:
+                return None
             e = self._launch_tp(key, host)
         else:
             e = self._get(key)
-            self.stager.to_device(host, out=e.buf)
-            e.graph.replay()
+            with span("graph.h2d"):
+                self.stager.to_device(host, out=e.buf)
+            if pre is not None:
+                pre(e.dstep)
+            t0 = time.perf_counter()
+            with span("graph.replay"):
+                e.graph.replay()
+            self.replay_host_s += time.perf_counter() - t0
         self.replays += 1
         return e.tokens
 

@@ -479,6 +479,37 @@ def sample_allowed(hidden, W, allow_ptr, allow_ids, ctr, temperature, seed, out_
     return t if out_tok is None else out_tok.copy_(t)
 
 
+def branch_select(prev_tok, tab, n: int, dstep, err):
+    """Decision lookahead: write the sampled outcome of each sequence's
+    pending choice into ``dstep``'s views (tokens, q_len, ctx_len, logit row,
+    allowed set; the rows past the outcome's span lose their KV slot) -
+    csrc/sampling.hip ``branch_select_kernel``; ``tab`` is the
+    int32 table of engine._launch_branch, already bounded on the host."""
+    a = dstep.attn
+    if prev_tok.is_cuda:
+        lib().branch_select(prev_tok, tab, int(n), dstep.token_ids, dstep.slots, a.q_len, a.ctx_len,
+                            dstep.logit_rows, dstep.allow_ptr, dstep.allow_ids, err)
+        return
+    t = tab.tolist()
+    off, chosen = 0, []
+    for i in range(n):
+        prev, qs, start, L, nb, rec = t[2 + 6 * i: 8 + 6 * i]
+        tok = int(prev_tok[prev])
+        b = next((b for b in range(nb) if t[rec + b * (4 + L)] == tok), None)
+        if b is None:
+            err[0] = 1 + i
+            b = 0
+        r = rec + b * (4 + L)
+        ql, aoff, alen = t[r + 1], t[r + 2], t[r + 3]
+        a.q_len[i], a.ctx_len[i], dstep.logit_rows[i] = ql, start + ql, qs + ql - 1
+        dstep.token_ids[qs:qs + L] = torch.tensor(t[r + 4:r + 4 + L], dtype=torch.int32)
+        dstep.slots[qs + ql:qs + L] = -1
+        dstep.allow_ptr[i] = off
+        dstep.allow_ids[off:off + alen] = torch.tensor(t[aoff:aoff + alen], dtype=torch.int32)
+        off += alen
+    dstep.allow_ptr[n:] = off
+
+
 def add_inplace(y, x):
     if y.is_cuda:
         lib().add_inplace(y, x)

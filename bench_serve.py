@@ -262,7 +262,12 @@ def main():
                    p50_warm_prefix_ms=round(statistics.median(warm) * 1e3, 2),
                    p90_warm_prefix_ms=round(pct(warm, 90) * 1e3, 2),
                    p50_cold_prefix_ms=round(statistics.median(cold) * 1e3, 2),
-                   graph_steps=engine.stats["graph_steps"], steps=engine.stats["steps"])
+                   graph_steps=engine.stats["graph_steps"], steps=engine.stats["steps"],
+                   host_us_per_step={k: round(1e6 * engine.stats[k] / max(1, engine.stats["steps"]), 1)
+                                     for k in ("schedule_s", "launch_s", "sample_s", "update_s")},
+                   replay_host_us_per_graph_step=round(
+                       1e6 * engine.graphs.replay_host_s / max(1, engine.graphs.replays), 1)
+                   if engine.graphs is not None else None)
     else:
         if world > 1:
             dist.barrier()

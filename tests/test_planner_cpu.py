@@ -239,6 +239,38 @@ def test_pipelined_engine_matches_synchronous():
     assert out[0] == out[1]
 
 
+@pytest.mark.parametrize("temperature", [0.0, 0.2])
+def test_lookahead_engine_matches_synchronous(temperature, monkeypatch):
+    """Decision lookahead (the next step launched over every outcome of the
+    pending choices, the sampled outcome picked on the device side by
+    ops.branch_select) produces the same plans as the synchronous engine, one
+    intent at a time and several at once; every KV block comes back."""
+    from mcp_amd.engine import native
+    if not native.available():
+        pytest.skip("native runtime not built")
+    reg = MemoryRegistry(synthetic_registry(7, seed=4))
+    intents = [synthetic_intent(i) for i in range(4)]
+    out, stats = [], []
+    import itertools
+    from mcp_amd.engine import engine as engine_mod
+    for look in (False, True):
+        torch.manual_seed(0)
+        # the sampling counter is (request uid, sample index): same uids in both runs
+        monkeypatch.setattr(engine_mod, "_uid", itertools.count(1))
+        model = LlamaModel.random("tiny", "cpu", seed=1)
+        eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=temperature,
+                        lookahead=look)
+        planner = LocalPlanner(eng, reg, max_nodes=4, min_nodes=2)
+        res = [planner.plan_many([it])[0] for it in intents[:2]]
+        res += planner.plan_many(intents)
+        out.append(res)
+        stats.append(dict(eng.stats))
+        assert eng.alloc.num_free == eng.kv.num_blocks and not eng._look and not eng.inflight
+    assert out[0] == out[1]
+    assert stats[0]["lookahead_steps"] == 0 and stats[1]["lookahead_steps"] > 0
+    assert stats[0]["samples"] == stats[1]["samples"]
+
+
 def test_graph_static_layout_matches_dynamic():
     """The fixed per-bucket layout used by captured hipGraphs (padding tokens,
     empty dummy sequences, padded work lists and allowed sets) computes the same
