@@ -122,8 +122,12 @@ void launch_sample_dense(const void* logits, int S, int V, const int* ctr, float
 // outcome's span get KV slot -1: their K/V are never written (they sit past
 // the context, in the tile the next step's attention masks - a masked key
 // still multiplies its V row by 0, and these rows' values are undefined).
-//   tab[0] = n;  tab[2 + 6 i ..] = {prev_row, q_start, start, Lmax, n_branches, rec_off}
+//   tab[0] = n;  tab[1] = offset of the tail section (0: none);
+//   tab[2 + 6 i ..] = {prev_row, q_start, start, Lmax, n_branches, rec_off}
 //   record (4 + Lmax ints) = {token, q_len, allowed_off, allowed_len, ids[Lmax]}
+//   tail = {nt, rel[nt + 1], pool[rel[nt]]}: the allowed sets of nt sampled
+//   rows after the n lookahead rows (requests admitted into the step, their
+//   tokens known), placed after the n rows' chosen sets
 // One block: n <= 64 sequences, a few hundred ints of output.
 constexpr int BRANCH_MAX_SEQS = 64;
 
@@ -169,8 +173,16 @@ __global__ __launch_bounds__(256) void branch_select_kernel(
     ctx_len[t] = h[2] + ql;
     rows[t] = h[1] + ql - 1;
   }
-  for (int i = n + t; i < aptr_len; i += 256) aptr[i] = s_aoff[n];
+  const int tail = tab[1];
+  const int nt = tail ? tab[tail] : 0;
+  const int total = s_aoff[n];
+  for (int i = n + t; i < aptr_len; i += 256)
+    aptr[i] = total + (tail ? tab[tail + 1 + min(i - n, nt)] : 0);
   if (t < n) aptr[t] = s_aoff[t];
+  if (tail) {
+    const int tl = tab[tail + 1 + nt];
+    for (int j = t; j < tl; j += 256) aids[total + j] = tab[tail + 2 + nt + j];
+  }
   for (int i = 0; i < n; ++i) {
     const int* h = tab + 2 + 6 * i;
     const int* rec = tab + s_rec[i];

@@ -244,7 +244,7 @@ class LLMEngine:
         self.stats = {"tokens": 0, "samples": 0, "steps": 0, "graph_steps": 0, "graph_cow_steps": 0,
                       "graph_split_steps": 0, "graph_cascade_steps": 0, "kv_split_steps": 0, "preemptions": 0,
                       "schedule_s": 0.0, "launch_s": 0.0, "sample_s": 0.0, "update_s": 0.0,
-                      "lookahead_steps": 0}
+                      "lookahead_steps": 0, "lookahead_admitted": 0}
 
     # ------------------------------------------------------------- prefixes
     def get_prefix(self, tokens: Seq[int]) -> Optional[PrefixEntry]:
@@ -853,12 +853,16 @@ class LLMEngine:
 
     # ------------------------------------------------------ decision lookahead
     LOOKAHEAD_MAX_SEQS = 8
+    # queued requests join a lookahead step instead of ending lookahead (an
+    # arrival would otherwise wait behind the step already queued)
+    LOOKAHEAD_ADMIT = os.environ.get("MCP_LOOKAHEAD_ADMIT", "1") == "1"
 
-    def _look_eligible(self, seqs) -> bool:
+    def _look_eligible(self, seqs, allow_waiting: bool = False) -> bool:
         """Every running request is at a pending grammar choice (nothing else
-        to schedule), few of them, native decoders, nothing queued."""
-        if (not seqs or len(seqs) > self.LOOKAHEAD_MAX_SEQS or self.waiting or self.inflight
-                or len(seqs) != len(self.running)):
+        to schedule), few of them, native decoders, nothing queued (or, with
+        ``allow_waiting``, queued requests the next step admits)."""
+        if (not seqs or len(seqs) > self.LOOKAHEAD_MAX_SEQS or (self.waiting and not allow_waiting)
+                or self.inflight or len(seqs) != len(self.running)):
             return False
         fa = _native_feed_advance()
         if fa is None:
@@ -897,12 +901,22 @@ class LLMEngine:
         self._look = [L, nxt]
         return True
 
-    def _launch_branch(self, prev: _Launch, seqs) -> Optional[_Launch]:
+    def _launch_branch(self, prev: _Launch, seqs, admit: bool = False) -> Optional[_Launch]:
         """Launch the step after ``prev`` for every outcome of the choices
         ``prev`` samples: sequence s gets 1 + (its longest forced span) token
         rows at its next positions; the device writes the sampled outcome's
         tokens, sizes, logit row and next allowed set (ops.branch_select).
-        None when the step does not fit (blocks, context, step budget)."""
+        ``admit``: queued requests join the step with their known tokens
+        (prompt suffix / prefix job) after the lookahead rows.  None when the
+        step does not fit (blocks, context, step budget)."""
+        try:
+            return self._launch_branch_inner(prev, seqs, admit)
+        finally:
+            if self._deferred_free:            # the step's copy list is queued on the stream
+                self.alloc.free(self._deferred_free)
+                self._deferred_free = []
+
+    def _launch_branch_inner(self, prev: _Launch, seqs, admit: bool) -> Optional[_Launch]:
         from . import native
         t_sched = time.perf_counter()
         rt = native._RT
@@ -934,7 +948,41 @@ class LLMEngine:
             T += Lm
         if T > self.max_step_tokens:
             return None
-        # the outcome table: header, per-outcome records, allowed-set pool
+        # admitted requests: their known tokens after the lookahead rows (no
+        # cascade, no memory-pressure path: a request that does not fit waits)
+        copies, explicit, tail_sets = [], [], []
+        if admit and self.waiting:
+            self._admit()
+            ids_look = {id(q) for q in seqs}
+            fa = _native_feed_advance()
+            for seq in self.running:
+                if id(seq) in ids_look:
+                    continue
+                if not seq.materialized and not seq.is_prefix_job and seq.prefix is not None \
+                        and seq.prefix.computed and self.alloc.num_free > 1:
+                    self._materialize(seq, copies)
+                if not (seq.materialized or seq.is_prefix_job) or seq.evicted or not seq.pending:
+                    continue
+                take = min(len(seq.pending), self.max_step_tokens - T)
+                if take <= 0:
+                    break
+                start = seq.num_cached
+                need = (start + take + BLOCK_SIZE - 1) // BLOCK_SIZE - len(seq.blocks)
+                if need > 0:
+                    if need >= self.alloc.num_free:
+                        continue
+                    seq.blocks += self.alloc.alloc(need)
+                dec = seq.decoder
+                sample = take == len(seq.pending) and dec is not None and not dec.done
+                entries.append((seq.pending, take, start, seq.blocks, 0, sample))
+                explicit.append((seq, take, sample))
+                if sample:
+                    a = fa[2]([dec])[0] if fa is not None and type(dec) is fa[1] else dec.allowed()
+                    allowed.append(list(a))
+                    tail_sets.append(list(a))
+                    ctr.append((seq.uid * 4096 + seq.n_samples) & 0x7FFFFFFF)
+                T += take
+        # the outcome table: header, per-outcome records, allowed-set pool, tail
         n = len(seqs)
         off = 2 + 6 * n
         tab = [n, 0] + [0] * (6 * n)
@@ -946,12 +994,18 @@ class LLMEngine:
                 recs += [tok, len(ids), pool_base + len(pool), len(nxt)] + list(ids) + [0] * (Lm - len(ids))
                 pool += nxt
         tab += recs + pool
-        tab[1] = len(tab)
+        if tail_sets:
+            tab[1] = len(tab)
+            rel = [0]
+            for a in tail_sets:
+                rel.append(rel[-1] + len(a))
+            tab += [len(tail_sets)] + rel + [x for a in tail_sets for x in a]
         group = self.model.cfg.group
-        own_keys = [p[2] + p[3] for p in per]
-        kv_splits = choose_kv_splits([p[3] for p in per], own_keys, group, self.model.hkv,
+        own_keys = [p[2] + p[3] for p in per] + [seq.num_cached + take for seq, take, _ in explicit]
+        q_lens = [p[3] for p in per] + [take for _, take, _ in explicit]
+        kv_splits = choose_kv_splits(q_lens, own_keys, group, self.model.hkv,
                                      hq=self.model.hq) if self.device.type == "cuda" else 1
-        host, layout = pack_step(entries, BLOCK_SIZE, group, [], None, 0, allowed, ctr)
+        host, layout = pack_step(entries, BLOCK_SIZE, group, copies, None, 0, allowed, ctr)
         own_tiles = -(-max(own_keys) // BLOCK_SIZE)
         layout = list(layout) + [kv_splits, 0, own_tiles]
         tab_dev = self._look_stager.to_device(np.asarray(tab, dtype=np.int32))
@@ -966,24 +1020,38 @@ class LLMEngine:
         self.stats["schedule_s"] += t0 - t_sched
         use_graph = (self.graphs is not None and T <= self.graphs.buckets[-1] and T <= _GRAPH_MAX_T
                      and self.temperature == self.graphs.temperature)
-        tok_dev = self.graphs.run(step_from_host(host, layout), (), kv_splits, pre=select) \
+        tok_dev = self.graphs.run(step_from_host(host, layout), copies, kv_splits, pre=select) \
             if use_graph else None
+        R = n + len(tail_sets)
         if tok_dev is not None:
             self.stats["graph_steps"] += 1
+            self.stats["graph_cow_steps"] += bool(copies)
             self.stats["graph_split_steps"] += kv_splits > 1
-            self.stats["samples"] += n
-            tokens, event = self._fetch(tok_dev[:n])
+            self.stats["samples"] += R
+            tokens, event = self._fetch(tok_dev[:R])
         else:
             hidden, dstep = self._launch(host, layout, pre=select)
-            tok_dev = self._sample(hidden, dstep, n)
+            tok_dev = self._sample(hidden, dstep, R)
             tokens, event = self._fetch(tok_dev)
+        # the admitted requests' tokens are counted now (a prefix job whose
+        # tokens are all queued is complete for every later step)
+        for seq, take, _ in explicit:
+            seq.num_cached += take
+            del seq.pending[:take]
+            if seq.is_prefix_job and not seq.pending:
+                self._finish(seq)
+        if any(q.done for q, _, _ in explicit):
+            self.running = [s for s in self.running if not s.done]
+        smp = [q for q, _, sm in explicit if sm]
+        self.stats["lookahead_admitted"] += len(explicit)
         self.stats["launch_s"] += time.perf_counter() - t0
         self.stats["tokens"] += T
         self.stats["steps"] += 1
         self.stats["lookahead_steps"] += 1
         self.steps += 1
-        return _Launch([], list(seqs), tokens, event, T, booked=True, tok_dev=tok_dev,
-                       seqs=list(seqs), branches=[{b[0]: b for b in p[4]} for p in per])
+        return _Launch([], list(seqs) + smp, tokens, event, T, booked=True, tok_dev=tok_dev,
+                       seqs=list(seqs) + smp,
+                       branches=[{b[0]: b for b in p[4]} for p in per] + [None] * len(smp))
 
     def _wait_tokens(self, L: _Launch) -> list:
         t1 = time.perf_counter()
@@ -1013,6 +1081,8 @@ class LLMEngine:
         finished = []
         with span("retire.update"):
             for q, brs in zip(cur.seqs, cur.branches):
+                if brs is None:               # admitted with known tokens (counted at launch)
+                    continue
                 t = toks[row[id(q)]]
                 br = brs.get(t)
                 if br is None:
@@ -1035,9 +1105,9 @@ class LLMEngine:
         self.stats["update_s"] += time.perf_counter() - t2
         live = [q for q in cur.seqs if not q.done]
         nxt = None
-        if live and self._look_eligible(live):
+        if live and self._look_eligible(live, allow_waiting=self.LOOKAHEAD_ADMIT):
             with span("engine.launch"):
-                nxt = self._launch_branch(cur, live)
+                nxt = self._launch_branch(cur, live, admit=self.LOOKAHEAD_ADMIT)
         if nxt is not None:
             self._look = [cur, nxt]
         else:

@@ -507,7 +507,16 @@ def branch_select(prev_tok, tab, n: int, dstep, err):
         dstep.allow_ptr[i] = off
         dstep.allow_ids[off:off + alen] = torch.tensor(t[aoff:aoff + alen], dtype=torch.int32)
         off += alen
-    dstep.allow_ptr[n:] = off
+    tail = t[1]
+    if not tail:
+        dstep.allow_ptr[n:] = off
+        return
+    nt = t[tail]
+    rel = t[tail + 1: tail + 2 + nt]
+    for i in range(n, dstep.allow_ptr.numel()):
+        dstep.allow_ptr[i] = off + rel[min(i - n, nt)]
+    dstep.allow_ids[off:off + rel[nt]] = torch.tensor(t[tail + 2 + nt: tail + 2 + nt + rel[nt]],
+                                                      dtype=torch.int32)
 
 
 def add_inplace(y, x):

@@ -46,8 +46,18 @@ def _table(rng, n, T_cap):
             recs += [t, len(ids), base + len(pool), len(nxt)] + ids + [0] * (L - len(ids))
             pool += nxt
     tab += recs + pool
-    tab[1] = len(tab)
     return tab, per
+
+
+def _with_tail(tab, tail_sets):
+    """Append the tail section: allowed sets of rows after the lookahead rows."""
+    tab = list(tab)
+    tab[1] = len(tab)
+    rel = [0]
+    for a in tail_sets:
+        rel.append(rel[-1] + len(a))
+    tab += [len(tail_sets)] + rel + [x for a in tail_sets for x in a]
+    return tab
 
 
 def _step(dev, T, S, A):
@@ -57,11 +67,14 @@ def _step(dev, T, S, A):
                       allow_ptr=z(S + 1), allow_ids=z(A), sample_ctr=z(S))
 
 
-@pytest.mark.parametrize("n", [1, 3, 8])
-def test_branch_select_kernel_matches_host(n):
+@pytest.mark.parametrize("n,tail", [(1, 0), (3, 0), (8, 0), (2, 3)])
+def test_branch_select_kernel_matches_host(n, tail):
     import numpy as np
     rng = np.random.default_rng(n)
     tab, per = _table(rng, n, 128)
+    tail_sets = [rng.integers(0, 1000, size=int(rng.integers(1, 5))).tolist() for _ in range(tail)]
+    if tail:
+        tab = _with_tail(tab, tail_sets)
     prev = torch.tensor([p[4][int(rng.integers(0, len(p[4])))][0] for p in per], dtype=torch.int32)
     outs = []
     for dev in ("cpu", "cuda"):
@@ -84,6 +97,9 @@ def test_branch_select_kernel_matches_host(n):
         assert outs[1][6][q0 + len(ids):q0 + L].tolist() == [-1] * (L - len(ids))
         a0, a1 = int(outs[1][4][i]), int(outs[1][4][i + 1])
         assert outs[1][5][a0:a1].tolist() == nxt
+    for j, a in enumerate(tail_sets):               # tail rows follow the chosen sets
+        a0, a1 = int(outs[1][4][n + j]), int(outs[1][4][n + j + 1])
+        assert outs[1][5][a0:a1].tolist() == a
 
 
 @pytest.mark.parametrize("graphs,temperature", [(False, 0.0), (True, 0.0), (True, 0.2)])
@@ -110,3 +126,32 @@ def test_lookahead_engine_matches_synchronous(graphs, temperature, monkeypatch):
     names = [s.name for s in reg.list_services()]
     for d in out[1]:
         validate_dag(d, names)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_lookahead_admits_arrivals_matches_synchronous(graphs, monkeypatch):
+    """Requests arriving during lookahead join the next lookahead step; the
+    plans equal the synchronous engine's under the same arrival schedule."""
+    model = LlamaModel.random("tiny", "cuda", seed=3)
+    reg = MemoryRegistry(synthetic_registry(8, seed=2))
+    out, admitted = [], []
+    for look in (False, True):
+        monkeypatch.setattr(engine_mod, "_uid", itertools.count(1))
+        eng = LLMEngine(model, num_blocks=512, max_batch=32, temperature=0.2, graphs=graphs,
+                        pipeline=False, lookahead=look)
+        planner = LocalPlanner(eng, reg, max_nodes=4, min_nodes=2)
+        planner.plan_many([synthetic_intent(99)])
+        seqs = []
+        for i in range(4):
+            dec, ptoks, stoks = planner.prepare(synthetic_intent(i))
+            seqs.append(eng.submit(dec, stoks, prefix_tokens=ptoks))
+            for _ in range(3 + i):
+                if eng.has_work():
+                    eng.step()
+        eng.run()
+        torch.cuda.synchronize()
+        assert all(q.error is None for q in seqs) and not eng._look
+        out.append([q.result for q in seqs])
+        admitted.append(eng.stats["lookahead_admitted"])
+    assert out[0] == out[1]
+    assert admitted[1] > 0

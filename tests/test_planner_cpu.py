@@ -271,6 +271,45 @@ def test_lookahead_engine_matches_synchronous(temperature, monkeypatch):
     assert stats[0]["samples"] == stats[1]["samples"]
 
 
+@pytest.mark.parametrize("temperature", [0.0, 0.2])
+def test_lookahead_admits_arrivals_and_matches_synchronous(temperature, monkeypatch):
+    """Requests arriving while the engine is in decision lookahead join the
+    next lookahead step (their prompt tokens after the lookahead rows,
+    MCP_LOOKAHEAD_ADMIT) and every plan equals the synchronous engine's under
+    the same arrival schedule."""
+    from mcp_amd.engine import native
+    if not native.available():
+        pytest.skip("native runtime not built")
+    import itertools
+    from mcp_amd.engine import engine as engine_mod
+    reg = MemoryRegistry(synthetic_registry(7, seed=4))
+    out, stats = [], []
+    for look in (False, True):
+        torch.manual_seed(0)
+        monkeypatch.setattr(engine_mod, "_uid", itertools.count(1))
+        model = LlamaModel.random("tiny", "cpu", seed=1)
+        eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=temperature,
+                        lookahead=look)
+        planner = LocalPlanner(eng, reg, max_nodes=4, min_nodes=2)
+        planner.plan_many([synthetic_intent(99)])           # the registry prefix is computed
+        seqs, k = [], 0
+        for i in range(4):
+            dec, ptoks, stoks = planner.prepare(synthetic_intent(i))
+            seqs.append(eng.submit(dec, stoks, prefix_tokens=ptoks))
+            for _ in range(3 + i):                          # arrivals mid-decode
+                if eng.has_work():
+                    eng.step()
+                    k += bool(eng._look)
+        eng.run()
+        out.append([q.result for q in seqs])
+        stats.append((dict(eng.stats), k))
+        assert all(q.error is None for q in seqs)
+        assert not eng._look and not eng.running
+    assert out[0] == out[1]
+    assert stats[1][0]["lookahead_steps"] > 0 and stats[1][1] > 0
+    assert stats[1][0]["lookahead_admitted"] > 0, stats[1][0]
+
+
 def test_graph_static_layout_matches_dynamic():
     """The fixed per-bucket layout used by captured hipGraphs (padding tokens,
     empty dummy sequences, padded work lists and allowed sets) computes the same
