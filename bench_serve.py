@@ -165,11 +165,16 @@ def run_via_api(args):
                 lat.append(time.perf_counter() - (t_start + arrivals[i]))
             tasks = []
             t_start = time.perf_counter()
+            next_log = 30.0            # a progress line every 30 s (long soak runs stay visibly alive)
             for i in range(n):
                 delay = t_start + arrivals[i] - time.perf_counter()
                 if delay > 0:
                     await asyncio.sleep(delay)
                 tasks.append(asyncio.create_task(one(i)))
+                if time.perf_counter() - t_start >= next_log:
+                    log(f"[via-api qps {qps}] {next_log:.0f} s: {i + 1} of {n} sent, "
+                        f"{len(lat)} done, {len(errs)} errors")
+                    next_log += 30.0
             await asyncio.gather(*tasks)
             elapsed = time.perf_counter() - t_start
             metrics = (await c.get("/metrics")).text
