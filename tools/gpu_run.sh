@@ -78,8 +78,12 @@ run_prof() {
 run_pmc() {
   local counters=$1
   shift
-  timeout -s KILL 120 rocprofv3 --pmc $counters -f rocpd -d "$O/pmc_$STEP" -o run -- "$@" \
+  # the database stays on the box (a counter pass over a serving run exceeds
+  # the 64 MiB copied back); the per-kernel summary comes back
+  timeout -s KILL 120 rocprofv3 --pmc $counters -f rocpd -d "/tmp/pmc_$STEP" -o run -- "$@" \
     > "$O/pmc_$STEP.log" 2>&1 || fail "pmc pass" "$O/pmc_$STEP.log"
+  python tools/pmc_summary.py --by-kernel "$(find /tmp/pmc_$STEP -name '*.db' | head -1)" \
+    > "$O/pmc_$STEP.md" 2>&1 || fail "pmc summary" "$O/pmc_$STEP.md"
   echo "pmc pass $STEP done"
 }
 
