@@ -881,6 +881,7 @@ class LLMEngine:
         tokens now and launch the next step over the outcomes of its samples.
         False: not eligible (the caller retires ``L`` as usual)."""
         if (L.tok_dev is None or not L.sample_seqs or len(L.sample_seqs) != len(L.batch_seqs)
+                or len(L.sample_seqs) > self.LOOKAHEAD_MAX_SEQS
                 or len(L.sample_seqs) != len(self.running) or self.waiting or self.inflight):
             return False
         for q, take in L.batch_seqs:
