@@ -28,6 +28,7 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
+import os
 import time
 from email.utils import formatdate
 from typing import Optional
@@ -67,7 +68,10 @@ def _head(status: int, headers, keep_alive: bool) -> bytes:
 
 
 class _Request:
-    __slots__ = ("method", "target", "version", "headers", "body", "keep_alive")
+    __slots__ = ("method", "target", "version", "headers", "body", "keep_alive", "error")
+
+
+MAX_CHUNK_LINE = 4096                # a chunk-size line (hex size + extensions)
 
 
 class FastHTTP(asyncio.Protocol):
@@ -80,13 +84,26 @@ class FastHTTP(asyncio.Protocol):
         self.closing = False
         self.continued = False                 # 100 Continue sent for the request being read
         self.paused = False                    # reading paused: MAX_PIPELINED requests queued
+        # the request whose head is parsed and whose body is still arriving:
+        # Content-Length bytes outstanding, or the chunked decoder's state
+        # (the decoded body so far, bytes left of the current chunk + CRLF,
+        # in the trailer section) - kept across data_received calls, so every
+        # byte is decoded once
+        self.cur: Optional[_Request] = None
+        self.clen = 0
+        self.chunked = False
+        self.body = bytearray()
+        self.chunk_left = -1                   # -1: a chunk-size line is next
+        self.trailers = False
 
     # ------------------------------------------------------------ transport
     def connection_made(self, transport):
         self.transport = transport
         self.queue = asyncio.Queue()
-        self.worker = asyncio.get_running_loop().create_task(self._serve())
+        self.loop = asyncio.get_running_loop()
+        self.worker = self.loop.create_task(self._serve())
         self.srv.conns.add(self)
+        self.srv.accepted += 1
 
     def connection_lost(self, exc):
         self.closing = True
@@ -100,7 +117,10 @@ class FastHTTP(asyncio.Protocol):
             req = self._parse()
             if req is None:
                 break
-            self.queue.put_nowait(req)
+            # pipelined requests run concurrently (each its own task, so a
+            # client that pipelines over few connections still fills every
+            # replica); their answers are written strictly in request order
+            self.queue.put_nowait((req, self.loop.create_task(self.srv.handle_safe(req))))
             if self.queue.qsize() >= MAX_PIPELINED and not self.paused:
                 # a client pipelining faster than it reads its answers: stop
                 # reading until the queue drains (flow control, bounded memory)
@@ -109,123 +129,195 @@ class FastHTTP(asyncio.Protocol):
 
     # -------------------------------------------------------------- parsing
     def _parse(self) -> Optional[_Request]:
+        if self.cur is None and not self._parse_head():
+            return None
+        body = self._chunked_body() if self.chunked else self._length_body()
+        if body is None:
+            return None
+        req, self.cur = self.cur, None
+        req.body = body
+        self.continued = False
+        return req
+
+    def _parse_head(self) -> bool:
         buf = self.buf
         end = buf.find(b"\r\n\r\n")
         if end < 0:
             if len(buf) > MAX_HEADER:
                 self._fail(400)
-            return None
+            return False
         lines = bytes(buf[:end]).split(b"\r\n")
         parts = lines[0].split(b" ")
         if len(parts) != 3 or not parts[2].startswith(b"HTTP/1."):
             self._fail(400)
-            return None
+            return False
         req = _Request()
+        req.error = None
         req.method, req.target, req.version = parts[0].decode("latin-1"), parts[1], parts[2]
         headers = []
-        clen = 0
-        chunked = False
+        clen = None
+        te = None
         conn = b""
         expect = False
         for ln in lines[1:]:
             k, sep, v = ln.partition(b":")
             if not sep:
                 self._fail(400)
-                return None
+                return False
             k = k.strip().lower()
             v = v.strip()
             headers.append((k, v))
             if k == b"content-length":
-                # digits only: int() would take "-5", "+5" or " 5_0"
-                if not v.isdigit():
+                # digits only: int() would take "-5", "+5" or " 5_0"; repeated
+                # headers must agree (RFC 7230 3.3.2)
+                if not v.isdigit() or (clen is not None and int(v) != clen):
                     self._fail(400)
-                    return None
+                    return False
                 clen = int(v)
             elif k == b"transfer-encoding":
-                chunked = b"chunked" in v.lower()
+                te = v.lower() if te is None else te + b"," + v.lower()
             elif k == b"connection":
                 conn = v.lower()
             elif k == b"expect":
                 expect = v.lower() == b"100-continue"
+        chunked = False
+        if te is not None:
+            # a message with both framings is a request-smuggling vector
+            # (RFC 7230 3.3.3): refuse it; chunked must be the last coding,
+            # and no other coding is decoded here
+            if clen is not None or te.replace(b" ", b"") != b"chunked":
+                self._fail(400)
+                return False
+            chunked = True
+        elif (clen or 0) > MAX_BODY:
+            self._fail(413)
+            return False
         if expect and not self.continued:
             # the client waits for this before it sends the body (curl does
             # for bodies over 1 KiB)
             self.continued = True
             self.transport.write(b"HTTP/1.1 100 Continue\r\n\r\n")
-        start = end + 4
-        if chunked:
-            body, used = self._dechunk(buf, start)
-            if body is None:
-                return None
-        else:
-            if clen > MAX_BODY:
-                self._fail(413)
-                return None
-            if len(buf) - start < clen:
-                return None
-            body, used = bytes(buf[start:start + clen]), start + clen
-        del buf[:used]
-        self.continued = False
+        del buf[:end + 4]
         req.headers = headers
-        req.body = body
         req.keep_alive = (conn != b"close") if req.version == b"HTTP/1.1" else (conn == b"keep-alive")
-        return req
+        self.cur = req
+        self.chunked = chunked
+        self.clen = clen or 0
+        self.body = bytearray()
+        self.chunk_left = -1
+        self.trailers = False
+        return True
 
-    def _dechunk(self, buf, pos):
-        out = bytearray()
+    def _length_body(self) -> Optional[bytes]:
+        buf = self.buf
+        if len(buf) < self.clen:
+            return None
+        body = bytes(buf[:self.clen])
+        del buf[:self.clen]
+        return body
+
+    def _chunked_body(self) -> Optional[bytes]:
+        """Decode what has arrived of a chunked body; None until it is
+        complete.  Bounded: a declared chunk size that would take the body past
+        MAX_BODY is refused (413) as soon as its size line is read."""
+        buf = self.buf
         while True:
-            e = buf.find(b"\r\n", pos)
-            if e < 0:
-                return None, 0
-            try:
-                n = int(bytes(buf[pos:e]).split(b";")[0], 16)
-            except ValueError:
-                self._fail(400)
-                return None, 0
-            pos = e + 2
-            if n == 0:
-                t = buf.find(b"\r\n\r\n", pos - 2)      # trailers end
+            if self.trailers:                          # after the 0-size chunk
+                if len(buf) < 2:
+                    return None
+                if buf[:2] == b"\r\n":
+                    del buf[:2]
+                    return bytes(self.body)
+                t = buf.find(b"\r\n\r\n")
                 if t < 0:
-                    return None, 0
-                return bytes(out), t + 4
-            if len(buf) < pos + n + 2:
-                return None, 0
-            out += buf[pos:pos + n]
-            pos += n + 2
-            if len(out) > MAX_BODY:
-                self._fail(413)
-                return None, 0
+                    if len(buf) > MAX_HEADER:
+                        self._fail(400)
+                    return None
+                del buf[:t + 4]
+                return bytes(self.body)
+            if self.chunk_left < 0:                    # a chunk-size line
+                e = buf.find(b"\r\n")
+                if e < 0:
+                    if len(buf) > MAX_CHUNK_LINE:
+                        self._fail(400)
+                    return None
+                size = bytes(buf[:e]).split(b";")[0].strip()
+                if not size or any(c not in b"0123456789abcdefABCDEF" for c in size):
+                    self._fail(400)
+                    return None
+                n = int(size, 16)
+                del buf[:e + 2]
+                if n == 0:
+                    self.trailers = True
+                    continue
+                if len(self.body) + n > MAX_BODY:
+                    self._fail(413)
+                    return None
+                self.chunk_left = n + 2                # data + its CRLF
+            data_left = self.chunk_left - 2
+            if data_left > 0:
+                take = min(data_left, len(buf))
+                self.body += buf[:take]
+                del buf[:take]
+                self.chunk_left -= take
+                if self.chunk_left > 2:
+                    return None
+            if len(buf) < 2:
+                return None
+            if buf[:2] != b"\r\n":
+                self._fail(400)
+                return None
+            del buf[:2]
+            self.chunk_left = -1
 
     def _fail(self, status: int):
+        """A request that cannot be framed: stop reading, and answer it in
+        order - after every request already queued on this connection - then
+        close (the error goes through the queue as a pseudo-request)."""
         self.closing = True
-        if self.transport is not None and not self.transport.is_closing():
-            self.transport.write(_head(status, [(b"content-length", b"0")], False))
-            self.transport.close()
+        self.cur = None
+        self.buf = bytearray()
+        if self.transport is None or self.transport.is_closing():
+            return
+        self.transport.pause_reading()
+        err = _Request()
+        err.method, err.target, err.version = "", b"", b"HTTP/1.1"
+        err.headers, err.body, err.keep_alive, err.error = [], b"", False, status
+        self.queue.put_nowait((err, None))
 
     # ------------------------------------------------------------- serving
     async def _serve(self):
-        while True:
-            req = await self.queue.get()
-            if req is None:
-                return
-            if self.paused and self.queue.qsize() < MAX_PIPELINED // 2 and not self.closing:
-                self.paused = False
-                self.transport.resume_reading()
-            try:
-                status, headers, body = await self.srv.handle(req)
-            except Exception:   # noqa: BLE001 - as Starlette's ServerErrorMiddleware
-                _log.exception("Exception in request %s %s", req.method, req.target)
-                status, headers, body = 500, [(b"content-type", b"text/plain; charset=utf-8")], \
-                    b"Internal Server Error"
-            if self.transport.is_closing():
-                return
-            hs = [h for h in headers if h[0] != b"content-length"]
-            hs.append((b"content-length", str(len(body)).encode()))
-            self.transport.write(_head(status, hs, req.keep_alive) + body)
-            if not req.keep_alive:
-                self.closing = True
-                self.transport.close()
-                return
+        try:
+            while True:
+                item = await self.queue.get()
+                if item is None:
+                    return
+                req, task = item
+                if req.error is not None:              # an unframeable request (_fail)
+                    if not self.transport.is_closing():
+                        self.transport.write(_head(req.error, [(b"content-length", b"0")], False))
+                        self.transport.close()
+                    return
+                if self.paused and self.queue.qsize() < MAX_PIPELINED // 2 and not self.closing:
+                    self.paused = False
+                    self.transport.resume_reading()
+                status, headers, body = await task
+                if self.transport.is_closing():
+                    return
+                hs = [h for h in headers if h[0] != b"content-length"]
+                hs.append((b"content-length", str(len(body)).encode()))
+                self.transport.write(_head(status, hs, req.keep_alive) + body)
+                self.srv.served += 1
+                if not req.keep_alive:
+                    self.closing = True
+                    self.transport.close()
+                    return
+        finally:
+            # the connection is gone: requests still queued behind it are dropped
+            while not self.queue.empty():
+                item = self.queue.get_nowait()
+                if item is not None and item[1] is not None and not item[1].done():
+                    item[1].cancel()
 
 
 class FastServer:
@@ -234,6 +326,8 @@ class FastServer:
     def __init__(self, app):
         self.app = app
         self.conns = set()
+        self.served = 0                     # responses written (stats windows)
+        self.accepted = 0                   # connections accepted
         self._lifespan_task = None
         self._lifespan_in: Optional[asyncio.Queue] = None
         self._started = None
@@ -273,7 +367,28 @@ class FastServer:
         finally:
             await asyncio.gather(self._lifespan_task, return_exceptions=True)
 
+    def stats(self) -> dict:
+        """This front end's window since the last call (``MCP_STATS_S``) plus
+        the planner's own (router queues / replica steps, engine thread)."""
+        out = {"conns": len(self.conns), "accepted": self.accepted, "served": self.served}
+        self.accepted = self.served = 0
+        planner = self.app.state.components.get("planner")
+        while planner is not None and not hasattr(planner, "stats") and hasattr(planner, "inner"):
+            planner = planner.inner                     # cache / adaptive wrappers
+        if planner is not None and hasattr(planner, "stats"):
+            out["planner"] = planner.stats()
+        return out
+
     # ------------------------------------------------------------- routing
+    async def handle_safe(self, req: _Request):
+        try:
+            return await self.handle(req)
+        except asyncio.CancelledError:
+            raise
+        except Exception:   # noqa: BLE001 - as Starlette's ServerErrorMiddleware
+            _log.exception("Exception in request %s %s", req.method, req.target)
+            return 500, [(b"content-type", b"text/plain; charset=utf-8")], b"Internal Server Error"
+
     async def handle(self, req: _Request):
         if req.method == "POST" and req.target == b"/plan":
             fast = self._fast_plan_intent(req)
@@ -361,11 +476,19 @@ async def serve_fast(app, sock=None, host: str = "0.0.0.0", port: int = 8000,
             loop.add_signal_handler(sig, stop.set)
         except (NotImplementedError, RuntimeError, ValueError):   # not the main thread
             pass
+    from ..utils.procstats import StatsLog, report_forever, stats_period
+    period = stats_period()
+    stats_task = None
+    if period > 0:                  # per-window health lines (MCP_STATS_S / MCP_STATS_FILE)
+        stats_task = loop.create_task(report_forever(
+            period, srv.stats, StatsLog(os.environ.get("MCP_STATS_FILE")), "api"))
     if ready is not None:
         ready()
     try:
         await stop.wait()
     finally:
+        if stats_task is not None:
+            stats_task.cancel()
         server.close()
         for c in list(srv.conns):
             if c.transport is not None:

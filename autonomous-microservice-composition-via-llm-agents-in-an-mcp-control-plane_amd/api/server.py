@@ -88,6 +88,48 @@ def replica_slice(groups: list, spec: Optional[str]) -> list:
     return groups[w * R // n:(w + 1) * R // n]
 
 
+def _stub_plan(registry: BaseRegistry, settings: Settings) -> Optional[dict]:
+    """Stub replicas' canned DAG: empty, or with MCP_STUB_PLAN_NODES=n a chain
+    over the first n registry services (a response the size of a real plan)."""
+    import os
+    n = int(os.environ.get("MCP_STUB_PLAN_NODES", "0") or 0)
+    if n <= 0:
+        return None
+    svcs = registry.list_services()[:n]
+    nodes = [{"name": s["name"], "endpoint": s["endpoint"],
+              "inputs": {"x": svcs[i - 1]["name"] if i else "payload"}}
+             for i, s in enumerate(svcs)]
+    edges = [{"from": a["name"], "to": b["name"]} for a, b in zip(svcs, svcs[1:])]
+    return {"nodes": nodes, "edges": edges}
+
+
+def replica_config(settings: Settings, registry: BaseRegistry):
+    """The replica processes' configuration from the settings."""
+    from ..parallel.router import ReplicaConfig
+    cfg = ReplicaConfig(model=settings.model, max_batch=settings.max_batch,
+                        max_nodes=settings.max_nodes, min_nodes=settings.min_nodes,
+                        seed=settings.seed, num_blocks=settings.kv_blocks or None,
+                        max_step_tokens=settings.max_step_tokens,
+                        temperature=settings.temperature,
+                        retrieval_threshold=settings.retrieval_threshold,
+                        topk=settings.topk, embed_dim=settings.embed_dim,
+                        tp=max(1, int(settings.tp)))
+    from ..registry import RedisRegistry
+    if isinstance(registry, RedisRegistry):
+        cfg.redis_url, cfg.services_prefix = registry.client.url, registry.prefix
+    if settings.model == "stub":
+        # stub replicas (no engine): MCP_STUB_LATENCY_MS per intent,
+        # MCP_STUB_STALL="at_s:stall_s" freezes each replica once
+        import os
+        stall = os.environ.get("MCP_STUB_STALL", "")
+        at, _, dur = stall.partition(":")
+        cfg.stub_latency_s = float(os.environ.get("MCP_STUB_LATENCY_MS", "0") or 0) / 1e3
+        cfg.stub_stall_at = float(at) if stall else -1.0
+        cfg.stub_stall_s = float(dur or 0)
+        cfg.stub_plan = _stub_plan(registry, settings)
+    return cfg
+
+
 def build_planner(settings: Settings, registry: BaseRegistry,
                   planner_transport: Optional[httpx.AsyncBaseTransport] = None) -> Planner:
     """The planner backend ``settings`` name: stub, a local engine (one
@@ -97,17 +139,10 @@ def build_planner(settings: Settings, registry: BaseRegistry,
         if settings.replicas > 1 or settings.router:
             # request-level DP over replicas, each a TP group of
             # settings.tp ranks (MCP_REPLICAS=2 MCP_TP=4: two TP=4 planners);
-            # with several API workers each routes to its own slice
-            from ..parallel.router import ReplicaConfig, ReplicaRouter, group_devices
-            cfg = ReplicaConfig(model=settings.model, max_batch=settings.max_batch,
-                                max_nodes=settings.max_nodes, min_nodes=settings.min_nodes,
-                                seed=settings.seed,
-                                num_blocks=settings.kv_blocks or None,
-                                max_step_tokens=settings.max_step_tokens,
-                                temperature=settings.temperature,
-                                retrieval_threshold=settings.retrieval_threshold,
-                                topk=settings.topk, embed_dim=settings.embed_dim,
-                                tp=max(1, int(settings.tp)))
+            # several API workers share the supervisor's replicas instead
+            # (serve(): SharedReplicas + SharedRouter)
+            from ..parallel.router import ReplicaRouter, group_devices
+            cfg = replica_config(settings, registry)
             groups = replica_slice(group_devices(settings.replicas, cfg.tp), settings.replica_slice)
             return ReplicaRouter(groups, settings.model, registry, config=cfg)
         if settings.tp > 1:
@@ -270,15 +305,20 @@ def _reuseport_socket(host: str, port: int):
 
 
 def _api_worker(idx: int, n: int, host: str, port: int, access_log: bool,
-                http: str = "fast"):  # pragma: no cover - process entry
-    """One API worker process: builds its planner (its slice of the node's
-    replicas) BEFORE it binds, so the kernel never hands a connection to a
-    worker that is still loading; then serves on its own SO_REUSEPORT socket."""
-    import os
-    os.environ["MCP_REPLICA_SLICE"] = f"{idx}/{n}"
+                http: str = "fast", shared=None):  # pragma: no cover - process entry
+    """One API worker process: builds its planner BEFORE it binds, so the
+    kernel never hands a connection to a worker that is still loading; then
+    serves on its own SO_REUSEPORT socket.  With the local planner the
+    planner is a ``SharedRouter`` over the supervisor's replicas (every
+    worker may dispatch to every replica); otherwise each worker builds its
+    own (stub / remote backends)."""
     settings = Settings.from_env()
     registry = make_registry_from(settings)
-    planner = build_planner(settings, registry)
+    if shared is not None:
+        from ..parallel.router import SharedRouter
+        planner = SharedRouter(shared, idx, registry)
+    else:
+        planner = build_planner(settings, registry)
     app = create_app(settings, registry=registry, planner=planner, settle_gc=True)
     sock = _reuseport_socket(host, port)
     msg = f"mcp api worker {idx}/{n} ready on {host}:{port} ({http})"
@@ -291,6 +331,22 @@ def _api_worker(idx: int, n: int, host: str, port: int, access_log: bool,
     server = uvicorn.Server(uvicorn.Config(app, host=host, port=port, access_log=access_log))
     print(msg, flush=True)
     server.run(sockets=[sock])
+
+
+def check_worker_layout(settings: Settings, workers: int) -> None:
+    """Several API workers with the local planner must split the node's
+    replicas between them (the router path): without it every worker would
+    build its own engine (or TP group) on the same GPU(s), N engines sizing
+    their KV pools from the same free HBM.  Raises SystemExit otherwise."""
+    if workers <= 1 or settings.planner_backend != "local":
+        return
+    if not (settings.replicas > 1 or settings.router):
+        raise SystemExit(f"--workers {workers} with the local planner needs the replica router "
+                         f"(MCP_REPLICAS >= {workers}, or MCP_ROUTER=1 with enough replicas): "
+                         "each API worker would otherwise load its own engine on the same GPU")
+    if workers > settings.replicas:
+        raise SystemExit(f"--workers {workers} > MCP_REPLICAS {settings.replicas}: "
+                         "every API worker routes to at least one replica")
 
 
 def serve(host: str, port: int, workers: int = 1, access_log: bool = True,
@@ -327,17 +383,25 @@ def serve(host: str, port: int, workers: int = 1, access_log: bool = True,
     import signal
     import time
     settings = Settings.from_env()
-    if settings.planner_backend == "local" and (settings.replicas > 1 or settings.router):
-        if workers > settings.replicas:
-            raise SystemExit(f"--workers {workers} > MCP_REPLICAS {settings.replicas}: "
-                             "every API worker routes to at least one replica")
+    check_worker_layout(settings, workers)
     ctx = mp.get_context("spawn")
     procs = {}
     restarts = [0] * workers
+    shared = None
+    if settings.planner_backend == "local":
+        # the node's replicas belong to this supervisor (which never touches
+        # the GPU itself) and are shared by every worker: request-level
+        # least-loaded dispatch whichever worker a connection landed on
+        from ..parallel.router import SharedReplicas, ensure_metrics_dir, group_devices
+        ensure_metrics_dir()
+        registry = make_registry_from(settings)
+        cfg = replica_config(settings, registry)
+        shared = SharedReplicas(group_devices(settings.replicas, cfg.tp), cfg, registry, workers)
+        shared.start()
 
     def start(i):
-        p = ctx.Process(target=_api_worker, args=(i, workers, host, port, access_log, http),
-                        name=f"mcp-api-{i}")
+        p = ctx.Process(target=_api_worker, args=(i, workers, host, port, access_log, http,
+                                                  shared), name=f"mcp-api-{i}")
         p.start()
         procs[i] = p
 
@@ -360,6 +424,8 @@ def serve(host: str, port: int, workers: int = 1, access_log: bool = True,
                     rc = 1
                     break
                 restarts[i] += 1
+                if shared is not None:
+                    shared.reset_worker(i)
                 start(i)
     for p in procs.values():
         if p.is_alive():
@@ -368,6 +434,8 @@ def serve(host: str, port: int, workers: int = 1, access_log: bool = True,
         p.join(timeout=30)
         if p.is_alive():
             p.kill()
+    if shared is not None:
+        shared.close()
     return rc
 
 

@@ -102,14 +102,25 @@ def run_via_api(args):
     behind the router (``MCP_REPLICAS`` / ``MCP_ROUTER``), or with
     ``--replicas 0`` the in-process engine thread of a one-GPU server - and
     this process as the load generator: Poisson arrivals of ``--qps`` per
-    replica over HTTP (httpx, 127.0.0.1), each request's arrival -> DAG time.
-    Same model, registry, DAG size and engine limits as the direct ``qps``
-    mode, so the two lines compare the engine with and without the front end."""
+    replica over HTTP (127.0.0.1), each request's time from its scheduled
+    arrival to its DAG.  Same model, registry, DAG size and engine limits as
+    the direct ``qps`` mode, so the two lines compare the engine with and
+    without the front end.
+
+    ``--client raw`` (default): ``utils/loadgen.py``, O(1) client work per
+    request; ``--client httpx``: the round-5 httpx client, whose pool costs
+    O(connections^2) per request (the cause of the round-5 soak collapse,
+    ``profiles/soak_root_cause_r6.md``).  ``--model stub`` runs stub replicas
+    (no GPU) with ``--stub-latency-ms`` of service time; ``--stub-stall
+    AT:SECONDS`` freezes each replica once.  Every ``--log-s`` seconds, send
+    phase and drain alike, the client logs its window (sent / done / in
+    flight / loop lag / GC) and the server writes its own (front end, router
+    queues, each replica's steps and GC) to ``--stats-file``."""
     import asyncio
     import logging
     import subprocess
-    import httpx
     from mcp_amd.parallel.launch import free_port
+    from mcp_amd.utils.loadgen import open_loop, plan_body
     logging.getLogger("httpx").setLevel(logging.WARNING)
     port = free_port()
     nrep = max(0, args.replicas)
@@ -117,7 +128,17 @@ def run_via_api(args):
                MCP_MAX_BATCH="512", MCP_MAX_STEP_TOKENS="16384", MCP_TEMPERATURE="0.2",
                MCP_MAX_NODES=str(args.max_nodes), MCP_MIN_NODES=str(args.min_nodes),
                MCP_SEED=str(args.seed), MCP_REPLICAS=str(max(1, nrep)),
-               MCP_ROUTER="1" if nrep >= 1 else "0", MCP_SYNTHETIC_SERVICES=str(args.services))
+               MCP_ROUTER="1" if nrep >= 1 else "0", MCP_SYNTHETIC_SERVICES=str(args.services),
+               MCP_STATS_S=str(args.log_s))
+    if args.stats_file:
+        os.makedirs(os.path.dirname(os.path.abspath(args.stats_file)), exist_ok=True)
+        open(args.stats_file, "w").close()
+        env["MCP_STATS_FILE"] = os.path.abspath(args.stats_file)
+    if args.model == "stub":
+        env.update(MCP_STUB_LATENCY_MS=str(args.stub_latency_ms),
+                   MCP_STUB_PLAN_NODES=str(args.max_nodes))
+        if args.stub_stall:
+            env["MCP_STUB_STALL"] = args.stub_stall
     if args.no_graphs:
         env["MCP_GRAPHS"] = "0"
     log_path = os.environ.get("MCP_SERVER_LOG", "/tmp/mcp_api_server.log")
@@ -126,13 +147,16 @@ def run_via_api(args):
                             "--workers", str(args.api_workers)],
                            env=env, stdout=open(log_path, "w"), stderr=subprocess.STDOUT,
                            cwd=os.path.dirname(os.path.abspath(__file__)))
-    base = f"http://127.0.0.1:{port}"
     reg = MemoryRegistry(synthetic_registry(args.services, seed=1))
     names = [s.name for s in reg.list_services()]
+    qps = args.qps * max(1, nrep)
 
-    async def drive():
-        limits = httpx.Limits(max_connections=4096, max_keepalive_connections=1024)
-        async with httpx.AsyncClient(base_url=base, timeout=600.0, limits=limits) as c:
+    def progress(rec):
+        log(f"[via-api qps {qps} {args.client}] " + json.dumps(rec, separators=(",", ":")))
+
+    async def wait_ready():
+        import httpx
+        async with httpx.AsyncClient(base_url=f"http://127.0.0.1:{port}", timeout=600.0) as c:
             t0 = time.time()
             while True:                                  # start-up: model init + graph capture
                 if srv.poll() is not None:
@@ -150,38 +174,82 @@ def run_via_api(args):
             # (MCP_SYNTHETIC_SERVICES, seed 1)
             await asyncio.gather(*[c.post("/plan", json={"intent": synthetic_intent(-1 - i)})
                                    for i in range(max(1, args.warmup))])
-            qps = args.qps * max(1, nrep)
+
+    async def drive_raw():
+        await wait_ready()
+        res = await open_loop("127.0.0.1", port, qps, args.duration,
+                              lambda i: plan_body(synthetic_intent(i)), seed=args.seed,
+                              log_s=args.log_s, progress=progress)
+        dags = [json.loads(b)["graph"] for b in res["bodies"]]
+        errs = res["errors"] if len(res["latencies"]) < res["n"] else []
+        return list(res["latencies"]), dags, errs, res["elapsed_s"], res["n"], res["windows"]
+
+    async def drive_httpx():
+        # the round-5 load generator (kept for the A/B): httpx pool, every
+        # task kept; progress now logged through the drain as well
+        import httpx
+        await wait_ready()
+        limits = httpx.Limits(max_connections=4096, max_keepalive_connections=1024)
+        async with httpx.AsyncClient(base_url=f"http://127.0.0.1:{port}", timeout=600.0,
+                                     limits=limits) as c:
             rng = np.random.default_rng(args.seed)
             n = max(1, int(qps * args.duration))
             arrivals = np.cumsum(rng.exponential(1.0 / qps, n))
             lat, dags, errs = [], [], []
+            st = {"sent": 0, "win_done": 0, "win_sent": 0}
+            windows = []
 
             async def one(i):
-                r = await c.post("/plan", json={"intent": synthetic_intent(i)})
-                if r.status_code != 200:
-                    errs.append(r.text)
-                    return
-                dags.append(r.json()["graph"])
-                lat.append(time.perf_counter() - (t_start + arrivals[i]))
+                try:
+                    r = await c.post("/plan", json={"intent": synthetic_intent(i)})
+                    if r.status_code != 200:
+                        errs.append(r.text)
+                        return
+                    dags.append(r.json()["graph"])
+                    lat.append(time.perf_counter() - (t_start + arrivals[i]))
+                finally:
+                    st["win_done"] += 1
+
+            async def reporter():
+                from mcp_amd.utils.procstats import GCWatch, LoopLag
+                gcw, lag = GCWatch(), LoopLag().start()
+                t_last = time.perf_counter()
+                try:
+                    while True:
+                        await asyncio.sleep(args.log_s)
+                        now = time.perf_counter()
+                        win, t_last = now - t_last, now
+                        pool = c._transport._pool
+                        rec = {"t": round(now - t_start, 1), "sent": st["sent"], "done": len(lat),
+                               "of": n, "sent_per_s": round(st["win_sent"] / win, 1),
+                               "done_per_s": round(st["win_done"] / win, 1), "errors": len(errs),
+                               "inflight": st["sent"] - len(lat) - len(errs),
+                               "conns": len(pool.connections)}
+                        rec.update(lag.snapshot())
+                        rec.update(gcw.snapshot())
+                        st["win_done"] = st["win_sent"] = 0
+                        windows.append(rec)
+                        progress(rec)
+                finally:
+                    lag.stop()
+                    gcw.close()
             tasks = []
             t_start = time.perf_counter()
-            next_log = 30.0            # a progress line every 30 s (long soak runs stay visibly alive)
+            rep = asyncio.get_running_loop().create_task(reporter())
             for i in range(n):
                 delay = t_start + arrivals[i] - time.perf_counter()
                 if delay > 0:
                     await asyncio.sleep(delay)
                 tasks.append(asyncio.create_task(one(i)))
-                if time.perf_counter() - t_start >= next_log:
-                    log(f"[via-api qps {qps}] {next_log:.0f} s: {i + 1} of {n} sent, "
-                        f"{len(lat)} done, {len(errs)} errors")
-                    next_log += 30.0
+                st["sent"] += 1
+                st["win_sent"] += 1
             await asyncio.gather(*tasks)
-            elapsed = time.perf_counter() - t_start
-            metrics = (await c.get("/metrics")).text
-            return lat, dags, errs, elapsed, n, metrics
+            rep.cancel()
+            return lat, dags, errs, time.perf_counter() - t_start, n, windows
 
     try:
-        lat, dags, errs, elapsed, n, metrics = asyncio.run(drive())
+        lat, dags, errs, elapsed, n, windows = asyncio.run(
+            drive_raw() if args.client == "raw" else drive_httpx())
     finally:
         srv.terminate()
         try:
@@ -192,17 +260,29 @@ def run_via_api(args):
         raise RuntimeError(f"{len(errs)} requests failed: {errs[0][:300]}")
     for d in dags:
         validate_dag(d, names)
+    # steady state: windows that ended while arrivals were still being sent
+    send_w = [w for w in windows if w["t"] <= args.duration]
     out = {"metric": "plans/sec at fixed QPS through the API (config 5, deployment path)",
            "path": (f"{'fast HTTP/1.1 front end' if args.http == 'fast' else 'uvicorn + FastAPI'}"
                     f" x {args.api_workers} API worker(s) + "
                     f"{'router -> %d replica process(es)' % nrep if nrep else 'in-process engine thread'}"),
+           "client": args.client,
            "model": args.model, "services": args.services, "dtype": "bf16",
            "data": "synthetic intents, random-init weights", "replicas": nrep,
-           "nodes_per_plan": [args.min_nodes, args.max_nodes], "offered_qps": args.qps * max(1, nrep),
+           "nodes_per_plan": [args.min_nodes, args.max_nodes], "offered_qps": qps,
            "value": round(len(lat) / elapsed, 2), "unit": "plans/s",
            "p50_latency_ms": round(statistics.median(lat) * 1e3, 1),
-           "p99_latency_ms": round(pct(lat, 99) * 1e3, 1), "requests": n, "duration_s": args.duration}
+           "p99_latency_ms": round(pct(lat, 99) * 1e3, 1), "requests": n, "duration_s": args.duration,
+           "window_s": args.log_s,
+           "window_done_per_s_min": min((w["done_per_s"] for w in send_w[1:]), default=None),
+           "window_done_per_s_max": max((w["done_per_s"] for w in send_w[1:]), default=None),
+           "max_inflight": max((w["inflight"] for w in windows), default=None),
+           "client_loop_lag_max_ms": max((w["loop_lag_max_ms"] for w in windows), default=None)}
+    if args.model == "stub":
+        out.update(dtype=None, data="synthetic intents, stub replicas (no model)",
+                   stub_latency_ms=args.stub_latency_ms, stub_stall=args.stub_stall)
     print(json.dumps(out), flush=True)
+    return out
 
 
 def main():
@@ -227,6 +307,16 @@ def main():
                     help="--via-api: the server's front end")
     ap.add_argument("--api-workers", type=int, default=1,
                     help="--via-api: API worker processes (each routes to its slice of the replicas)")
+    ap.add_argument("--client", choices=["raw", "httpx"], default="raw",
+                    help="--via-api: load generator (raw: O(1) per request; httpx: round 5's)")
+    ap.add_argument("--log-s", type=float, default=30.0,
+                    help="--via-api: progress / server stats window, seconds")
+    ap.add_argument("--stats-file", default=None,
+                    help="--via-api: server-side stats lines (JSONL; default: server log)")
+    ap.add_argument("--stub-latency-ms", type=float, default=150.0,
+                    help="--via-api --model stub: replica service time per intent")
+    ap.add_argument("--stub-stall", default="",
+                    help="--via-api --model stub: AT:SECONDS, each replica freezes once")
     args = ap.parse_args()
     if args.via_api:
         return run_via_api(args)

@@ -198,6 +198,59 @@ def test_fast_front_end_http_framing():
         srv.close()
 
 
+def test_fast_front_end_framing_is_strict_and_bounded():
+    """a declared chunk size past MAX_BODY is refused at its size
+    line (no buffering of the body); Transfer-Encoding with Content-Length and
+    conflicting Content-Lengths are 400 (request smuggling, RFC 7230 3.3.3); an
+    unframeable request queued behind good pipelined ones is answered after
+    them, in order; a chunked body delivered one byte per segment decodes."""
+    srv = _FastThread(_make_app())
+    try:
+        head = b"POST /plan HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+        # huge chunk: 413 as soon as the size line is in, body never sent
+        s = socket.create_connection(("127.0.0.1", srv.port), timeout=10)
+        s.sendall(head + b"Transfer-Encoding: chunked\r\n\r\nffffffffff\r\n")
+        got = s.recv(1000)
+        assert got.startswith(b"HTTP/1.1 413"), got
+        s.close()
+        for extra in (b"Transfer-Encoding: chunked\r\nContent-Length: 5\r\n",
+                      b"Content-Length: 5\r\nContent-Length: 6\r\n",
+                      b"Transfer-Encoding: gzip\r\n",
+                      b"Transfer-Encoding: chunked, gzip\r\n"):
+            (st, _, _), = _raw(srv.port, head + extra + b"\r\n0\r\n\r\n")
+            assert st == 400, extra
+        # same Content-Length twice is fine
+        body = b'{"intent": "dup"}'
+        n = str(len(body)).encode()
+        (st, _, _), = _raw(srv.port, head + b"Content-Length: " + n + b"\r\nContent-Length: " + n +
+                           b"\r\n\r\n" + body)
+        assert st == 200
+        # two good pipelined requests, then garbage: 200, 200, 400 in order
+        pipe = (_post(b"/plan", b'{"intent": "one"}') + _post(b"/plan", b'{"intent": "two"}') +
+                b"GARBAGE\r\n\r\n")
+        rs = _raw(srv.port, pipe, n_responses=3)
+        assert [r[0] for r in rs] == [200, 200, 400]
+        assert rs[2][1].get(b"connection") == b"close"
+        # bad chunk framing (data not followed by CRLF) is 400
+        (st, _, _), = _raw(srv.port, head + b"Transfer-Encoding: chunked\r\n\r\n3\r\nabcXY0\r\n\r\n")
+        assert st == 400
+        # chunked body, one byte per send, with a chunk extension and a trailer
+        body = b'{"intent": "slow chunks"}'
+        msg = (head + b"Transfer-Encoding: chunked\r\n\r\n" + b"%x;ext=1\r\n" % 7 + body[:7] +
+               b"\r\n" + b"%x\r\n" % (len(body) - 7) + body[7:] + b"\r\n0\r\nX-T: 1\r\n\r\n")
+        s = socket.create_connection(("127.0.0.1", srv.port), timeout=10)
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        for i in range(len(msg)):
+            s.sendall(msg[i:i + 1])
+        got = b""
+        while b"\r\n\r\n" not in got:
+            got += s.recv(65536)
+        assert got.startswith(b"HTTP/1.1 200"), got
+        s.close()
+    finally:
+        srv.close()
+
+
 def _start_server(port, workers, replicas, http="fast"):
     env = dict(os.environ, MCP_PLANNER_BACKEND="local", MCP_MODEL="stub",
                MCP_REPLICAS=str(replicas), MCP_SYNTHETIC_SERVICES="10", PYTHONPATH=ROOT)
@@ -239,6 +292,79 @@ def test_four_api_workers_carry_eight_replicas_over_real_http():
         out = http_load.main(["--port", str(port), "--seconds", "4", "--conns", "32", "--procs", "3"])
         assert out["status"] == {200: out["requests"]}
         assert out["rps"] >= 3000, out
+    finally:
+        _stop_server(p)
+
+
+@pytest.mark.timeout(300)
+def test_shared_replicas_balance_requests_and_metrics_cover_the_node(tmp_path):
+    """4 API workers share 8 stub replicas (50 ms service
+    time).  A client with only 2 keep-alive connections - so at most 2
+    workers ever see a request - pipelines 40 requests per round on each;
+    pipelined requests run concurrently and every worker dispatches to the
+    node-wide least-loaded replica, so EVERY replica gets work.  One /metrics
+    scrape answers node totals: every request counted once across the 12
+    processes (4 API workers + 8 replicas)."""
+    port = _free_port()
+    mdir = str(tmp_path / "metrics")
+    env = dict(os.environ, MCP_PLANNER_BACKEND="local", MCP_MODEL="stub", MCP_REPLICAS="8",
+               MCP_SYNTHETIC_SERVICES="10", MCP_STUB_LATENCY_MS="50", MCP_METRICS_DIR=mdir,
+               PYTHONPATH=ROOT)
+    p = subprocess.Popen([sys.executable, "-m", "mcp_amd.api.server", "--host", "127.0.0.1",
+                          "--port", str(port), "--workers", "4", "--no-access-log"], cwd=ROOT,
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                         start_new_session=True)
+    try:
+        ready = 0
+        while ready < 4:
+            line = p.stdout.readline()
+            assert line, "server exited during start-up"
+            ready += "ready on" in line
+        socks = [socket.create_connection(("127.0.0.1", port), timeout=30) for _ in range(2)]
+        sent = 0
+        t0 = time.perf_counter()
+        for rnd in range(5):
+            for k, s in enumerate(socks):
+                s.sendall(b"".join(_post(b"/plan", json.dumps({"intent": f"r{rnd} c{k} {i}"}).encode())
+                                   for i in range(40)))
+                sent += 40
+            for s in socks:                               # 40 answers per connection
+                buf, got = b"", 0
+                while got < 40:
+                    chunk = s.recv(1 << 16)
+                    assert chunk
+                    buf += chunk
+                    while True:
+                        h = buf.find(b"\r\n\r\n")
+                        if h < 0:
+                            break
+                        head = buf[:h].split(b"\r\n")
+                        assert head[0].startswith(b"HTTP/1.1 200"), head[0]
+                        n = int(next(x.split(b":")[1] for x in head[1:]
+                                     if x.lower().startswith(b"content-length")))
+                        if len(buf) < h + 4 + n:
+                            break
+                        buf = buf[h + 4 + n:]
+                        got += 1
+        wall = time.perf_counter() - t0
+        for s in socks:
+            s.close()
+        # 400 requests at 50 ms each, one connection-at-a-time would take 10 s
+        assert wall < 5.0, wall
+        time.sleep(2.5)                                   # a metrics export period or two
+        per = {}
+        for n in os.listdir(mdir):
+            if n.startswith("replica-") and n.endswith(".json"):
+                with open(os.path.join(mdir, n)) as f:
+                    per[n] = json.load(f)["counters"].get("plans_total", 0)
+        assert len(per) == 8 and all(v > 0 for v in per.values()), per
+        assert sum(per.values()) == sent
+        with httpx.Client(base_url=f"http://127.0.0.1:{port}") as c:
+            text = c.get("/metrics").text
+        vals = {ln.split(" ")[0]: float(ln.split(" ")[1]) for ln in text.splitlines()
+                if ln and not ln.startswith("#") and "{" not in ln}
+        assert vals["mcp_plans_total"] == sent
+        assert vals["mcp_node_processes"] == 12
     finally:
         _stop_server(p)
 
