@@ -182,6 +182,9 @@ def run_via_api(args):
                               log_s=args.log_s, progress=progress)
         dags = [json.loads(b)["graph"] for b in res["bodies"]]
         errs = res["errors"] if len(res["latencies"]) < res["n"] else []
+        import httpx
+        async with httpx.AsyncClient(base_url=f"http://127.0.0.1:{port}", timeout=60.0) as c:
+            server_metrics["text"] = (await c.get("/metrics")).text
         return list(res["latencies"]), dags, errs, res["elapsed_s"], res["n"], res["windows"]
 
     async def drive_httpx():
@@ -247,6 +250,7 @@ def run_via_api(args):
             rep.cancel()
             return lat, dags, errs, time.perf_counter() - t_start, n, windows
 
+    server_metrics = {}
     try:
         lat, dags, errs, elapsed, n, windows = asyncio.run(
             drive_raw() if args.client == "raw" else drive_httpx())
@@ -278,6 +282,16 @@ def run_via_api(args):
            "window_done_per_s_max": max((w["done_per_s"] for w in send_w[1:]), default=None),
            "max_inflight": max((w["inflight"] for w in windows), default=None),
            "client_loop_lag_max_ms": max((w["loop_lag_max_ms"] for w in windows), default=None)}
+    if server_metrics:
+        # the node's own view (replica engines' windows, last 4096 requests
+        # each): submit -> DAG inside the engine, and its phases, p50 in ms
+        ph = {}
+        for ln in server_metrics["text"].splitlines():
+            if ln.startswith("mcp_") and 'quantile="0.5"' in ln:
+                k = ln.split("{")[0][4:]
+                if k in ("plan_latency_s", "queue_s", "ttft_s", "decode_s", "engine_latency_s"):
+                    ph[k] = round(float(ln.split()[-1]) * 1e3, 1)
+        out["server_p50_ms"] = ph
     if args.model == "stub":
         out.update(dtype=None, data="synthetic intents, stub replicas (no model)",
                    stub_latency_ms=args.stub_latency_ms, stub_stall=args.stub_stall)
