@@ -76,8 +76,10 @@ struct DecArgs {
   int rel;                 // 1: block z covers the own tiles [kt0 + z C, ...), kt0 = kv_begin / 64
 };
 
+// One block of the decode attention: work item b, kv head kvh, key block z
+// (the grid position of attn_decode_kernel; attn_oproj_kernel maps a flat id).
 template <int G>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
+DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const int z) {
   constexpr int TPR = 16 / G;                        // tokens per 16-row tile
   __shared__ __attribute__((aligned(16))) bf16 smem[NWV * TILE];   // per wave: V tile, then O
   __shared__ float s_ml[NWV][2][16];                 // per wave: row max, row sum
@@ -85,8 +87,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int kvh = blockIdx.y, z = blockIdx.z;
-  const int b = blockIdx.x;
   const bool wide = b < 4 * a.nwork4;
   const int s = wide ? a.work_seq4[b >> 2] : a.work_seq1[b - 4 * a.nwork4];
   const int q0 = wide ? a.work_q04[b >> 2] + (b & 3) * TPR : a.work_q01[b - 4 * a.nwork4];
@@ -367,9 +367,150 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
   *reinterpret_cast<bf16x8*>(a.out + grow * D + 8 * c8) = ov;
 }
 
+template <int G>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(const DecArgs a) {
+  attn_decode_body<G>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// ---------------------------------------------------------------------------
+// Decode attention with the o-projection in the same launch (config 2 / low-QPS
+// decode steps, TP = 1).  A decode layer is a chain of short kernels, each
+// paying a launch boundary and a weight-stream ramp; the attention in the
+// middle is a chain of dependent memory round trips (~14 us over a few MB of
+// K / V) during which HBM idles, and the o-projection after it streams 33.5 MB
+// of weights (Llama-3-8B) in ~10-13 us, mostly ramp and tail (5.6 us at
+// 6 TB/s).  Here the grid is [attention blocks | o-projection blocks]:
+//
+//  * the o-projection blocks (16 weight rows x all of K each, 4 waves split K)
+//    load their whole weight slice into registers at once, while the
+//    attention blocks run - the stream overlaps the attention's latency chain;
+//  * each attention block, when done (every path, early exits included),
+//    drains its stores and publishes with the canonical hand-off
+//    (MI355X_MICROARCH.md "Valid forms": stores -> s_waitcnt vmcnt(0) ->
+//    barrier -> lane-0 agent release -> s_waitcnt -> relaxed agent counter add);
+//  * an o-projection block polls the counter (relaxed agent loads, s_sleep,
+//    bounded: a timeout sets the error word and proceeds), takes ONE agent
+//    acquire, loads the attention rows (two halves of its K range), and
+//    finishes with the residual GEMM epilogue of gemm_skinny (EPI 1: + x in
+//    place, the rows' fused-norm statistic);
+//  * the last o-projection block past its poll resets both counters (every
+//    attention block has counted by then), so hipGraph replays start at 0.
+//
+// Attention blocks come first in block order: dispatch is in order per XCD
+// (observed), so a waiting o-projection block never holds a slot an attention
+// block still needs; the grid also fits in two blocks per CU at config 2.
+struct OprojArgs {
+  const bf16* W;                     // [N, K] o-projection weight
+  const bf16* X;                     // [M, K] attention output (= DecArgs.out)
+  bf16* Y;                           // [M, N]: residual in, x + X W^T out (in place)
+  unsigned long long* ss_out;        // fused-norm statistic of the rows written, or null
+  int* sync;                         // [0] attention blocks done, [1] o blocks past the poll
+  int* err;                          // nonzero: a poll timed out
+  int M, N, K;
+  int n_attn, nitems;                // attention blocks, attention grid x extent
+};
+
+constexpr int OP_STEP = 128;
+
+template <int KS>                    // k-steps of 128 per wave: K = 4 x 128 x KS
+DEV void oproj_block(const OprojArgs& o, const int j) {
+  __shared__ f32x4 ored[NWV][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = j * 16;
+  const int kb = wave * KS * OP_STEP;
+  // the weight slice (16 rows x K / 4 per wave) into registers, all in flight
+  const bf16* wrow = o.W + (size_t)(n0 + r) * o.K + kb + 8 * g;
+  bf16x8 w[KS][4];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[s][q] = *reinterpret_cast<const bf16x8*>(wrow + s * OP_STEP + 32 * q);
+  const int m = min(r, o.M - 1);
+  const bf16x4 rr = *reinterpret_cast<const bf16x4*>(o.Y + (size_t)m * o.N + n0 + 4 * g);
+  if (threadIdx.x == 0) {
+    int spins = 0;
+    while (__hip_atomic_load(o.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < o.n_attn) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 24)) {                     // ~seconds: never in a healthy launch
+        __hip_atomic_store(o.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int n_o = o.N / 16;
+    const int old = __hip_atomic_fetch_add(o.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == n_o - 1) {                            // every block is past its poll
+      __hip_atomic_store(o.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // the attention rows, in two halves of this wave's K range
+  const bf16* xrow = o.X + (size_t)m * o.K + kb + 8 * g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int H = KS / 2;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    bf16x8 x[H][4];
+#pragma unroll
+    for (int s = 0; s < H; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        x[s][q] = *reinterpret_cast<const bf16x8*>(xrow + (half * H + s) * OP_STEP + 32 * q);
+#pragma unroll
+    for (int s = 0; s < H; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma16x16x32(w[half * H + s][q], x[s][q], acc);
+  }
+  ored[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0) return;
+  f32x4 v = ored[0][lane] + ored[1][lane] + ored[2][lane] + ored[3][lane];
+  // C layout: lane holds weight rows n0 + 4 g .. + 3 of token r
+  if (r >= o.M) return;                              // all four g lanes of token r together
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] += (float)rr[q];
+  bf16x4 out;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[q] = (bf16)v[q];
+  *reinterpret_cast<bf16x4*>(o.Y + (size_t)r * o.N + n0 + 4 * g) = out;
+  if (o.ss_out) {
+    float ss = sumsq_bf16x4(out);
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (g == 0) ss_atomic_add(o.ss_out + r, ss);
+  }
+}
+
+template <int G, int KS>
+__global__ __launch_bounds__(256, 2) void attn_oproj_kernel(const DecArgs a, const OprojArgs o) {
+  const int f = blockIdx.x;
+  if (f >= o.n_attn) {
+    oproj_block<KS>(o, f - o.n_attn);
+    return;
+  }
+  const int rest = f / o.nitems;
+  attn_decode_body<G>(a, f - rest * o.nitems, rest % a.Hkv, rest / a.Hkv);
+  // publish this block's rows (whichever path it took through the body)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(o.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 }  // namespace
 
 int* attn_split_counters();   // attention.hip
+// the fused kernel's sync words live past the tickets the decode kernel uses
+constexpr int AOP_RESERVED = 64;
+constexpr int SPLIT_TICKETS = (1 << 16) - AOP_RESERVED;
 
 // tiles per wave for a block-table width: <= 64 blocks per (item, kv head)
 int attn_decode_tpw(int max_blocks) {
@@ -387,7 +528,18 @@ int attn_decode_blocks(int max_blocks) {
 // own-span (rel) mode: the same rule over the longest own key span
 int attn_decode_rel_blocks(int own_tiles) { return attn_decode_blocks(own_tiles > 0 ? own_tiles : 1); }
 
+static int launch_attn_decode_impl(const void* q, const void* k_cache, const void* v_cache,
+                                   void* out, const int* q_start, const int* q_len,
+                                   const int* ctx_len, const int* block_table, int max_blocks,
+                                   const int* work_seq4, const int* work_q04, int nwork4,
+                                   const int* work_seq1, const int* work_q01, int nwork1, int Hq,
+                                   int Hkv, int head_dim, float scale, const int* kv_begin,
+                                   const void* pre_o, const float* pre_lse, float* split_o,
+                                   float* split_lse, int rows, int nz, hipStream_t s,
+                                   int own_tiles, const OprojArgs* oproj);
+
 // nonzero: not launched (the caller uses the work-list split path)
+
 int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, void* out,
                        const int* q_start, const int* q_len, const int* ctx_len,
                        const int* block_table, int max_blocks, const int* work_seq4,
@@ -395,16 +547,61 @@ int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, 
                        int nwork1, int Hq, int Hkv, int head_dim, float scale, const int* kv_begin,
                        const void* pre_o, const float* pre_lse, float* split_o, float* split_lse,
                        int rows, int nz, hipStream_t s, int own_tiles) {
+  return launch_attn_decode_impl(q, k_cache, v_cache, out, q_start, q_len, ctx_len, block_table,
+                            max_blocks, work_seq4, work_q04, nwork4, work_seq1, work_q01, nwork1,
+                            Hq, Hkv, head_dim, scale, kv_begin, pre_o, pre_lse, split_o, split_lse,
+                            rows, nz, s, own_tiles, nullptr);
+}
+
+// decode attention + o-projection in one launch (attn_oproj_kernel); nonzero:
+// not launched (7: shape outside the fused form) - the caller runs both apart
+int launch_attn_decode_oproj(const void* q, const void* k_cache, const void* v_cache, void* out,
+                             const int* q_start, const int* q_len, const int* ctx_len,
+                             const int* block_table, int max_blocks, const int* work_seq4,
+                             const int* work_q04, int nwork4, const int* work_seq1,
+                             const int* work_q01, int nwork1, int Hq, int Hkv, int head_dim,
+                             float scale, float* split_o, float* split_lse, int rows, int nz,
+                             const void* Wo, void* x, int M, int N, int K,
+                             unsigned long long* ss_out, hipStream_t s) {
+  OprojArgs o{};
+  o.W = (const bf16*)Wo;
+  o.Y = (bf16*)x;
+  o.ss_out = ss_out;
+  o.M = M;
+  o.N = N;
+  o.K = K;
+  return launch_attn_decode_impl(q, k_cache, v_cache, out, q_start, q_len, ctx_len, block_table,
+                            max_blocks, work_seq4, work_q04, nwork4, work_seq1, work_q01, nwork1,
+                            Hq, Hkv, head_dim, scale, nullptr, nullptr, nullptr, split_o, split_lse,
+                            rows, nz, s, 0, &o);
+}
+
+// the fused kernel's error word (nonzero: an o-projection block's wait timed out)
+int attn_oproj_error() {
+  int* cnt = attn_split_counters();
+  if (!cnt) return 0;
+  int v = 0;
+  if (hipMemcpy(&v, cnt + SPLIT_TICKETS + 2, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return v;
+}
+
+static int launch_attn_decode_impl(const void* q, const void* k_cache, const void* v_cache, void* out,
+                       const int* q_start, const int* q_len, const int* ctx_len,
+                       const int* block_table, int max_blocks, const int* work_seq4,
+                       const int* work_q04, int nwork4, const int* work_seq1, const int* work_q01,
+                       int nwork1, int Hq, int Hkv, int head_dim, float scale, const int* kv_begin,
+                       const void* pre_o, const float* pre_lse, float* split_o, float* split_lse,
+                       int rows, int nz, hipStream_t s, int own_tiles, const OprojArgs* oproj) {
   if (head_dim != D) return 1;
   const int nitems = 4 * nwork4 + nwork1;            // 4-wave items: one block per row tile
-  if (nitems <= 0) return 0;
+  if (nitems <= 0) return oproj ? 7 : 0;
   if (max_blocks <= 0) return 2;
   // own_tiles > 0: own-span mode, the longest own key span in tiles
   const int span = own_tiles > 0 ? own_tiles : max_blocks;
   const int tpw = attn_decode_tpw(span);
   if (nz != attn_decode_blocks(span)) return 3;
   int* cnt = attn_split_counters();
-  if (!cnt || (long long)nitems * Hkv > (1 << 16)) return 5;
+  if (!cnt || (long long)nitems * Hkv > SPLIT_TICKETS) return 5;
   if (nz > 1 && (!split_o || !split_lse || (long long)nz * rows * D * 4 >= (1ll << 31))) return 6;
   DecArgs a{};
   a.q = (const bf16*)q;
@@ -433,6 +630,28 @@ int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, 
   a.split_cnt = cnt;
   a.tpw = tpw;
   a.rel = own_tiles > 0;
+  if (oproj) {
+    // fused o-projection (attn_oproj_kernel): K = Hq D = 4 x 128 x KS, KS = 8
+    // (Llama-3-8B / 3.2-3B padded heads), one 16-token row tile
+    if (own_tiles > 0 || oproj->K != Hq * D || oproj->K != 4 * OP_STEP * 8 || oproj->N % 16 ||
+        oproj->M < 1 || oproj->M > 16 || oproj->M * Hq != rows)
+      return 7;
+    OprojArgs o = *oproj;
+    o.X = a.out;
+    o.sync = cnt + SPLIT_TICKETS;
+    o.err = cnt + SPLIT_TICKETS + 2;
+    o.nitems = nitems;
+    o.n_attn = nitems * Hkv * nz;
+    const int grid1 = o.n_attn + o.N / 16;
+    switch (Hq / Hkv) {
+      case 1: attn_oproj_kernel<1, 8><<<grid1, 256, 0, s>>>(a, o); break;
+      case 2: attn_oproj_kernel<2, 8><<<grid1, 256, 0, s>>>(a, o); break;
+      case 4: attn_oproj_kernel<4, 8><<<grid1, 256, 0, s>>>(a, o); break;
+      case 8: attn_oproj_kernel<8, 8><<<grid1, 256, 0, s>>>(a, o); break;
+      default: return 4;
+    }
+    return 0;
+  }
   const dim3 grid(nitems, Hkv, nz);
   switch (Hq / Hkv) {
     case 1: attn_decode_kernel<1><<<grid, 256, 0, s>>>(a); break;

@@ -536,6 +536,59 @@ bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, cons
   return true;
 }
 
+// decode attention + o-projection in one launch (attention_decode.hip
+// attn_oproj_kernel): out = attention, x += out Wo^T (in place) with the rows'
+// fused-norm statistic added to ss_out; false = not launched (the caller runs
+// paged_attention_decode and the GEMM apart)
+bool paged_attention_decode_oproj(const at::Tensor& q, const at::Tensor& k_cache,
+                                  const at::Tensor& v_cache, at::Tensor& out,
+                                  const at::Tensor& q_start, const at::Tensor& q_len,
+                                  const at::Tensor& ctx_len, const at::Tensor& block_table,
+                                  const at::Tensor& work_seq4, const at::Tensor& work_q04,
+                                  const at::Tensor& work_seq1, const at::Tensor& work_q01,
+                                  double scale, int64_t nz, at::Tensor& split_o,
+                                  at::Tensor& split_lse, const at::Tensor& wo, at::Tensor& x,
+                                  const c10::optional<at::Tensor>& ss_out) {
+  CHECK_BF16_TENSOR(q); CHECK_BF16_TENSOR(k_cache); CHECK_BF16_TENSOR(v_cache); CHECK_BF16_TENSOR(out);
+  CHECK_BF16_TENSOR(wo); CHECK_BF16_TENSOR(x);
+  CHECK_I32_TENSOR(q_start); CHECK_I32_TENSOR(q_len); CHECK_I32_TENSOR(ctx_len);
+  CHECK_I32_TENSOR(block_table); CHECK_I32_TENSOR(work_seq4); CHECK_I32_TENSOR(work_q04);
+  CHECK_I32_TENSOR(work_seq1); CHECK_I32_TENSOR(work_q01);
+  TORCH_CHECK(q.dim() == 3, "q must be [T, Hq, D]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64, "cache block size must be 64");
+  const int Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1);
+  const int T = q.size(0);
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out shape");
+  TORCH_CHECK(block_table.dim() == 2 && block_table.size(0) == q_len.numel(), "block_table [S, max_blocks]");
+  TORCH_CHECK(work_seq4.numel() == work_q04.numel() && work_seq1.numel() == work_q01.numel(),
+              "work lists");
+  TORCH_CHECK(nz == attn_decode_blocks(block_table.size(1)), "nz must be attn_decode_blocks(max_blocks)");
+  TORCH_CHECK(split_o.scalar_type() == at::kFloat && split_o.is_contiguous() &&
+              (nz == 1 || split_o.numel() >= nz * q.numel()), "split_o [nz, T, Hq, D] f32");
+  TORCH_CHECK(split_lse.scalar_type() == at::kFloat && split_lse.is_contiguous() &&
+              (nz == 1 || split_lse.numel() >= nz * T * Hq), "split_lse [nz, T, Hq] f32");
+  TORCH_CHECK(wo.dim() == 2 && wo.size(1) == (int64_t)Hq * D, "wo [N, Hq * D]");
+  TORCH_CHECK(x.dim() == 2 && x.size(0) == T && x.size(1) == wo.size(0), "x [T, N]");
+  unsigned long long* ss = nullptr;
+  if (ss_out.has_value()) {
+    TORCH_CHECK(ss_out->scalar_type() == at::kLong && ss_out->is_contiguous() && ss_out->numel() >= T,
+                "ss_out int64 [>= T]");
+    ss = reinterpret_cast<unsigned long long*>(ss_out->data_ptr<int64_t>());
+  }
+  const int rc = launch_attn_decode_oproj(
+      q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(), q_start.data_ptr<int>(),
+      q_len.data_ptr<int>(), ctx_len.data_ptr<int>(), block_table.data_ptr<int>(),
+      block_table.size(1), work_seq4.data_ptr<int>(), work_q04.data_ptr<int>(), work_seq4.numel(),
+      work_seq1.data_ptr<int>(), work_q01.data_ptr<int>(), work_seq1.numel(), Hq, Hkv, D,
+      (float)scale, split_o.data_ptr<float>(), split_lse.data_ptr<float>(), T * Hq, (int)nz,
+      wo.data_ptr(), x.data_ptr(), T, (int)wo.size(0), (int)wo.size(1), ss, stream());
+  TORCH_CHECK(rc != 1 && rc != 3 && rc != 4, "paged_attention_decode_oproj: unsupported config (code ", rc, ")");
+  if (rc != 0) return false;
+  check_launch("paged_attention_decode_oproj");
+  return true;
+}
+
 void cascade_merge(at::Tensor& out, const at::Tensor& own_lse, const at::Tensor& pre_o,
                    const at::Tensor& pre_lse, int64_t pre_tokens,
                    const c10::optional<at::Tensor>& pre_dims) {
@@ -869,6 +922,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_dense", &sample_dense);
   m.def("branch_select", &branch_select);
   m.def("add_inplace", &add_inplace);
+  m.def("paged_attention_decode_oproj", &paged_attention_decode_oproj,
+        "decode attention + o-projection (x += out Wo^T, in place) in one launch; false: not launched",
+        py::arg("q"), py::arg("k_cache"), py::arg("v_cache"), py::arg("out"), py::arg("q_start"),
+        py::arg("q_len"), py::arg("ctx_len"), py::arg("block_table"), py::arg("work_seq4"),
+        py::arg("work_q04"), py::arg("work_seq1"), py::arg("work_q01"), py::arg("scale"),
+        py::arg("nz"), py::arg("split_o"), py::arg("split_lse"), py::arg("wo"), py::arg("x"),
+        py::arg("ss_out") = py::none());
+  m.def("attn_oproj_error", &attn_oproj_error, "nonzero: a fused o-projection wait timed out");
   m.def("attn_decode_blocks", &attn_decode_blocks, "grid z of paged_attention_decode for a table width");
   m.def("paged_attention_decode", &paged_attention_decode, py::arg("q"), py::arg("k_cache"),
         py::arg("v_cache"), py::arg("out"), py::arg("q_start"), py::arg("q_len"), py::arg("ctx_len"),

@@ -169,6 +169,17 @@ int launch_attn_decode(const void* q, const void* k_cache, const void* v_cache, 
                        const void* pre_o, const float* pre_lse, float* split_o, float* split_lse,
                        int rows, int nz, hipStream_t s, int own_tiles = 0);
 int attn_decode_rel_blocks(int own_tiles);   // grid z of the own-span mode
+// the decode attention and the o-projection (x += out Wo^T, fused-norm
+// statistic) in one launch; nonzero = not launched (shape outside the form)
+int launch_attn_decode_oproj(const void* q, const void* k_cache, const void* v_cache, void* out,
+                             const int* q_start, const int* q_len, const int* ctx_len,
+                             const int* block_table, int max_blocks, const int* work_seq4,
+                             const int* work_q04, int nwork4, const int* work_seq1,
+                             const int* work_q01, int nwork1, int Hq, int Hkv, int head_dim,
+                             float scale, float* split_o, float* split_lse, int rows, int nz,
+                             const void* Wo, void* x, int M, int N, int K,
+                             unsigned long long* ss_out, hipStream_t s);
+int attn_oproj_error();
 int launch_paged_attention_mixed(const void* q, const void* k_cache, const void* v_cache,
                                  void* out, const int* q_start, const int* q_len,
                                  const int* ctx_len, const int* block_table, int max_blocks,

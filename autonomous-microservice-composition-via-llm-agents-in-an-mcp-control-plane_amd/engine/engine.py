@@ -221,6 +221,13 @@ class LLMEngine:
         # (retrieval-sized) prompt no longer stretches every running
         # request's decision step to a whole-prompt forward (config 3)
         self.prefill_chunk = int(os.environ.get("MCP_PREFILL_CHUNK", "0"))
+        # decode priority: with MCP_PREFILL_DECODE_REF = r
+        # > 0 the prompt budget shrinks as decoding requests grow - the chunk
+        # while at most r requests decode, chunk * r / n with n decoding,
+        # never below MCP_PREFILL_MIN - so a step's decisions stay cheap when
+        # many requests wait on them, and prompts go faster when few do
+        self.prefill_decode_ref = int(os.environ.get("MCP_PREFILL_DECODE_REF", "0"))
+        self.prefill_min = int(os.environ.get("MCP_PREFILL_MIN", "64"))
         self.temperature = temperature
         self.seed = seed
         self.running: List[Sequence] = []
@@ -662,6 +669,14 @@ class LLMEngine:
                 return True
         return False
 
+    def prefill_budget(self, n_decoding: int) -> int:
+        """Prompt tokens one step may take while ``n_decoding`` requests are
+        past their first sample (chunked prefill, decode priority)."""
+        c, r = self.prefill_chunk, self.prefill_decode_ref
+        if r <= 0 or n_decoding <= r:
+            return c
+        return max(min(c, self.prefill_min), c * r // n_decoding)
+
     def _schedule_launch(self, cohort: Optional[int]) -> Optional[_Launch]:
         try:
             return self._schedule_launch_inner(cohort)
@@ -721,8 +736,10 @@ class LLMEngine:
         # chunked prefill: the prompt-token budget of this step, when decoding
         # requests share it (None: no cap)
         pf_left = None
-        if self.prefill_chunk > 0 and any(q.n_samples > 0 for q in order):
-            pf_left = self.prefill_chunk
+        if self.prefill_chunk > 0:
+            n_dec = sum(1 for q in order if q.n_samples > 0)
+            if n_dec:
+                pf_left = self.prefill_budget(n_dec)
         add_entry, add_batch, add_sample = entries.append, batch_seqs.append, sample_seqs.append
         # the per-request loop of every step (host critical path): locals bound,
         # _ensure_blocks / wants_sample inlined

@@ -267,7 +267,11 @@ class GraphRunner:
         self._body(e)                                   # eager warm-up (lazy allocations)
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self._pool):
+        # thread_local: another host thread's work on its own stream (the
+        # planner's prep thread running a retrieval search, MCP_PREP_THREAD)
+        # may proceed while this thread captures a lazily built bucket
+        mode = "thread_local" if os.environ.get("MCP_PREP_THREAD", "0") == "1" else "global"
+        with torch.cuda.graph(g, pool=self._pool, capture_error_mode=mode):
             e.tokens = self._body(e)
         self._pool = g.pool()
         e.graph = g

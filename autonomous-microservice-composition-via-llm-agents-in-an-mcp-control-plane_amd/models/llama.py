@@ -171,6 +171,9 @@ CONFIGS = {
     # reduced configs with the same kernels (tests / smoke): head_dim stays 128
     "llama3-1b-ish": LlamaConfig("llama3-1b-ish", hidden=2048, layers=16, heads=16, kv_heads=4, ffn=8192),
     "tiny": LlamaConfig("tiny", hidden=256, layers=2, heads=2, kv_heads=1, ffn=512),
+    # Llama-3-8B layer shapes, 2 layers: tests of shape-specific kernels
+    # (the fused decode attention + o-projection needs K = Hq D = 4096)
+    "llama3-8b-2l": LlamaConfig("llama3-8b-2l", layers=2),
     "tiny-tp": LlamaConfig("tiny-tp", hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024),
     # 8 KV heads: shards to TP = 8 like the 70B (one KV head per rank)
     "tiny-tp8": LlamaConfig("tiny-tp8", hidden=2048, layers=2, heads=16, kv_heads=8, ffn=4096),
@@ -496,6 +499,15 @@ class LlamaModel:
                     rest = _PF_BYTES - lw.wo.numel() * lw.wo.element_size()
                     if rest > 0:
                         ops.weight_prefetch(lw.w_gate_up, rest, _PF_WGS)
+            if (self.tp == 1 and l + 1 < L and x.is_cuda and side is None
+                    and ops.attention_oproj(q, kc, vc, step.attn, self.scale, lw.wo, x,
+                                            ss_out=ss[l, 1])):
+                # decode-sized step: attention and the o-projection (+ residual,
+                # fused-norm statistic) in one launch, the o weights streaming
+                # under the attention's latency chain (csrc/attention_decode.hip)
+                act = ops.gemm_silu(x, lw.w_gate_up, ss_in=ss[l, 1], eps=eps)
+                x = self._residual_gemm_ss(act, lw.w_down, x, ss[l + 1, 0])
+                continue
             a = ops.paged_attention(q, kc, vc, step.attn, self.scale)
             if l + 1 == L:
                 # last layer: only the sampled rows go on (see ``forward``)

@@ -322,6 +322,62 @@ def prefix_splits(pre_tokens: int, pre_keys: int, hkv: int, num_cus: int = 256) 
     return ns if ns >= 2 else 1
 
 
+# decode attention + o-projection in one launch (csrc/attention_decode.hip
+# attn_oproj_kernel; MCP_ATTN_OPROJ=0 disables)
+_ATTN_OPROJ = os.environ.get("MCP_ATTN_OPROJ", "1") == "1"
+
+
+def _decode_lists(q, k_cache, meta):
+    """The decode kernel's work lists and grid z when a step takes it (the
+    use_dec rule of paged_attention), else None."""
+    L = lib()
+    ns = int(getattr(meta, "kv_splits", 1))
+    if not (ns > 1 and _DECODE_SPLIT and hasattr(L, "paged_attention_decode")):
+        return None
+    lists = {nw: (ws, wq) for nw, ws, wq in meta.work_lists()}
+    e = torch.empty(0, dtype=torch.int32, device=q.device)
+    ws4, wq4 = lists.get(4, (e, e))
+    ws1, wq1 = lists.get(1, (e, e))
+    nz = L.attn_decode_blocks(int(meta.block_table.shape[1]))
+    use = _DECODE_FORCE or getattr(meta, "padded", False) or (
+        (4 * ws4.numel() + ws1.numel()) * k_cache.shape[1] * nz
+        <= _DECODE_BLOCKS_PER_CU * _num_cus(q.device))
+    return (ws4, wq4, ws1, wq1, nz) if use else None
+
+
+def attention_oproj(q, k_cache, v_cache, meta, scale, wo, x, ss_out=None, out=None) -> bool:
+    """Decode-sized step, TP = 1: paged attention into ``out`` and
+    ``x += out.view(T, -1) @ wo.T`` (in place, the rows' fused-norm statistic
+    added to ``ss_out``) in ONE launch, the o-projection's weights streamed
+    while the attention runs.  True when done; False when the step is outside
+    the fused form (cascade prefix, no split-KV decode path, > 16 tokens,
+    K != 4096) - nothing was launched and the caller runs both ops apart.
+    Reference semantics: ``paged_attention`` then ``gemm(a, wo, R=x, out=x,
+    ss_out=ss_out)``."""
+    if not (q.is_cuda and _ATTN_OPROJ) or meta.pre_tokens > 0 or q.shape[0] > 16:
+        return False
+    L = lib()
+    if not hasattr(L, "paged_attention_decode_oproj"):
+        return False
+    dl = _decode_lists(q, k_cache, meta)
+    if dl is None:
+        return False
+    ws4, wq4, ws1, wq1, nz = dl
+    global ATTN_OPROJ_LAUNCHES
+    out = torch.empty_like(q) if out is None else out
+    so = torch.empty(nz if nz > 1 else 0, *q.shape, device=q.device, dtype=torch.float32)
+    sl = torch.empty(nz if nz > 1 else 0, q.shape[0], q.shape[1], device=q.device,
+                     dtype=torch.float32)
+    done = bool(L.paged_attention_decode_oproj(q, k_cache, v_cache, out, meta.q_start, meta.q_len,
+                                               meta.ctx_len, meta.block_table, ws4, wq4, ws1, wq1,
+                                               scale, nz, so, sl, wo, x, ss_out))
+    ATTN_OPROJ_LAUNCHES += done
+    return done
+
+
+ATTN_OPROJ_LAUNCHES = 0          # host-side count of fused launches (captures count once)
+
+
 def paged_attention(q, k_cache, v_cache, meta, scale, out=None):
     """``meta`` is an ``AttnMeta`` (engine.batch) holding the per-sequence and
     work-list int32 tensors."""

@@ -70,6 +70,13 @@ class LocalPlanner(Planner):
         self.stalled = False
         # retrieval counts and their rank snapshot (MCP_RETRIEVAL_ORDER=popular)
         self._pop = {"counts": {}, "rank": {}, "n": 0, "lock": threading.Lock()}
+        # MCP_PREP_THREAD=1: the per-request host phases (retrieval, grammar,
+        # tokenisation) run on their own thread, so the engine thread only
+        # schedules and launches steps; the prep thread's Python work runs
+        # while the engine thread waits on the GPU (which releases the GIL)
+        self.prep_thread = os.environ.get("MCP_PREP_THREAD", "0") == "1"
+        self._prepq: "queue.Queue" = queue.Queue()
+        self._prep: Optional[threading.Thread] = None
 
     # ----------------------------------------------------------- factory
     @classmethod
@@ -235,6 +242,9 @@ class LocalPlanner(Planner):
         if self._thread is None or not self._thread.is_alive():
             self._thread = threading.Thread(target=self._loop, name="mcp-engine", daemon=True)
             self._thread.start()
+        if self.prep_thread and (self._prep is None or not self._prep.is_alive()):
+            self._prep = threading.Thread(target=self._prep_loop, name="mcp-prep", daemon=True)
+            self._prep.start()
         if self.watchdog_s > 0 and (self._watchdog is None or not self._watchdog.is_alive()):
             self._watchdog = threading.Thread(target=self._watch, name="mcp-watchdog", daemon=True)
             self._watchdog.start()
@@ -266,9 +276,10 @@ class LocalPlanner(Planner):
             except queue.Empty:
                 item = None
             while item is not None:
-                intent, loop, fut = item
+                intent, loop, fut = item[:3]
                 try:
-                    dec, ptoks, stoks = self.prepare(intent)
+                    # prepared on the prep thread, or here
+                    dec, ptoks, stoks = item[3] if len(item) > 3 else self.prepare(intent)
                     t0 = time.perf_counter()
 
                     def done(seq, loop=loop, fut=fut, t0=t0):
@@ -296,6 +307,17 @@ class LocalPlanner(Planner):
                 METRICS.inc("aborted_requests", n)
                 self.stalled = False
 
+    def _prep_loop(self):
+        while not self._stop.is_set():
+            try:
+                intent, loop, fut = self._prepq.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            try:
+                self._q.put((intent, loop, fut, self.prepare(intent)))
+            except Exception as e:  # noqa: BLE001
+                loop.call_soon_threadsafe(_set_exc, fut, e)
+
     async def plan(self, intent: str) -> dict:
         if self.stalled:
             raise EngineStalled("planner engine is stalled")
@@ -304,13 +326,15 @@ class LocalPlanner(Planner):
         fut = loop.create_future()
         with self._pending_lock:
             self._pending[id(fut)] = (loop, fut)
-        self._q.put((intent, loop, fut))
+        (self._prepq if self.prep_thread else self._q).put((intent, loop, fut))
         return await fut
 
     async def aclose(self):
         self._stop.set()
         if self._thread is not None:
             self._thread.join(timeout=5)
+        if self._prep is not None:
+            self._prep.join(timeout=5)
 
 
 def _set_result(fut, v):

@@ -786,3 +786,61 @@ def test_chunked_prefill_caps_prompt_tokens_beside_decoding_requests(monkeypatch
     assert out[0] == out[1]
     assert worst[0] > 24 >= worst[1], worst
     assert steps[1] > steps[0]
+
+
+def test_decode_priority_prefill_budget_shrinks_with_decoders(monkeypatch):
+    """MCP_PREFILL_DECODE_REF makes the per-step prompt
+    budget shrink as decoding requests grow (chunk while <= ref decode, chunk
+    * ref / n beyond, floored at MCP_PREFILL_MIN); plans stay the greedy plans."""
+    monkeypatch.setenv("MCP_PREFILL_CHUNK", "512")
+    monkeypatch.setenv("MCP_PREFILL_DECODE_REF", "4")
+    monkeypatch.setenv("MCP_PREFILL_MIN", "64")
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, graphs=False)
+    assert [eng.prefill_budget(n) for n in (1, 4, 8, 16, 32, 64)] == [512, 512, 256, 128, 64, 64]
+    monkeypatch.setenv("MCP_PREFILL_DECODE_REF", "0")
+    eng0 = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, graphs=False)
+    assert eng0.prefill_budget(64) == 512
+    reg = MemoryRegistry(synthetic_registry(12, seed=5))
+    intents = [synthetic_intent(i) for i in range(6)]
+    outs = []
+    for ref in ("0", "1"):
+        monkeypatch.setenv("MCP_PREFILL_CHUNK", "16")
+        monkeypatch.setenv("MCP_PREFILL_DECODE_REF", ref)
+        monkeypatch.setenv("MCP_PREFILL_MIN", "8")
+        torch.manual_seed(0)
+        e = LLMEngine(LlamaModel.random("tiny", "cpu", seed=1), num_blocks=256, max_batch=16,
+                      temperature=0.0, graphs=False)
+        planner = LocalPlanner(e, reg, max_nodes=3)
+        seqs = planner.submit_many(intents[:3])
+        while not all(q.n_samples > 0 for q in seqs):
+            e.step()
+        seqs += planner.submit_many(intents[3:])
+        e.run()
+        assert all(q.done and q.error is None for q in seqs)
+        outs.append([q.result for q in seqs])
+    assert outs[0] == outs[1]
+
+
+def test_prep_thread_gives_the_same_plans(monkeypatch):
+    """MCP_PREP_THREAD=1: retrieval, grammar and tokenisation run on a prep
+    thread beside the engine thread; concurrent async plans are the greedy
+    plans of the in-line path."""
+    from mcp_amd.retrieval.store import SchemaIndex
+    reg = MemoryRegistry(synthetic_registry(60, seed=7))
+    intents = [synthetic_intent(300 + i) for i in range(8)]
+    outs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("MCP_PREP_THREAD", on)
+        model = LlamaModel.random("tiny", "cpu", seed=1)
+        eng = LLMEngine(model, num_blocks=256, max_batch=8, temperature=0.0, graphs=False)
+        retr = SchemaIndex(reg, dim=64, device="cpu")
+        retr.refresh()
+        planner = LocalPlanner(eng, reg, max_nodes=3, retriever=retr, retrieval_threshold=8, topk=6)
+        assert planner.prep_thread == (on == "1")
+
+        async def serve():
+            return await asyncio.gather(*[planner.plan(x) for x in intents])
+        outs.append(asyncio.run(serve()))
+        asyncio.run(planner.aclose())
+    assert outs[0] == outs[1]
