@@ -536,6 +536,18 @@ bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, cons
   return true;
 }
 
+// GEMM power ladder rung (gemm256d.hip PROBE): Y [M, N] (epi 0) or [M, N/2] (epi 2)
+void gemm_probe(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y, int64_t epi, int64_t probe) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
+  const int M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "W [N, K]");
+  TORCH_CHECK(Y.size(0) == M && Y.size(1) == (epi == 2 ? N / 2 : N), "Y shape");
+  const int rc = launch_gemm_probe(X.data_ptr(), W.data_ptr(), Y.data_ptr(), M, N, K, (int)epi,
+                                   (int)probe, stream());
+  TORCH_CHECK(rc == 0, "gemm_probe: M % 256, N % 256, K % 128, epi 0 / 2, probe 0-3");
+  check_launch("gemm_probe");
+}
+
 // decode attention + o-projection in one launch (attention_decode.hip
 // attn_oproj_kernel): out = attention, x += out Wo^T (in place) with the rows'
 // fused-norm statistic added to ss_out; false = not launched (the caller runs
@@ -929,6 +941,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("work_q04"), py::arg("work_seq1"), py::arg("work_q01"), py::arg("scale"),
         py::arg("nz"), py::arg("split_o"), py::arg("split_lse"), py::arg("wo"), py::arg("x"),
         py::arg("ss_out") = py::none());
+  m.def("gemm_probe", &gemm_probe, "GEMM power-ladder rung (gemm256d.hip PROBE 0-3)");
   m.def("attn_oproj_error", &attn_oproj_error, "nonzero: a fused o-projection wait timed out");
   m.def("attn_decode_blocks", &attn_decode_blocks, "grid z of paged_attention_decode for a table width");
   m.def("paged_attention_decode", &paged_attention_decode, py::arg("q"), py::arg("k_cache"),

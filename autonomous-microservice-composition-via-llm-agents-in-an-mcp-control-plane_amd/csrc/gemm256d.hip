@@ -85,7 +85,12 @@ constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 
 // The epilogue goes through LDS (row-contiguous 16-B stores); the direct
 // MFMA-layout store measured 10-15 % slower (profiles/gemm_tuning.md).
-template <int EPI, int BMT, bool WIDE = false>
+// PROBE (timing / power ladder only, tools/gemm_power_ladder.py; results are
+// not a product): 0 = production; 1 = the MFMA issue alone (fragments read
+// once, no DMA, no barriers, no stores); 2 = + the ds_read fragment schedule
+// and the barriers (no DMA, no stores); 3 = + the LDS-DMA (the whole
+// mainloop, no epilogue stores).  Rung 0 minus rung 3 is the epilogue.
+template <int EPI, int BMT, bool WIDE = false, int PROBE = 0>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
@@ -135,6 +140,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // the last row of X / W
   const int nt = K / BK;                             // >= 2, even (launcher)
   auto dma1 = [&](int t, int slot, int i) {          // i < QA: A instruction i, else B i-QA
+    if (PROBE == 1 || PROBE == 2) {
+      if (t > 1) return;                             // probes: the prologue's tiles only
+    }
     const bool b = i >= QA;
     const int q = b ? i - QA : i;
     const int kb = min(t, nt - 1) * BK * 2;
@@ -160,7 +168,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
       rbase[sl][kh][0] = sl * SLOT_B + (wm * WROWS + fr) * ROWB + ch;
       rbase[sl][kh][1] = sl * SLOT_B + PIECE_A + (wn * 128 + fr) * ROWB + ch;
     }
+  bool prologue = true;                              // PROBE 1 reads fragments here only
   auto fread1 = [&](int slot, int kh, Frags<MTW>& f, int i) {   // i < 8: B[i], else A[i-8]
+    if constexpr (PROBE == 1) {
+      if (!prologue) return;
+    }
     if (i < 8)
       f.b[i] = *reinterpret_cast<const bf16x8*>(smem + rbase[slot][kh][1] + i * 2048);
     else
@@ -195,6 +207,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   raw_barrier();
 #pragma unroll
   for (int i = 0; i < NRD; ++i) fread1(0, 0, F[0], i);
+  if constexpr (PROBE == 1) {                        // both fragment sets hold real data
+#pragma unroll
+    for (int i = 0; i < NRD; ++i) fread1(0, 1, F[1], i);
+    prologue = false;
+  }
   __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): clean waitcnt state at the loop head
   asm volatile("s_nop 4" ::: "memory");
 
@@ -225,8 +242,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     }
     keep(F[0]);
     // tile t+1 landed (own DMAs), and this wave's reads of slot C are done
-    __builtin_amdgcn_s_waitcnt(0x0070);              // vmcnt(0) lgkmcnt(0)
-    raw_barrier();
+    if constexpr (PROBE != 1) {
+      __builtin_amdgcn_s_waitcnt(0x0070);            // vmcnt(0) lgkmcnt(0)
+      raw_barrier();
+    }
     fence();
 #pragma unroll
     for (int j = 0; j < NP; ++j) {                   // half 1: F[1], reads of (t+1, k0), DMA t+2
@@ -250,6 +269,19 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // drain the trailing (unconsumed) DMAs before the workgroup's LDS is released,
   // and pad MFMA results -> VALU reads (inline asm is not padded)
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  if constexpr (PROBE != 0) {
+    // probes store nothing; one accumulator reaches memory under a condition
+    // no launch meets, so the MFMA results stay live
+    if (M == -7 && lane == 0) {
+      f32x4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t += acc[i][j];
+      *reinterpret_cast<f32x4*>(Y) = t;
+    }
+    return;
+  }
 
   if constexpr (WIDE && EPI != 3) {
     // ---- wide direct epilogue (common.h store_wide): straight from the
@@ -674,4 +706,39 @@ void launch_qkv_rope(const void* X, const void* W, void* qkv, int M, int N, int 
 int launch_gemm_tn_256d(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
                         int epi, hipStream_t s) {
   return launch_gemm_tn_256d_bm(X, W, Y, R, M, N, K, epi, 0, s);
+}
+
+// the power / issue ladder of the production gate|up kernel (SwiGLU, wide
+// epilogue, 256-row tiles) and of a plain 256-row one: rung 0 = production,
+// 1-3 = the PROBE forms above (tools/gemm_power_ladder.py); nonzero if the
+// shape is not a whole-tile one
+int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K, int epi,
+                      int probe, hipStream_t s) {
+  if (M % 256 || N % BN || K % (2 * BK) || (epi != 0 && epi != 2) || probe < 0 || probe > 3)
+    return 1;
+  const dim3 grid((M / 256) * (N / BN));
+  const int group = gemm256d_group(M, N, K);
+  auto x = (const bf16*)X;
+  auto w = (const bf16*)W;
+  auto y = (bf16*)Y;
+  const RopeArgs ra{};
+  const NormEpi ne{};
+#define PROBE_LAUNCH(E, P) gemm_tn_256d<E, 256, true, P><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, ne)
+  if (epi == 2) {
+    switch (probe) {
+      case 0: PROBE_LAUNCH(2, 0); break;
+      case 1: PROBE_LAUNCH(2, 1); break;
+      case 2: PROBE_LAUNCH(2, 2); break;
+      default: PROBE_LAUNCH(2, 3); break;
+    }
+  } else {
+    switch (probe) {
+      case 0: PROBE_LAUNCH(0, 0); break;
+      case 1: PROBE_LAUNCH(0, 1); break;
+      case 2: PROBE_LAUNCH(0, 2); break;
+      default: PROBE_LAUNCH(0, 3); break;
+    }
+  }
+#undef PROBE_LAUNCH
+  return 0;
 }

@@ -122,6 +122,10 @@ int gemm_plan_split(int M, int N, int K);
 void gemm_plan_clear();
 int gemm256d_ok(int M, int N, int K);
 int gemm256d_code_height(int code);     // plan code 1..5 -> AGPR tile height (0: none)
+// timing / power ladder of the 256-row AGPR kernel (tools/gemm_power_ladder.py):
+// probe 0 production, 1 MFMA only, 2 + ds_read + barriers, 3 + LDS-DMA (no stores)
+int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K, int epi,
+                      int probe, hipStream_t s);
 int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
                            int K, int epi, int bm, hipStream_t s);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]
