@@ -1097,6 +1097,7 @@ class LLMEngine:
         row = {id(q): i for i, q in enumerate(order)}
         now = None
         finished = []
+        bad = False
         with span("retire.update"):
             for q, brs in zip(cur.seqs, cur.branches):
                 if brs is None:               # admitted with known tokens (counted at launch)
@@ -1104,8 +1105,17 @@ class LLMEngine:
                 t = toks[row[id(q)]]
                 br = brs.get(t)
                 if br is None:
-                    raise RuntimeError(f"decision lookahead: sampled token {t} is not an outcome "
-                                       f"of the pending choice")
+                    # cannot happen with the grammar's allowed sets (the kernel
+                    # samples only from them); if it does, the branch step ran
+                    # this request on outcome 0's tokens: fail THIS request
+                    # (its blocks come back) and leave lookahead below - the
+                    # host check is authoritative (branch_select's device
+                    # error word marks the same case)
+                    q.error = (f"decision lookahead: sampled token {t} is not an outcome "
+                               f"of the pending choice")
+                    finished.append(q)
+                    bad = True
+                    continue
                 tok, ids, fin, _, dec = br
                 if q.t_first is None:
                     q.t_first = now = now or time.perf_counter()
@@ -1123,7 +1133,7 @@ class LLMEngine:
         self.stats["update_s"] += time.perf_counter() - t2
         live = [q for q in cur.seqs if not q.done]
         nxt = None
-        if live and self._look_eligible(live, allow_waiting=self.LOOKAHEAD_ADMIT):
+        if live and not bad and self._look_eligible(live, allow_waiting=self.LOOKAHEAD_ADMIT):
             with span("engine.launch"):
                 nxt = self._launch_branch(cur, live, admit=self.LOOKAHEAD_ADMIT)
         if nxt is not None:

@@ -126,6 +126,13 @@ class LocalPlanner(Planner):
     #     (16, 64, ... 16384, then every 16384), so the order - and the cached
     #     blocks - stay put between snapshots;
     #   name - name order; score - the similarity order.
+    # Reproducibility: under "popular" the prompt of an intent depends on the
+    # process's earlier traffic (the rank snapshot), so the same intent can
+    # plan differently on another replica or later in the run.  Sampled plans
+    # (temperature 0.2, control_plane.py:72) depend on that history anyway -
+    # the Gumbel counter is (request uid, sample) - so for reproducible plans
+    # run temperature 0 with MCP_RETRIEVAL_ORDER=name: the prompt is then a
+    # function of the intent and the registry only.
     # 10k-service registry, 320 synthetic intents, top-32, a CPU replay of the
     # prompts' 64-token block chains: 69 % of the prefix blocks shared in
     # popularity order, 53 % in name order, 34 % in score order

@@ -377,6 +377,9 @@ def e2e(n: int, model: str, runs: int, conc: int, churn: int):
         report("single", lats, wall, 1)
         lats, wall = phase(c, conc, 100_000)
         report("concurrent", lats, wall, conc)
+        if os.environ.get("MCP_E2E_CHURN_PHASE", "1") == "0":     # A/B sweeps: two phases only
+            planner._stop.set()
+            return
         stop = threading.Event()
         extra = [dict(synthetic_registry(1, seed=10_000 + i)[0]) for i in range(churn)]
 

@@ -844,3 +844,38 @@ def test_prep_thread_gives_the_same_plans(monkeypatch):
         outs.append(asyncio.run(serve()))
         asyncio.run(planner.aclose())
     assert outs[0] == outs[1]
+
+
+def test_lookahead_outcome_mismatch_fails_only_that_request(monkeypatch):
+    """a sampled token that is no outcome of the pending choice
+    (impossible under the grammar's allowed sets; forced here) fails only that
+    request with a clear error, the engine leaves lookahead and finishes the
+    others, and every KV block comes back."""
+    from mcp_amd.engine import native
+    if not native.available():
+        pytest.skip("native runtime not built")
+    reg = MemoryRegistry(synthetic_registry(7, seed=4))
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, lookahead=True)
+    planner = LocalPlanner(eng, reg, max_nodes=4, min_nodes=2)
+    real = eng._wait_tokens
+    state = {"done": False}
+
+    def corrupt(L):
+        toks = real(L)
+        import inspect
+        if not state["done"] and inspect.stack()[1].function == "_step_look" and toks:
+            state["done"] = True
+            toks = list(toks)
+            toks[0] = -12345                          # no outcome carries this token
+        return toks
+    monkeypatch.setattr(eng, "_wait_tokens", corrupt)
+    seqs = planner.submit_many([synthetic_intent(i) for i in range(3)])
+    eng.run()
+    assert state["done"], "lookahead never ran"
+    errs = [q for q in seqs if q.error]
+    assert len(errs) == 1 and "not an outcome" in errs[0].error
+    assert all(q.done for q in seqs) and sum(q.result is not None for q in seqs) == 2
+    assert not eng._look and not eng.inflight
+    eng.drop_prefixes()
+    assert eng.alloc.num_free == eng.kv.num_blocks
