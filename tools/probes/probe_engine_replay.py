@@ -1,7 +1,7 @@
 """Host time of the engine's own hipGraph replays (config 2 shape): which part
 of the captured decode step keeps ``CUDAGraph.replay()`` on the host for the
 whole forward (r5g1: 3.6 ms per replay in engine.launch, against ~80 us for a
-graph of 192 of the same GEMM kernels, bench_data/probe_graph_launch.py).
+graph of 192 of the same GEMM kernels, tools/probes/probe_graph_launch.py).
 
 For the buckets the single-intent run used: the replay as captured, and
 re-captures of the same step's pieces (forward only, the sampler only, the

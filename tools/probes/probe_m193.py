@@ -3,7 +3,7 @@ the plan's code for the bucket (timed at M = 256, where the AGPR height is
 used).  Cold-weight times of production vs the AGPR heights at these M."""
 import json, os, sys
 import torch
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
 import mcp_amd.ops as ops
 L = ops.lib()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
