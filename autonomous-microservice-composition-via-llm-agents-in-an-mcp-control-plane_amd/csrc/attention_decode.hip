@@ -74,12 +74,27 @@ struct DecArgs {
   int* split_cnt;          // per (block row, kv head) arrival tickets, zero between launches
   int tpw;                 // tiles per wave
   int rel;                 // 1: block z covers the own tiles [kt0 + z C, ...), kt0 = kv_begin / 64
+  int sc1_out;             // 1: out rows stored write-through (sc1) - the fused o-projection's hand-off
 };
+
+// one 16-B piece of an output row: plain, or write-through (sc1: leaves the
+// XCD's L2 at once, MI355X_MICROARCH.md "Valid forms" producer condition (2))
+DEV void store_out(const DecArgs& a, size_t elem, const bf16x8& v) {
+  if (a.sc1_out) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (unsigned)(elem * 2), 0, 16);
+  } else {
+    *reinterpret_cast<bf16x8*>(a.out + elem) = v;
+  }
+}
 
 // One block of the decode attention: work item b, kv head kvh, key block z
 // (the grid position of attn_decode_kernel; attn_oproj_kernel maps a flat id).
+// Returns (block-uniform) 1 when this block wrote its item's output rows (the
+// item's only block), 2 when it did as the last arriving block of a split
+// item, 0 when it wrote none.
 template <int G>
-DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const int z) {
+DEV int attn_decode_body(const DecArgs& a, const int b, const int kvh, const int z) {
   constexpr int TPR = 16 / G;                        // tokens per 16-row tile
   __shared__ __attribute__((aligned(16))) bf16 smem[NWV * TILE];   // per wave: V tile, then O
   __shared__ float s_ml[NWV][2][16];                 // per wave: row max, row sum
@@ -140,7 +155,7 @@ DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const in
   const int z_first = a.rel ? 0 : kt0 / C;
   const int z_last = a.rel ? (kt1 - 1 - kt0) / C : (kt1 - 1) / C;
   // padding items / row tiles past the span, blocks wholly outside the own keys
-  if (q0 >= ql || kt1 <= kt0 || z < z_first || z > z_last) return;
+  if (q0 >= ql || kt1 <= kt0 || z < z_first || z > z_last) return 0;
   const int nact = z_last - z_first + 1;
   if (kt_first >= kt0 && kt_first < kt1) load_tile(blk0);
 
@@ -295,7 +310,7 @@ DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const in
         ov[i] = (bf16)acc0[i];
         ov[4 + i] = (bf16)acc1[i];
       }
-      *reinterpret_cast<bf16x8*>(a.out + grow * D + 8 * c8) = ov;
+      store_out(a, grow * D + 8 * c8, ov);
     } else {
       // one of several blocks: its normalised partial, write-through
       const int zr = z - z_first;
@@ -307,7 +322,7 @@ DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const in
                                               (unsigned)(((size_t)zr * a.rows + grow) * 4), 0, 16);
     }
   }
-  if (nact == 1) return;
+  if (nact == 1) return 1;
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();                                   // every partial of this block is out
@@ -319,7 +334,8 @@ DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const in
     s_last = last;
   }
   __syncthreads();
-  if (!s_last || !rvalid) return;
+  if (!s_last) return 0;
+  if (!rvalid) return 2;
   // ---- last arriver: every block's partial in block order (deterministic)
   float mx = -INFINITY;
 #pragma unroll 8
@@ -364,7 +380,8 @@ DEV void attn_decode_body(const DecArgs& a, const int b, const int kvh, const in
     ov[i] = (bf16)(acc0[i] * inv);
     ov[4 + i] = (bf16)(acc1[i] * inv);
   }
-  *reinterpret_cast<bf16x8*>(a.out + grow * D + 8 * c8) = ov;
+  store_out(a, grow * D + 8 * c8, ov);
+  return 2;
 }
 
 template <int G>
@@ -412,8 +429,9 @@ struct OprojArgs {
 
 constexpr int OP_STEP = 128;
 
-template <int KS>                    // k-steps of 128 per wave: K = 4 x 128 x KS
-DEV void oproj_block(const OprojArgs& o, const int j) {
+template <int G, int KS>              // k-steps of 128 per wave: K = 4 x 128 x KS
+DEV void oproj_block(const DecArgs& a, const OprojArgs& o, const int j) {
+  constexpr int TPR = 16 / G;
   __shared__ f32x4 ored[NWV][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -428,23 +446,40 @@ DEV void oproj_block(const OprojArgs& o, const int j) {
     for (int q = 0; q < 4; ++q) w[s][q] = *reinterpret_cast<const bf16x8*>(wrow + s * OP_STEP + 32 * q);
   const int m = min(r, o.M - 1);
   const bf16x4 rr = *reinterpret_cast<const bf16x4*>(o.Y + (size_t)m * o.N + n0 + 4 * g);
-  if (threadIdx.x == 0) {
-    int spins = 0;
-    while (__hip_atomic_load(o.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < o.n_attn) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 24)) {                     // ~seconds: never in a healthy launch
-        __hip_atomic_store(o.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+  if (wave == 0) {
+    // the writers to wait for: one per (item with rows, kv head) - the item's
+    // only block or its last arriving one (attn_decode_body returns nonzero);
+    // an item has rows iff q0 < q_len of its sequence (no cascade here, so
+    // every such item has keys).  Counted on the device: a hipGraph replay's
+    // items are padded, and their real count is only known here
+    int cnt = 0;
+    for (int b = lane; b < o.nitems; b += 64) {
+      const bool wide = b < 4 * a.nwork4;
+      const int s = wide ? a.work_seq4[b >> 2] : a.work_seq1[b - 4 * a.nwork4];
+      const int q0 = wide ? a.work_q04[b >> 2] + (b & 3) * TPR : a.work_q01[b - 4 * a.nwork4];
+      cnt += q0 < a.q_len[s];
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0) {
+      const int expect = cnt * a.Hkv;
+      int spins = 0;
+      while (__hip_atomic_load(o.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < expect) {
+        __builtin_amdgcn_s_sleep(4);
+        if (++spins > (1 << 23)) {                   // ~seconds: never in a healthy launch
+          __hip_atomic_store(o.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const int n_o = o.N / 16;
     const int old = __hip_atomic_fetch_add(o.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == n_o - 1) {                            // every block is past its poll
+    if (old == n_o - 1) {                            // every block is past its wait
       __hip_atomic_store(o.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -490,18 +525,19 @@ template <int G, int KS>
 __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(const DecArgs a, const OprojArgs o) {
   const int f = blockIdx.x;
   if (f >= o.n_attn) {
-    oproj_block<KS>(o, f - o.n_attn);
+    oproj_block<G, KS>(a, o, f - o.n_attn);
     return;
   }
   const int rest = f / o.nitems;
-  attn_decode_body<G>(a, f - rest * o.nitems, rest % a.Hkv, rest / a.Hkv);
-  // publish this block's rows (whichever path it took through the body)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  const int wrote = attn_decode_body<G>(a, f - rest * o.nitems, rest % a.Hkv, rest / a.Hkv);
+  // hand-off of this block's rows (block-uniform: only writers signal, so the
+  // padded items of a graph replay cost no atomics): sc1 stores drained by
+  // every wave, a barrier, one relaxed agent-scope add; the reader's acquire
+  // completes it (MI355X_MICROARCH.md "Valid forms", producer (2) + (3))
+  if (wrote) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(o.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(o.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -637,6 +673,7 @@ static int launch_attn_decode_impl(const void* q, const void* k_cache, const voi
         oproj->M < 1 || oproj->M > 16 || oproj->M * Hq != rows)
       return 7;
     OprojArgs o = *oproj;
+    a.sc1_out = 1;
     o.X = a.out;
     o.sync = cnt + SPLIT_TICKETS;
     o.err = cnt + SPLIT_TICKETS + 2;
