@@ -425,6 +425,8 @@ struct OprojArgs {
   int* err;                          // nonzero: a poll timed out
   int M, N, K;
   int n_attn, nitems;                // attention blocks, attention grid x extent
+  int pace;                          // weight-load pacing (MCP_AOP_PACE): s_sleep(32) x pace between
+                                     // k-steps; < 0: load the weights only after the wait
 };
 
 constexpr int OP_STEP = 128;
@@ -437,13 +439,20 @@ DEV void oproj_block(const DecArgs& a, const OprojArgs& o, const int j) {
   const int r = lane & 15, g = lane >> 4;
   const int n0 = j * 16;
   const int kb = wave * KS * OP_STEP;
-  // the weight slice (16 rows x K / 4 per wave) into registers, all in flight
+  // the weight slice (16 rows x K / 4 per wave) into registers, all in
+  // flight while the attention runs (paced: the attention's own round trips
+  // queue behind this stream in HBM)
   const bf16* wrow = o.W + (size_t)(n0 + r) * o.K + kb + 8 * g;
   bf16x8 w[KS][4];
+  auto load_w = [&]() {
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < KS; ++s) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) w[s][q] = *reinterpret_cast<const bf16x8*>(wrow + s * OP_STEP + 32 * q);
+      for (int q = 0; q < 4; ++q) w[s][q] = *reinterpret_cast<const bf16x8*>(wrow + s * OP_STEP + 32 * q);
+      for (int p = 0; p < o.pace; ++p) __builtin_amdgcn_s_sleep(32);
+    }
+  };
+  if (o.pace >= 0) load_w();
   const int m = min(r, o.M - 1);
   const bf16x4 rr = *reinterpret_cast<const bf16x4*>(o.Y + (size_t)m * o.N + n0 + 4 * g);
   if (wave == 0) {
@@ -476,6 +485,7 @@ DEV void oproj_block(const DecArgs& a, const OprojArgs& o, const int j) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (o.pace < 0) load_w();
   if (threadIdx.x == 0) {
     const int n_o = o.N / 16;
     const int old = __hip_atomic_fetch_add(o.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -673,6 +683,8 @@ static int launch_attn_decode_impl(const void* q, const void* k_cache, const voi
         oproj->M < 1 || oproj->M > 16 || oproj->M * Hq != rows)
       return 7;
     OprojArgs o = *oproj;
+    static const int pace = getenv("MCP_AOP_PACE") ? atoi(getenv("MCP_AOP_PACE")) : 0;
+    o.pace = pace;
     a.sc1_out = 1;
     o.X = a.out;
     o.sync = cnt + SPLIT_TICKETS;
