@@ -323,8 +323,13 @@ def prefix_splits(pre_tokens: int, pre_keys: int, hkv: int, num_cus: int = 256) 
 
 
 # decode attention + o-projection in one launch (csrc/attention_decode.hip
-# attn_oproj_kernel; MCP_ATTN_OPROJ=0 disables)
-_ATTN_OPROJ = os.environ.get("MCP_ATTN_OPROJ", "1") == "1"
+# attn_oproj_kernel; MCP_ATTN_OPROJ=1 enables).  Measured and off: config 2
+# p50 86.2 ms unfused vs 88.8-89.0 fused (weights preloaded) and 91.2 (loaded
+# after the wait): the in-launch hand-off (writer count, poll, acquire, the
+# attention rows re-read) costs more than the launch boundary it removes, and
+# the preloaded weight stream slows the attention's round trips
+# (profiles/config2_attn_oproj_fused_ab_r6.md)
+_ATTN_OPROJ = os.environ.get("MCP_ATTN_OPROJ", "0") == "1"
 
 
 def _decode_lists(q, k_cache, meta):
