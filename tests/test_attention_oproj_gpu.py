@@ -3,7 +3,9 @@ attn_oproj_kernel): every fused call of a config-2 style run is checked in
 place against the two ops it replaces (paged_attention, then the residual
 GEMM with its fused-norm statistic) - themselves checked against fp32 in
 test_kernels_gpu.py - and against an fp32 reference of the o-projection; the
-plans match the unfused engine's, eager and hipGraph-replayed.
+plans match the unfused engine's, eager and hipGraph-replayed.  The fused
+form is off by default (measured slower on config 2,
+profiles/config2_attn_oproj_fused_ab_r6.md); these tests switch it on.
 
 Reference: the planner call it serves, control_plane.py:69-73."""
 import pytest
@@ -31,6 +33,7 @@ def _plans(model, reg, intents, graphs):
 
 
 def test_fused_calls_match_the_unfused_ops(model, monkeypatch):
+    monkeypatch.setattr(ops, "_ATTN_OPROJ", True)          # off by default (measured slower)
     reg = MemoryRegistry(synthetic_registry(10, seed=1))
     real = ops.attention_oproj
     checked = []
