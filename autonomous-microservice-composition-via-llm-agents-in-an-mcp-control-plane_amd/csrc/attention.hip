@@ -105,6 +105,11 @@ struct AttnArgs {
   // block id % 8 (the XCD) is the kv head when Hkv = 8: each XCD's L2 then
   // holds one head's prefix K/V (352 KiB) instead of all eight
   int head_major;
+  // shared-prefix pass: lazy max rescaling (MCP_ATTN_LAZY_RESCALE) - the
+  // running max and the O / row-sum rescale are updated only when some row of
+  // the wave's tile grows its max by more than LAZY_T (log2 units); otherwise
+  // the scores are exponentiated against the stale max (p <= 2^LAZY_T)
+  int lazy;
   // MIXED split launch (split-KV steps): blocks [0, nwork4) run the 4-wave
   // list (work_seq / work_q0), blocks [nwork4, ...) the 1-wave list
   // (work_seq1 / work_q01) as 4-wave blocks whose waves 1-3 hold no rows;
@@ -527,6 +532,8 @@ void attn_kernel(const AttnArgs a) {
 // did not overlap; profiles/attention_tuning.md).  B reads the V tile of the
 // previous step while the next tile is staged, so the ring has 3 buffers
 // (96 KiB); every wave passes the same barriers.
+constexpr float LAZY_T = 8.f;                // lazy rescale: p <= 2^8 against a stale max
+
 template <int NW, int G, int RT, bool PP = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(RT >= 4 ? 1 : 2)))
 void attn_prefix_kernel(const AttnArgs a) {
@@ -646,20 +653,29 @@ void attn_prefix_kernel(const AttnArgs a) {
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float m_new = fmaxf(m_run[r], tmax * c);
-      const float alpha = fexp2(m_run[r] - m_new);
-      m_run[r] = m_new;
+      // lazy: keep the stale max unless some row of this wave's tile grew it
+      // by more than LAZY_T (wave-uniform test, so the rescale is skipped
+      // for the whole wave - the softmax chain loses the exp and the 32 + 1
+      // multiplies of the O / sum rescale on most tiles)
+      const bool rescale = !a.lazy || __builtin_amdgcn_ballot_w64(m_new > m_run[r] + LAZY_T) != 0;
       float psum = 0.f;
+      if (rescale) {
+        const float alpha = fexp2(m_run[r] - m_new);
+        m_run[r] = m_new;
+        l_part[r] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
+      }
+      const float mu = m_run[r];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = fexp2(fmaf(sacc[r][nt][e], c, -m_new));
+          const float p = fexp2(fmaf(sacc[r][nt][e], c, -mu));
           psum += p;
           pf[r][nt >> 1][(nt & 1) * 4 + e] = (bf16)p;
         }
-      l_part[r] = l_part[r] * alpha + psum;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[r][dt] *= alpha;
+      l_part[r] += psum;
     }
   };
   // ---- O^T += V^T P^T: each transposed V fragment feeds the RT row tiles
@@ -1004,6 +1020,10 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
 
 int attn_tokens_per_item(int nw, int group) { return nw * (16 / group); }
 
+// shared-prefix pass lazy rescaling: -1 = MCP_ATTN_LAZY_RESCALE (default 0)
+static int g_lazy_rescale = -1;
+void attn_lazy_rescale(int on) { g_lazy_rescale = on; }
+
 int* attn_split_counters() { return split_counters(); }
 
 int attn_split_init() {
@@ -1146,6 +1166,9 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
   // MCP_ATTN_PREFIX_HEAD_MAJOR=0: token-major grid (A/B)
   static const int head_major = getenv("MCP_ATTN_PREFIX_HEAD_MAJOR") ? atoi(getenv("MCP_ATTN_PREFIX_HEAD_MAJOR")) : 1;
   a.head_major = head_major;
+  if (g_lazy_rescale < 0)
+    g_lazy_rescale = getenv("MCP_ATTN_LAZY_RESCALE") ? atoi(getenv("MCP_ATTN_LAZY_RESCALE")) : 0;
+  a.lazy = g_lazy_rescale;
   ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s, nsplit))
   return 0;
 }

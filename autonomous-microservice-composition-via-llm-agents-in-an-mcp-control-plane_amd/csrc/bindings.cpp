@@ -941,6 +941,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("work_q04"), py::arg("work_seq1"), py::arg("work_q01"), py::arg("scale"),
         py::arg("nz"), py::arg("split_o"), py::arg("split_lse"), py::arg("wo"), py::arg("x"),
         py::arg("ss_out") = py::none());
+  m.def("attn_lazy_rescale", &attn_lazy_rescale, "shared-prefix attention: lazy max rescaling on / off");
   m.def("gemm_probe", &gemm_probe, "GEMM power-ladder rung (gemm256d.hip PROBE 0-3)");
   m.def("attn_oproj_error", &attn_oproj_error, "nonzero: a fused o-projection wait timed out");
   m.def("attn_decode_blocks", &attn_decode_blocks, "grid z of paged_attention_decode for a table width");

@@ -162,6 +162,7 @@ int launch_paged_attention(const void* q, const void* k_cache, const void* v_cac
                            float* split_o = nullptr, float* split_lse = nullptr, int rows = 0,
                            float* own_lse = nullptr);
 int attn_split_init();
+void attn_lazy_rescale(int on);   // shared-prefix pass: lazy max rescaling (1) or exact (0)
 // decode-sized split-KV steps (attention_decode.hip): grid (items, Hkv, nz),
 // nz = attn_decode_blocks(max_blocks); nonzero = not launched
 int attn_decode_blocks(int max_blocks);

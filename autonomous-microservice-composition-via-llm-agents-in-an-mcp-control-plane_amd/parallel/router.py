@@ -970,6 +970,14 @@ class SharedRouter(ReplicaRouter):
 
 
 def default_devices(n: int) -> List[str]:
+    """One device per replica: cuda:0 .. cuda:n-1 (as many as exist).
+    ``MCP_REPLICA_DEVICES`` ("cuda:0,cuda:0", ...) places them explicitly -
+    e.g. several replicas sharing one GPU for a one-GPU test of the
+    multi-replica paths (size their KV pools with MCP_KV_BLOCKS then)."""
+    forced = os.environ.get("MCP_REPLICA_DEVICES")
+    if forced:
+        devs = [d.strip() for d in forced.split(",") if d.strip()]
+        return (devs * n)[:n]
     import torch
     if torch.cuda.is_available():
         return [f"cuda:{i}" for i in range(min(n, torch.cuda.device_count()))]

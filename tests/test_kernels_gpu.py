@@ -555,12 +555,24 @@ def test_prefix_pass_ping_pong_form(T, P, monkeypatch):
     assert rel_err(outs[1][0], exp_o) < 2e-2
 
 
-@pytest.mark.parametrize("rt", ["1", "2"])
-def test_prefix_pass_growing_max(rt, monkeypatch):
+@pytest.fixture
+def lazy_rescale():
+    """Switch the prefix pass's lazy max rescaling; restored afterwards."""
+    def set_(on):
+        ops.lib().attn_lazy_rescale(int(on))
+    yield set_
+    ops.lib().attn_lazy_rescale(-1)
+
+
+@pytest.mark.parametrize("lazy", [0, 1])
+@pytest.mark.parametrize("rt", ["1", "2", "4"])
+def test_prefix_pass_growing_max(rt, lazy, monkeypatch, lazy_rescale):
     """Keys whose scale grows tile by tile (the online-softmax max jumps by
     large and small amounts between tiles): O and LSE still match fp32
-    softmax attention."""
+    softmax attention - also with lazy rescaling (the max and the O / sum
+    rescale held back while it grows by <= 2^8; rt 2 / 4 = attn_prefix_kernel)."""
     monkeypatch.setenv("MCP_ATTN_PREFIX_RT", rt)
+    lazy_rescale(lazy)
     torch.manual_seed(12)
     Hq, Hkv, D, P, T = 32, 8, 128, 768, 200
     n_pre = P // 64
