@@ -270,7 +270,7 @@ class GraphRunner:
         # thread_local: another host thread's work on its own stream (the
         # planner's prep thread running a retrieval search, MCP_PREP_THREAD)
         # may proceed while this thread captures a lazily built bucket
-        mode = "thread_local" if os.environ.get("MCP_PREP_THREAD", "0") == "1" else "global"
+        mode = "thread_local" if os.environ.get("MCP_PREP_THREAD", "1") == "1" else "global"
         with torch.cuda.graph(g, pool=self._pool, capture_error_mode=mode):
             e.tokens = self._body(e)
         self._pool = g.pool()
