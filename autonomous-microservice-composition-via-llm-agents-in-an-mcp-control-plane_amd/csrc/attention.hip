@@ -534,7 +534,13 @@ void attn_kernel(const AttnArgs a) {
 // (96 KiB); every wave passes the same barriers.
 constexpr float LAZY_T = 8.f;                // lazy rescale: p <= 2^8 against a stale max
 
-template <int NW, int G, int RT, bool PP = false>
+// SW: the K|V image's 16-B chunk swizzle.  false: chunk ^ (row & 15) (the
+// image of attn_kernel); true: chunk ^ ((row & 7) << 1), which keeps the K
+// row reads (ds_read_b128) conflict-free and makes the transposed V reads
+// (ds_read_b64_tr_b16: a 32-lane half reads 8 consecutive keys) conflict-free
+// too - 2-way on the first image (tools/lds_banks.py; round-5 PMC: LDS
+// bank-conflict cycles 2.9 M against 2.6 M active on this pass)
+template <int NW, int G, int RT, bool PP = false, bool SW = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(RT >= 4 ? 1 : 2)))
 void attn_prefix_kernel(const AttnArgs a) {
   static_assert(!PP || NW == 8, "ping-pong: two groups of 4 waves");
@@ -580,9 +586,10 @@ void attn_prefix_kernel(const AttnArgs a) {
   // 2 x PIECES / NW VGPRs live across the loop and the 4-wave form spilled,
   // while the buffer form measured ~3 % slower on the 8-wave one (r5c7)
   constexpr bool BUF_DMA = NW == 4 || PP;
+  auto pswz = [](int row) { return SW ? ((row & 7) << 1) : (row & 15); };
   unsigned voff[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) voff[i] = (unsigned)((srow * D + (((lane & 15) ^ (4 * i + srow)) << 3)) * 2);
+  for (int i = 0; i < 4; ++i) voff[i] = (unsigned)((srow * D + (((lane & 15) ^ pswz(4 * i + srow)) << 3)) * 2);
   auto stage = [&](int kt, int buf) {
     const size_t blk = (size_t)bt_at(kt);
     const size_t off = (blk * Hkv + kvh) * (size_t)TILE;
@@ -605,7 +612,7 @@ void attn_prefix_kernel(const AttnArgs a) {
         const int p = wave * (PIECES / NW) + i;
         const int tile = p >> 4, pr = p & 15;
         const int row = pr * 4 + srow;
-        const int chunk = (lane & 15) ^ (row & 15);
+        const int chunk = (lane & 15) ^ pswz(row);
         glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
       }
     }
@@ -633,7 +640,7 @@ void attn_prefix_kernel(const AttnArgs a) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int cc = ks * 4 + fq;
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * D + ((cc ^ (row & 15)) << 3));
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + row * D + ((cc ^ pswz(row)) << 3));
 #pragma unroll
         for (int r = 0; r < RT; ++r) sacc[r][nt] = mfma16x16x32(kf, qf[r][ks], sacc[r][nt]);
       }
@@ -688,8 +695,8 @@ void attn_prefix_kernel(const AttnArgs a) {
       for (int k2 = 0; k2 < 2; ++k2) {
         const int key0 = k2 * 32 + fq * 4 + tq;
         const int key1 = key0 + 16;
-        const bf16x4 v0 = tr_read(Vl + key0 * D + ((chunk ^ (key0 & 15)) << 3) + half);
-        const bf16x4 v1 = tr_read(Vl + key1 * D + ((chunk ^ (key1 & 15)) << 3) + half);
+        const bf16x4 v0 = tr_read(Vl + key0 * D + ((chunk ^ pswz(key0)) << 3) + half);
+        const bf16x4 v1 = tr_read(Vl + key1 * D + ((chunk ^ pswz(key1)) << 3) + half);
         const bf16x8 vf = bf16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 #pragma unroll
         for (int r = 0; r < RT; ++r) o[r][dt] = mfma16x16x32(vf, pf[r][k2], o[r][dt]);
@@ -967,6 +974,12 @@ static bool prefix_pp() {
   const char* e = getenv("MCP_ATTN_PREFIX_PP");
   return e && e[0] == '1';
 }
+// MCP_ATTN_PREFIX_SWZ=1: the conflict-free K|V image (attn_prefix_kernel SW)
+// for the lock-step forms (read per launch: the tests compare both images)
+static bool prefix_swz() {
+  const char* e = getenv("MCP_ATTN_PREFIX_SWZ");
+  return e && e[0] == '1';
+}
 
 // Shared-prefix pass: 8 waves per block (32 tokens x G heads) -> half the K/V
 // tile staging per query of the 4-wave item and 4 waves per SIMD at 2 blocks/CU
@@ -995,10 +1008,14 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
     };
     if (rt == 4)
       attn_prefix_kernel<4, G, 4><<<grid_for(4 * 4 * (16 / G)), 256, 0, s>>>(a);
+    else if (prefix_nw(a.pre_tokens, 8 * 2 * (16 / G), a.Hkv) == 4 && prefix_swz())
+      attn_prefix_kernel<4, G, 2, false, true><<<grid_for(4 * 2 * (16 / G)), 256, 0, s>>>(a);
     else if (prefix_nw(a.pre_tokens, 8 * 2 * (16 / G), a.Hkv) == 4)
       attn_prefix_kernel<4, G, 2><<<grid_for(4 * 2 * (16 / G)), 256, 0, s>>>(a);
     else if (prefix_pp())
       attn_prefix_kernel<8, G, 2, true><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
+    else if (prefix_swz())
+      attn_prefix_kernel<8, G, 2, false, true><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     else
       attn_prefix_kernel<8, G, 2><<<grid_for(8 * 2 * (16 / G)), 512, 0, s>>>(a);
     return;

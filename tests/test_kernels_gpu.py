@@ -555,6 +555,37 @@ def test_prefix_pass_ping_pong_form(T, P, monkeypatch):
     assert rel_err(outs[1][0], exp_o) < 2e-2
 
 
+@pytest.mark.parametrize("T,P", [(300, 704), (2100, 640), (4096, 704)])
+def test_prefix_pass_conflict_free_image(T, P, monkeypatch):
+    """MCP_ATTN_PREFIX_SWZ=1: the prefix pass's K|V image swizzled chunk ^
+    ((row & 7) << 1) (conflict-free transposed V reads) gives the same bits as
+    the chunk ^ (row & 15) image - only addresses change - in the 4- and
+    8-wave lock-step forms, and matches fp32 attention."""
+    monkeypatch.setenv("MCP_ATTN_PREFIX_RT", "2")
+    torch.manual_seed(17)
+    Hq, Hkv, D = 32, 8, 128
+    n_pre = P // 64
+    kc, vc = _cache(n_pre + 2, Hkv)
+    pre_bt = torch.randperm(n_pre + 2, device=DEV)[:n_pre].to(torch.int32)
+    q = torch.randn(T, Hq, D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    outs = []
+    for sw in ("0", "1"):
+        monkeypatch.setenv("MCP_ATTN_PREFIX_SWZ", sw)
+        out = torch.empty_like(q)
+        lse = torch.empty(T, Hq, device=DEV, dtype=torch.float32)
+        ops.lib().prefix_attention(q, kc, vc, out, lse, pre_bt, P, T, scale)
+        torch.cuda.synchronize()
+        outs.append((out, lse))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    G = Hq // Hkv
+    k = kc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    v = vc[pre_bt.long()].float().permute(1, 0, 2, 3).reshape(Hkv, P, D)
+    s_ = torch.einsum("thgd,hpd->thgp", q.float().view(T, Hkv, G, D), k) * scale
+    exp_o = torch.einsum("thgp,hpd->thgd", torch.softmax(s_, -1), v).reshape(T, Hq, D)
+    assert rel_err(outs[1][0], exp_o) < 2e-2
+
+
 @pytest.fixture
 def lazy_rescale():
     """Switch the prefix pass's lazy max rescaling; restored afterwards."""
