@@ -1037,7 +1037,9 @@ void attn_prefix_dispatch(const AttnArgs& a, hipStream_t s, int nsplit = 1) {
 
 int attn_tokens_per_item(int nw, int group) { return nw * (16 / group); }
 
-// shared-prefix pass lazy rescaling: -1 = MCP_ATTN_LAZY_RESCALE (default 0)
+// shared-prefix pass lazy rescaling: -1 = MCP_ATTN_LAZY_RESCALE (default 1:
+// tools/bench_attention.py 16, same box alternated, prefix pass 77.7 / 78.3
+// -> 75.3 / 75.7 us, headline within noise; profiles/attention_prefix_r6.md)
 static int g_lazy_rescale = -1;
 void attn_lazy_rescale(int on) { g_lazy_rescale = on; }
 
@@ -1184,7 +1186,7 @@ int launch_prefix_attention(const void* q, const void* k_cache, const void* v_ca
   static const int head_major = getenv("MCP_ATTN_PREFIX_HEAD_MAJOR") ? atoi(getenv("MCP_ATTN_PREFIX_HEAD_MAJOR")) : 1;
   a.head_major = head_major;
   if (g_lazy_rescale < 0)
-    g_lazy_rescale = getenv("MCP_ATTN_LAZY_RESCALE") ? atoi(getenv("MCP_ATTN_LAZY_RESCALE")) : 0;
+    g_lazy_rescale = getenv("MCP_ATTN_LAZY_RESCALE") ? atoi(getenv("MCP_ATTN_LAZY_RESCALE")) : 1;
   a.lazy = g_lazy_rescale;
   ATTN_SWITCH_G(Hq / Hkv, attn_prefix_dispatch<GG>(a, s, nsplit))
   return 0;
