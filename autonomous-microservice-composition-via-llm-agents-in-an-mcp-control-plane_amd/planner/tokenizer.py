@@ -141,7 +141,11 @@ class Tokenizer:
         return cls(path, bos_id=special("bos_token"), eos_id=special("eos_token"),
                    vocab_size=vocab, synthetic=False)
 
-    @functools.lru_cache(maxsize=65536)
+    # repeated texts only (registry prefixes, repeated intents): every unique
+    # intent's suffix also passes through here, so a large cache is ~700 B per
+    # request of dead entries (65,536 entries held ~50 MB in a serving
+    # replica: the RSS growth of the round-6 950 s soak)
+    @functools.lru_cache(maxsize=2048)
     def _encode_cached(self, text: str) -> tuple:
         return tuple(self._tok.encode(text, add_special_tokens=False).ids)
 

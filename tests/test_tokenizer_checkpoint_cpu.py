@@ -98,3 +98,15 @@ def test_vocab_larger_than_model_is_refused(tmp_path, ckpt):
     (d / "config.json").write_text(json.dumps(cfg))
     with pytest.raises(ValueError):
         Tokenizer.from_pretrained(str(d))
+
+
+def test_encode_cache_stays_small():
+    """Every unique intent's suffix passes through the tokenizer's encode
+    cache: a large bound held ~700 B per request of dead entries (~50 MB in a
+    serving replica at 65,536 entries, the RSS growth of the round-6 soak)."""
+    from mcp_amd.planner.tokenizer import get_tokenizer
+    tok = get_tokenizer()
+    for i in range(3000):
+        tok.encode(f"\nUser intent: “book trip {i}”\n\nJSON DAG:")
+    info = type(tok)._encode_cached.cache_info()
+    assert info.maxsize <= 4096 and info.currsize <= 4096
