@@ -253,7 +253,7 @@ void gemm_plan_set_silu_py(int64_t N, int64_t K, const std::vector<int64_t>& cod
   std::vector<int> c(codes.begin(), codes.end());
   for (int v : c)
     TORCH_CHECK(v == -1 || (v >= 1 && v <= 5) || (v >= 101 && v <= 116) || v == 200 ||
-                    (v >= 300 && v < 364) || (v >= 1000 && v < 1000 + 16 * 16),
+                    (v >= 300 && v < 364) || (v >= 401 && v <= 405) || (v >= 1000 && v < 1000 + 16 * 16),
                 "gemm plan silu: -1 or a launch_gemm_silu_algo code");
   gemm_plan_set_silu((int)N, (int)K, c.data(), (int)c.size());
 }
@@ -534,6 +534,24 @@ bool paged_attention_decode(const at::Tensor& q, const at::Tensor& k_cache, cons
   if (rc != 0) return false;
   check_launch("paged_attention_decode");
   return true;
+}
+
+// K-half split AGPR GEMM (gemm256d.hip SPLIT 2), plain (R none) or + residual
+// R; tests / tuning.  Returns the launcher's code (0 = launched)
+int64_t gemm_split2(const at::Tensor& X, const at::Tensor& W, at::Tensor& Y,
+                    const c10::optional<at::Tensor>& R, int64_t bm) {
+  CHECK_BF16_TENSOR(X); CHECK_BF16_TENSOR(W); CHECK_BF16_TENSOR(Y);
+  const int M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && Y.size(0) == M && Y.size(1) == N, "gemm_split2: X [M, K], W [N, K], Y [M, N]");
+  if (R) {
+    CHECK_BF16_TENSOR((*R));
+    TORCH_CHECK(R->size(0) == M && R->size(1) == N, "gemm_split2: R [M, N]");
+  }
+  const int rc = launch_gemm_tn_256d_split2(X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                            R ? R->data_ptr() : nullptr, M, N, K, R ? 1 : 0, (int)bm,
+                                            stream());
+  if (rc == 0) check_launch("gemm_split2");
+  return rc;
 }
 
 // GEMM power ladder rung (gemm256d.hip PROBE): Y [M, N] (epi 0) or [M, N/2] (epi 2)
@@ -942,6 +960,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("nz"), py::arg("split_o"), py::arg("split_lse"), py::arg("wo"), py::arg("x"),
         py::arg("ss_out") = py::none());
   m.def("attn_lazy_rescale", &attn_lazy_rescale, "shared-prefix attention: lazy max rescaling on / off");
+  m.def("gemm_split2", &gemm_split2, "AGPR GEMM, K halves over two workgroups per tile (tests / tuning)",
+        py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none(), py::arg("bm") = 256);
   m.def("gemm_probe", &gemm_probe, "GEMM power-ladder rung (gemm256d.hip PROBE 0-3)");
   m.def("attn_oproj_error", &attn_oproj_error, "nonzero: a fused o-projection wait timed out");
   m.def("attn_decode_blocks", &attn_decode_blocks, "grid z of paged_attention_decode for a table width");

@@ -295,3 +295,96 @@ DEV void store_wide(const f32x4 (&acc)[MT][8], RS rsY, const bf16* __restrict__ 
     }
   }
 }
+
+// store_wide plus ``sl`` (gemm256d.hip SPLIT 2): the other K half's fp32 partials, added to
+// the accumulators here, one row tile at a time, two row tiles of loads in
+// flight (a separate add pass over all MT x 8 accumulators makes hipcc copy
+// them out of the AGPRs at once and spill): f32x4 r = (mt, nt) of this lane
+// sits at byte r * 4096 + lane_off of the slab, read with sc1 loads.
+template <class RS>
+struct SlabIn {
+  static constexpr bool on = true;
+  RS rs;
+  unsigned lane_off;
+};
+template <int EPI, int MT, class RS, class NE, class SL>
+DEV void store_wide_slab(const f32x4 (&acc)[MT][8], RS rsY, const bf16* __restrict__ R, int M, int ldy,
+                         int mb, int col0, int fr, int fq, const float* rsc, const NE& ne,
+                         const SL& sl) {
+  constexpr int NPAIR = EPI == 2 ? 2 : 4;
+  f32x4 pre[2][SL::on ? 8 : 1];
+  auto slab_load = [&](int mt, int b) {
+    if constexpr (SL::on) {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+        pre[b][nt] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(sl.rs, sl.lane_off, (mt * 8 + nt) * 4096, 16));
+    }
+  };
+  if constexpr (SL::on) {
+    slab_load(0, 0);
+    if (MT > 1) slab_load(1, 1);
+  }
+  const int lcol = 16 * (fq & 1) + 8 * (fq >> 1);
+  bf16x8 rres[EPI == 1 ? MT * NPAIR : 1];
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p) {
+        const int m = min(mb + mt * 16 + fr, M - 1);
+        rres[mt * NPAIR + p] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldy + col0 + 32 * p + lcol);
+      }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mb + mt * 16 + fr;
+    float ss = 0.f;
+    f32x4 sum[SL::on ? 8 : 1];
+    if constexpr (SL::on) {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) sum[nt] = acc[mt][nt] + pre[mt & 1][nt];
+      if (mt + 2 < MT) slab_load(mt + 2, mt & 1);
+    }
+    auto av = [&](int nt) -> f32x4 {
+      if constexpr (SL::on) return sum[nt];
+      else return acc[mt][nt];
+    };
+#pragma unroll
+    for (int p = 0; p < NPAIR; ++p) {
+      bf16x4 oa, ob;
+      if constexpr (EPI == 2) {
+        const float s = rsc[mt];
+        const f32x4 ga = av(4 * p) * s, ua = av(4 * p + 1) * s;
+        const f32x4 gb = av(4 * p + 2) * s, ub = av(4 * p + 3) * s;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          oa[e] = (bf16)(ga[e] / (1.f + __expf(-ga[e])) * ua[e]);
+          ob[e] = (bf16)(gb[e] / (1.f + __expf(-gb[e])) * ub[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          oa[e] = (bf16)av(2 * p)[e];
+          ob[e] = (bf16)av(2 * p + 1)[e];
+        }
+      }
+      u32x2 a = __builtin_bit_cast(u32x2, oa), b = __builtin_bit_cast(u32x2, ob);
+      swap_col_pairs(a, b);
+      bf16x8 v = __builtin_bit_cast(bf16x8, u32x4{a.x, a.y, b.x, b.y});
+      if constexpr (EPI == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] + (float)rres[mt * NPAIR + p][e]);
+        if (ne.ss_out) ss += m < M ? sumsq_bf16x8(v) : 0.f;
+      }
+      const unsigned off = (unsigned)(((size_t)m * ldy + col0 + 32 * p + lcol) * 2);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsY,
+                                             m < M ? off : 0x80000000u, 0, 0);
+    }
+    if (EPI == 1 && ne.ss_out) {
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (fq == 0 && m < M) ss_atomic_add(ne.ss_out + m, ss);
+    }
+  }
+}

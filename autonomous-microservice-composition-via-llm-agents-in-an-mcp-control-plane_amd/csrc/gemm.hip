@@ -474,11 +474,12 @@ int gemm_stream_enabled() {
 }
 
 int gemm256sk_prealloc();
+int gemm256d_split2_prealloc();
 
 int gemm_splitk_init(size_t bytes) {
   // the stream-K tail's slabs / counters too (gemm256sk.hip): both are
   // allocated here, at library load, never inside a hipGraph capture
-  if (gemm256sk_prealloc() != 0) return 2;
+  if (gemm256sk_prealloc() != 0 || gemm256d_split2_prealloc() != 0) return 2;
   if (!g_splitk_tickets) {
     if (hipMalloc(&g_splitk_tickets, MAX_SPLIT_TILES * sizeof(int)) != hipSuccess) {
       g_splitk_tickets = nullptr;
@@ -776,6 +777,8 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
 //   100 + S       128^2 kernel, S-way split-K through the reduce (S = 1: none)
 //   200           weight-streaming kernel (M <= 128)
 //   300 + f       flex tile candidate f (+32: 4-stage) with the SwiGLU epilogue
+//   400 + c       AGPR kernel at the height of code c, K halves over two
+//                 workgroups per tile (SPLIT 2, in-launch hand-off)
 //   1000 + 16 c + S  flex tile c with S-way split-K, the reduce applies SwiGLU
 // nonzero: not supported for this shape (nothing launched)
 int launch_gemm_silu_algo(const void* X, const void* W, void* Y, int M, int N, int K, int algo,
@@ -783,6 +786,8 @@ int launch_gemm_silu_algo(const void* X, const void* W, void* Y, int M, int N, i
   if (N % 64) return 1;
   if (algo >= 1000)
     return launch_gemm_flex_split(X, W, Y, nullptr, M, N, K, (algo - 1000) / 16, (algo - 1000) % 16, 2, s);
+  if (algo >= 401 && algo <= 405)                    // AGPR kernel, K halves over two workgroups
+    return launch_gemm_tn_256d_split2(X, W, Y, nullptr, M, N, K, 2, gemm256d_code_height(algo - 400), s);
   if (algo >= 300) {
     if (!gemm_flex_silu_ok(algo - 300)) return 2;
     return launch_gemm_flex_epi(X, W, Y, nullptr, M, N, K, algo - 300, 2, s);

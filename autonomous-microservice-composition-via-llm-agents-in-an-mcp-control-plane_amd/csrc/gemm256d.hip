@@ -47,6 +47,7 @@
 namespace {
 
 constexpr int BN = 256, BK = 64;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
 constexpr int ROWB = BK * 2;                        // 128-byte LDS rows
 constexpr int PIECE_BB = 256 * ROWB;                // the W operand of a slot: 32 KiB
 
@@ -90,13 +91,28 @@ constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 // once, no DMA, no barriers, no stores); 2 = + the ds_read fragment schedule
 // and the barriers (no DMA, no stores); 3 = + the LDS-DMA (the whole
 // mainloop, no epilogue stores).  Rung 0 minus rung 3 is the epilogue.
-template <int EPI, int BMT, bool WIDE = false, int PROBE = 0>
+//
+// SPLIT = 2 (mid M, one wave of tiles too few for the chip: gate|up at
+// M = 129-256 has 112 column tiles for 256 CUs): two workgroups per tile, each
+// walks half of K; grid = 2 x tiles, tile = id / 2 after the XCD remap (a
+// tile's halves usually share an XCD, which only matters for speed).  The
+// hand-off is the sc1 counter form of cdna_hip_programming.md §5 "Projection
+// GEMM at M = 256" item 2, made wait-free for the first arriver: each half
+// draws a ticket on cnt[tile] when its mainloop is done; ticket 0 stores its
+// fp32 accumulators (sc1, write-through) to the tile's slab, drains, bumps
+// the counter again and exits; ticket 1 polls (relaxed) until the counter
+// reads 3 - it only ever waits on a workgroup that is already running, so no
+// residency assumption - re-arms it, adds the slab (sc1 loads, every one) to
+// its accumulators and runs the epilogue.  ws: >= tiles x BMT x 256 floats.
+template <int EPI, int BMT, bool WIDE = false, int PROBE = 0, int SPLIT = 1>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
                                                        const bf16* __restrict__ R, int M, int N,
                                                        int K, int group, const RopeArgs ra,
-                                                       const NormEpi ne) {
+                                                       const NormEpi ne, f32x4* __restrict__ ws,
+                                                       int* __restrict__ cnt) {
+  static_assert(SPLIT == 1 || (SPLIT == 2 && PROBE == 0 && WIDE && EPI != 3), "split forms: wide epilogue");
   static_assert(BMT % 32 == 0 && BMT >= 128 && BMT <= 256, "tile height");
   constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (4..8)
   constexpr int WROWS = BMT / 2;                    // rows per wave (64..128)
@@ -114,8 +130,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   const int nm = (M + BMT - 1) / BMT, nn = (N + BN - 1) / BN;
   int m0, n0;
   // grid = the first gridDim.x tiles of the grouped order (all of them, or the
-  // full waves of a hybrid launch whose tail runs stream-K, gemm256sk.hip)
-  tile_coords(xcd_remap(blockIdx.x, gridDim.x), nm, nn, BMT, group, m0, n0);
+  // full waves of a hybrid launch whose tail runs stream-K, gemm256sk.hip);
+  // SPLIT 2: two workgroups per tile, K halves
+  const int wgl = xcd_remap(blockIdx.x, gridDim.x);
+  const int tl = SPLIT == 2 ? wgl >> 1 : wgl;
+  const int kslice = SPLIT == 2 ? wgl & 1 : 0;
+  tile_coords(tl, nm, nn, BMT, group, m0, n0);
 
   // ---- LDS-DMA: instruction q of an operand fills rows 8q..8q+7,
   //      lane-linearly (row 8q + lane/8, LDS chunk lane%8, swizzled source
@@ -138,14 +158,15 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // k-tile t of the trailing (unconsumed) DMAs is clamped to the last one:
   // soffset is outside the range check, so t >= nt would read past the end of
   // the last row of X / W
-  const int nt = K / BK;                             // >= 2, even (launcher)
+  const int nt = K / BK / SPLIT;                     // >= 2, even (launcher)
+  const int kb0 = kslice * nt * BK * 2;              // this workgroup's K half (SPLIT 2)
   auto dma1 = [&](int t, int slot, int i) {          // i < QA: A instruction i, else B i-QA
     if (PROBE == 1 || PROBE == 2) {
       if (t > 1) return;                             // probes: the prologue's tiles only
     }
     const bool b = i >= QA;
     const int q = b ? i - QA : i;
-    const int kb = min(t, nt - 1) * BK * 2;
+    const int kb = kb0 + min(t, nt - 1) * BK * 2;
     auto* dst = (__attribute__((address_space(3))) void*)(
         smem + slot * SLOT_B + (b ? PIECE_A + (8 * wave + q) * 1024 : (QA * wave + q) * 1024));
     if (b)
@@ -283,6 +304,44 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     return;
   }
 
+  // SPLIT 2: the slab of the other K half, added in the (wide) epilogue
+  constexpr int NACC = MTW * 8;                      // f32x4 per lane
+  [[maybe_unused]] const SlabIn<std::remove_const_t<decltype(rsA)>> slab{
+      __builtin_amdgcn_make_buffer_rsrc((void*)(ws + (size_t)tl * NACC * 256), (short)0, NACC * 256 * 16,
+                                        0x00020000),
+      (unsigned)tid * 16};
+  if constexpr (SPLIT == 2) {
+    // ---- K-half hand-off (see the SPLIT note above the kernel)
+    int* tick = reinterpret_cast<int*>(smem);        // the one LDS array (no second __shared__)
+    __syncthreads();                                 // every wave is done with the slots
+    if (tid == 0) *tick = __hip_atomic_fetch_add(cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int ticket = *tick;
+    f32x4* sbase = ws + (size_t)tl * NACC * 256 + tid;
+    if (ticket == 0) {
+      // straight from the AGPRs (a builtin store makes hipcc copy them all to
+      // VGPRs first and spill); sc1 = write-through, no release fence needed
+#pragma unroll
+      for (int r = 0; r < NACC; ++r)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(sbase + r * 256), "a"(acc[r >> 3][r & 7])
+                     : "memory");
+      asm volatile("s_nop 1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      // the partner drew ticket 0, so it is running and its store + bump come;
+      // the bound (~1 s) only keeps a broken invariant from hanging the GPU
+      for (int spin = 0; spin < (1 << 24); ++spin) {
+        if (__hip_atomic_load(cnt + tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+    }
+    __syncthreads();
+  }
+
   if constexpr (WIDE && EPI != 3) {
     // ---- wide direct epilogue (common.h store_wide): straight from the
     //      accumulators, 16-B stores after a permlane16 exchange, no LDS
@@ -295,7 +354,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     if constexpr (EPI == 2) norm_row_scales(ne, rrow, rsc);
     const auto rsY = __builtin_amdgcn_make_buffer_rsrc((void*)Y, (short)0, (int)((size_t)M * ldy * 2),
                                                        0x00020000);
-    store_wide<EPI, MTW>(acc, rsY, R, M, ldy, m0 + wm * WROWS, col0, fr, fq, rsc, ne);
+    if constexpr (SPLIT == 2)
+      store_wide_slab<EPI, MTW>(acc, rsY, R, M, ldy, m0 + wm * WROWS, col0, fr, fq, rsc, ne, slab);
+    else
+      store_wide<EPI, MTW>(acc, rsY, R, M, ldy, m0 + wm * WROWS, col0, fr, fq, rsc, ne);
   } else {
     // ---- staged epilogue.  The direct one below stores 8 B per lane in
     //      32-B row pieces (the MFMA layout: lane = 4 columns of one row); at
@@ -583,17 +645,17 @@ static int launch_height(const void* X, const void* W, void* Y, const void* R, i
   auto r = (const bf16*)R;
   if (gemm_wide_on(M, N, epi)) {
     switch (epi) {
-      case 0: gemm_tn_256d<0, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
-      case 1: gemm_tn_256d<1, BMT, true><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;
-      case 2: gemm_tn_256d<2, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+      case 0: gemm_tn_256d<0, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
+      case 1: gemm_tn_256d<1, BMT, true><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
+      case 2: gemm_tn_256d<2, BMT, true><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
       default: return 2;
     }
   }
   switch (epi) {
-    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
-    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi()); return 0;
-    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
-    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi()); return 0;
+    case 0: gemm_tn_256d<0, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
+    case 1: gemm_tn_256d<1, BMT><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
+    case 2: gemm_tn_256d<2, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
+    case 3: gemm_tn_256d<3, BMT><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), nullptr, nullptr); return 0;
     default: return 2;
   }
 }
@@ -723,7 +785,7 @@ int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K
   auto y = (bf16*)Y;
   const RopeArgs ra{};
   const NormEpi ne{};
-#define PROBE_LAUNCH(E, P) gemm_tn_256d<E, 256, true, P><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, ne)
+#define PROBE_LAUNCH(E, P) gemm_tn_256d<E, 256, true, P><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, ne, nullptr, nullptr)
   if (epi == 2) {
     switch (probe) {
       case 0: PROBE_LAUNCH(2, 0); break;
@@ -741,4 +803,81 @@ int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K
   }
 #undef PROBE_LAUNCH
   return 0;
+}
+
+// ---- SPLIT 2 (K halves, in-launch hand-off): slabs + tile counters, one set
+//      per device, allocated at library load (gemm_splitk_init), never inside
+//      a hipGraph capture.  Counters start at 0 and every tile's last arriver
+//      re-arms its own, so graph replays need no memset node.  One launch at a
+//      time (the model's stream), as for the stream-K slabs.
+namespace {
+constexpr int SPLIT_MAX_TILES = 128;                 // one wave: 2 x 128 workgroups
+struct Split2State {
+  f32x4* ws = nullptr;
+  int* cnt = nullptr;
+};
+Split2State* split2_state() {
+  static Split2State devs[64];
+  int d = 0;
+  (void)hipGetDevice(&d);
+  Split2State& st = devs[d & 63];
+  if (!st.ws) {
+    f32x4* ws = nullptr;
+    int* cnt = nullptr;
+    if (hipMalloc(&ws, (size_t)SPLIT_MAX_TILES * 256 * 256 * sizeof(float)) != hipSuccess) return nullptr;
+    if (hipMalloc(&cnt, SPLIT_MAX_TILES * sizeof(int)) != hipSuccess) {
+      (void)hipFree(ws);
+      return nullptr;
+    }
+    (void)hipMemset(cnt, 0, SPLIT_MAX_TILES * sizeof(int));
+    (void)hipDeviceSynchronize();
+    st.ws = ws;
+    st.cnt = cnt;
+  }
+  return &st;
+}
+
+template <int BMT>
+int launch_split2_height(const void* X, const void* W, void* Y, const void* R, int M, int N, int K,
+                         int epi, int group, const Split2State& st, hipStream_t s) {
+  const int tiles = ((M + BMT - 1) / BMT) * (N / BN);
+  if (tiles > SPLIT_MAX_TILES) return 6;
+  const dim3 grid(2 * tiles);
+  auto x = (const bf16*)X;
+  auto w = (const bf16*)W;
+  auto y = (bf16*)Y;
+  auto r = (const bf16*)R;
+  const RopeArgs ra{};
+  // always the wide epilogue (it adds the other half's slab); Y < 2 GiB
+  if ((size_t)M * (epi == 2 ? N / 2 : N) * 2 >= (1ull << 31)) return 8;
+  switch (epi) {
+    case 0: gemm_tn_256d<0, BMT, true, 0, 2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
+    case 1: gemm_tn_256d<1, BMT, true, 0, 2><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
+    case 2: gemm_tn_256d<2, BMT, true, 0, 2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
+    default: return 2;
+  }
+}
+}  // namespace
+
+int gemm256d_split2_prealloc() { return split2_state() ? 0 : 1; }
+
+// Y = X W^T (+ R | SwiGLU) with every tile over two workgroups (K halves);
+// bm = a tile height 128-256.  Nonzero (nothing launched): 1-3 gemm256d_ok,
+// 4 bad height, 5 K not a multiple of 256 (each half an even number of
+// 64-deep k-tiles), 6 more than 128 tiles, 7 no workspace, 2 epilogue
+int launch_gemm_tn_256d_split2(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                               int K, int epi, int bm, hipStream_t s) {
+  if (const int rc = gemm256d_ok(M, N, K)) return rc;
+  if (K % (4 * BK)) return 5;
+  Split2State* st = split2_state();
+  if (!st) return 7;
+  const int group = gemm256d_group(M, N, K);
+  switch (bm) {
+    case 256: return launch_split2_height<256>(X, W, Y, R, M, N, K, epi, group, *st, s);
+    case 224: return launch_split2_height<224>(X, W, Y, R, M, N, K, epi, group, *st, s);
+    case 192: return launch_split2_height<192>(X, W, Y, R, M, N, K, epi, group, *st, s);
+    case 160: return launch_split2_height<160>(X, W, Y, R, M, N, K, epi, group, *st, s);
+    case 128: return launch_split2_height<128>(X, W, Y, R, M, N, K, epi, group, *st, s);
+    default: return 4;
+  }
 }

@@ -126,6 +126,9 @@ int gemm256d_code_height(int code);     // plan code 1..5 -> AGPR tile height (0
 // probe 0 production, 1 MFMA only, 2 + ds_read + barriers, 3 + LDS-DMA (no stores)
 int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K, int epi,
                       int probe, hipStream_t s);
+// K-half split form (gemm256d.hip SPLIT 2): two workgroups per tile
+int launch_gemm_tn_256d_split2(const void* X, const void* W, void* Y, const void* R, int M, int N,
+                               int K, int epi, int bm, hipStream_t s);
 int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,
                            int K, int epi, int bm, hipStream_t s);
 // Y[M, N/2] = silu(X W_g^T) * (X W_u^T), W rows interleaved [gate 16 | up 16]

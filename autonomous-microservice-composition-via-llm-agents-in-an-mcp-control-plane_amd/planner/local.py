@@ -276,36 +276,49 @@ class LocalPlanner(Planner):
                 for loop, fut in items:
                     loop.call_soon_threadsafe(_set_exc, fut, err)
 
+    def _submit_item(self, item):
+        intent, loop, fut = item[:3]
+        try:
+            # prepared on the prep thread, or here
+            dec, ptoks, stoks = item[3] if len(item) > 3 else self.prepare(intent)
+            t0 = time.perf_counter()
+
+            def done(seq, loop=loop, fut=fut, t0=t0):
+                METRICS.observe("engine_latency_s", time.perf_counter() - t0)
+                with self._pending_lock:
+                    self._pending.pop(id(fut), None)
+                if seq.error:
+                    loop.call_soon_threadsafe(_set_exc, fut, RuntimeError(seq.error))
+                else:
+                    loop.call_soon_threadsafe(_set_result, fut, seq.result)
+            self.engine.submit(dec, stoks, prefix_tokens=ptoks, on_done=done)
+        except Exception as e:  # noqa: BLE001
+            loop.call_soon_threadsafe(_set_exc, fut, e)
+
+    def _pump(self) -> int:
+        """Submit every request already queued (the engine's arrival pump,
+        called on the engine thread while a lookahead launch is held)."""
+        n = 0
+        while True:
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                return n
+            self._submit_item(item)
+            n += 1
+
     def _loop(self):
         eng = self.engine
+        eng.poll_arrivals = self._pump
         while not self._stop.is_set():
             try:
                 block = not eng.has_work()
                 item = self._q.get(timeout=0.05) if block else self._q.get_nowait()
             except queue.Empty:
                 item = None
-            while item is not None:
-                intent, loop, fut = item[:3]
-                try:
-                    # prepared on the prep thread, or here
-                    dec, ptoks, stoks = item[3] if len(item) > 3 else self.prepare(intent)
-                    t0 = time.perf_counter()
-
-                    def done(seq, loop=loop, fut=fut, t0=t0):
-                        METRICS.observe("engine_latency_s", time.perf_counter() - t0)
-                        with self._pending_lock:
-                            self._pending.pop(id(fut), None)
-                        if seq.error:
-                            loop.call_soon_threadsafe(_set_exc, fut, RuntimeError(seq.error))
-                        else:
-                            loop.call_soon_threadsafe(_set_result, fut, seq.result)
-                    eng.submit(dec, stoks, prefix_tokens=ptoks, on_done=done)
-                except Exception as e:  # noqa: BLE001
-                    loop.call_soon_threadsafe(_set_exc, fut, e)
-                try:
-                    item = self._q.get_nowait()
-                except queue.Empty:
-                    item = None
+            if item is not None:
+                self._submit_item(item)
+                self._pump()
             if eng.has_work():
                 with self._lock:
                     eng.step()

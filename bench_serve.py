@@ -68,12 +68,12 @@ def run_qps(planner, engine, qps, duration, seed, rank):
     i = 0
     batch_sizes = []
     next_log = 30.0            # a progress line every 30 s (long soak runs stay visibly alive)
-    while i < n or engine.has_work():
+    def pump():
+        """Submit the arrivals that are due (also the engine's arrival pump
+        while it holds a lookahead launch)."""
+        nonlocal i
         now = time.perf_counter() - t0
-        if now >= next_log:
-            log(f"[qps {qps}] {now:.0f} s: {i} of {n} submitted, {len(done_at)} done, "
-                f"{len(engine.running)} running")
-            next_log += 30.0
+        k = 0
         while i < n and arrivals[i] <= now:
             dec, ptoks, stoks = planner.prepare(synthetic_intent(rank * 1_000_000 + i), services)
             arr = arrivals[i]
@@ -82,12 +82,24 @@ def run_qps(planner, engine, qps, duration, seed, rank):
                 done_at[seq.uid] = (time.perf_counter() - t0, arr, seq.result)
             engine.submit(dec, stoks, prefix_tokens=ptoks, on_done=on_done)
             i += 1
+            k += 1
+        return k
+
+    engine.poll_arrivals = pump
+    while i < n or engine.has_work():
+        now = time.perf_counter() - t0
+        if now >= next_log:
+            log(f"[qps {qps}] {now:.0f} s: {i} of {n} submitted, {len(done_at)} done, "
+                f"{len(engine.running)} running")
+            next_log += 30.0
+        pump()
         if engine.has_work():
             batch_sizes.append(len(engine.running))
             engine.step()
         elif i < n:
             time.sleep(max(0.0, min(arrivals[i] - (time.perf_counter() - t0), 0.002)))
     elapsed = time.perf_counter() - t0
+    engine.poll_arrivals = None
     for t_done, arr, res in done_at.values():
         lat.append(t_done - arr)
         dags.append(res)

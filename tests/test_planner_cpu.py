@@ -7,6 +7,8 @@ import re
 
 import httpx
 import numpy as np
+import time
+
 import pytest
 import torch
 from fastapi.testclient import TestClient
@@ -308,6 +310,55 @@ def test_lookahead_admits_arrivals_and_matches_synchronous(temperature, monkeypa
     assert out[0] == out[1]
     assert stats[1][0]["lookahead_steps"] > 0 and stats[1][1] > 0
     assert stats[1][0]["lookahead_admitted"] > 0, stats[1][0]
+
+
+def test_lookahead_hold_pumps_arrivals_into_branch_step(monkeypatch):
+    """The lookahead hold (MCP_LOOKAHEAD_HOLD): once a step time is measured,
+    the branch launch waits until shortly before the current step's end and
+    pumps the driver's arrivals meanwhile; an arrival ends the wait and joins
+    the branch step.  On the CPU the forward is synchronous, so the sampled-
+    token wait is slowed to look device-bound."""
+    from mcp_amd.engine import native
+    if not native.available():
+        pytest.skip("native runtime not built")
+    from mcp_amd.engine import engine as engine_mod
+    reg = MemoryRegistry(synthetic_registry(7, seed=4))
+    torch.manual_seed(0)
+    model = LlamaModel.random("tiny", "cpu", seed=1)
+    eng = LLMEngine(model, num_blocks=256, max_batch=16, temperature=0.0, lookahead=True)
+    planner = LocalPlanner(eng, reg, max_nodes=4, min_nodes=2)
+    planner.plan_many([synthetic_intent(99)])           # the registry prefix is computed
+    real_wait = engine_mod.LLMEngine._wait_tokens
+
+    def slow_wait(self, L):
+        time.sleep(0.004)                                # the device "runs" for 4 ms
+        return real_wait(self, L)
+    monkeypatch.setattr(engine_mod.LLMEngine, "_wait_tokens", slow_wait)
+    monkeypatch.setattr(engine_mod.LLMEngine, "LOOK_LEAD_S", 0.001)
+    pending = [planner.prepare(synthetic_intent(i)) for i in range(1, 4)]
+    seqs, calls = [], []
+
+    def pump():
+        calls.append(len(eng._look))
+        if len(calls) % 3 == 0 and pending:             # an arrival during some holds
+            dec, ptoks, stoks = pending.pop(0)
+            seqs.append(eng.submit(dec, stoks, prefix_tokens=ptoks))
+            return 1
+        return 0
+    eng.poll_arrivals = pump
+    dec, ptoks, stoks = planner.prepare(synthetic_intent(0))
+    seqs.append(eng.submit(dec, stoks, prefix_tokens=ptoks))
+    eng.run()
+    while pending:                                       # arrivals the run did not pump
+        dec, ptoks, stoks = pending.pop(0)
+        seqs.append(eng.submit(dec, stoks, prefix_tokens=ptoks))
+        eng.run()
+    assert calls, "the hold never pumped arrivals"
+    assert eng.stats.get("look_hold_s", 0.0) > 0.0
+    assert eng.stats["lookahead_admitted"] > 0, eng.stats
+    assert all(q.error is None and q.result for q in seqs)
+    eng.drop_prefixes()                                  # the cached registry prefix
+    assert not eng._look and not eng.running and eng.alloc.num_free == eng.kv.num_blocks
 
 
 def test_graph_static_layout_matches_dynamic():
