@@ -253,7 +253,7 @@ void gemm_plan_set_silu_py(int64_t N, int64_t K, const std::vector<int64_t>& cod
   std::vector<int> c(codes.begin(), codes.end());
   for (int v : c)
     TORCH_CHECK(v == -1 || (v >= 1 && v <= 5) || (v >= 101 && v <= 116) || v == 200 ||
-                    (v >= 300 && v < 364) || (v >= 401 && v <= 405) || (v >= 1000 && v < 1000 + 16 * 16),
+                    (v >= 300 && v < 364) || (v >= 400 && v <= 405) || (v >= 1000 && v < 1000 + 16 * 16),
                 "gemm plan silu: -1 or a launch_gemm_silu_algo code");
   gemm_plan_set_silu((int)N, (int)K, c.data(), (int)c.size());
 }

@@ -778,7 +778,8 @@ void launch_gemm_tn_256_silu(const void* X, const void* W, void* Y, int M, int N
 //   200           weight-streaming kernel (M <= 128)
 //   300 + f       flex tile candidate f (+32: 4-stage) with the SwiGLU epilogue
 //   400 + c       AGPR kernel at the height of code c, K halves over two
-//                 workgroups per tile (SPLIT 2, in-launch hand-off)
+//                 workgroups per tile (SPLIT 2, in-launch hand-off); 400 =
+//                 the smallest height >= M (M <= 224, else nonzero)
 //   1000 + 16 c + S  flex tile c with S-way split-K, the reduce applies SwiGLU
 // nonzero: not supported for this shape (nothing launched)
 int launch_gemm_silu_algo(const void* X, const void* W, void* Y, int M, int N, int K, int algo,
@@ -788,6 +789,16 @@ int launch_gemm_silu_algo(const void* X, const void* W, void* Y, int M, int N, i
     return launch_gemm_flex_split(X, W, Y, nullptr, M, N, K, (algo - 1000) / 16, (algo - 1000) % 16, 2, s);
   if (algo >= 401 && algo <= 405)                    // AGPR kernel, K halves over two workgroups
     return launch_gemm_tn_256d_split2(X, W, Y, nullptr, M, N, K, 2, gemm256d_code_height(algo - 400), s);
+  if (algo == 400) {
+    // K halves at the smallest tile height that holds all M rows, up to 224
+    // (gate|up at M = 129-224: one wave of 2 x 112 workgroups, W streamed
+    // once; profiles/gate_up_midm_r6.md).  Past 224 rows nonzero: the
+    // caller's rule path runs.  MCP_GEMM_SPLIT2=0 turns it off (A/B).
+    static const int on = getenv("MCP_GEMM_SPLIT2") ? atoi(getenv("MCP_GEMM_SPLIT2")) : 1;
+    if (!on || M > 224) return 6;
+    const int bm = M <= 128 ? 128 : M <= 160 ? 160 : M <= 192 ? 192 : 224;
+    return launch_gemm_tn_256d_split2(X, W, Y, nullptr, M, N, K, 2, bm, s);
+  }
   if (algo >= 300) {
     if (!gemm_flex_silu_ok(algo - 300)) return 2;
     return launch_gemm_flex_epi(X, W, Y, nullptr, M, N, K, algo - 300, 2, s);

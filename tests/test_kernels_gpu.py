@@ -655,7 +655,7 @@ def test_gemm_silu_every_path(M):
     ss = (X.float().pow(2).sum(-1) * (1 << 20)).round().to(torch.int64)
     rs = torch.rsqrt(ss.double() / (1 << 20) / K + eps).float()[:, None]
     exp = torch.nn.functional.silu((X.float() @ g.float().t()) * rs) * ((X.float() @ u.float().t()) * rs)
-    algos = [1, 2, 3, 4, 5, 101, 102, 104, 200, 401, 402, 403, 404, 405]
+    algos = [1, 2, 3, 4, 5, 101, 102, 104, 200, 400, 401, 402, 403, 404, 405]
     algos += [300 + f for f in range(L.gemm_flex_count()) if L.gemm_flex_silu_ok(f)]
     algos += [1000 + 16 * c + S for c in (0, 6, 10) for S in (2, 4)]
     ran = 0

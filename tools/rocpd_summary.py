@@ -6,6 +6,7 @@ per-kernel calls / total / mean time and a per-category breakdown.
 ``last_ms``: only kernels that start in the last ``last_ms`` milliseconds of
 the trace (e.g. the timed steps of bench.py, after model init and warm-up).
 """
+import os
 import re
 import sqlite3
 import sys
@@ -22,6 +23,8 @@ CATS = [("gemm (MFMA 256x256, AGPR 1 wave/SIMD)", r"gemm_tn_256d"),
 
 
 def short(name):
+    if os.environ.get("MCP_SUMMARY_FULL_NAMES") == "1":   # e.g. hipBLASLt's tile / split fields
+        return name
     n = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", name)
     m = re.match(r"(\w+?)I(.*)E(vPK|v)", n)
     return (m.group(1) + "<" + m.group(2)[:40] + ">") if m else n[:80]
