@@ -960,6 +960,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("nz"), py::arg("split_o"), py::arg("split_lse"), py::arg("wo"), py::arg("x"),
         py::arg("ss_out") = py::none());
   m.def("attn_lazy_rescale", &attn_lazy_rescale, "shared-prefix attention: lazy max rescaling on / off");
+  m.def("gemm_pf_force", &gemm_pf_force, "split-form W L2 fills ahead of the DMA: -1 = MCP_GEMM_PF, 0 off, 1 on");
   m.def("gemm_split2", &gemm_split2, "AGPR GEMM, K halves over two workgroups per tile (tests / tuning)",
         py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("R") = py::none(), py::arg("bm") = 256);
   m.def("gemm_probe", &gemm_probe, "GEMM power-ladder rung (gemm256d.hip PROBE 0-3)");

@@ -104,7 +104,16 @@ constexpr int op0_at(int j, int n, int P) { return (j * n) / P; }
 // reads 3 - it only ever waits on a workgroup that is already running, so no
 // residency assumption - re-arms it, adds the slab (sc1 loads, every one) to
 // its accumulators and runs the epilogue.  ws: >= tiles x BMT x 256 floats.
-template <int EPI, int BMT, bool WIDE = false, int PROBE = 0, int SPLIT = 1>
+//
+// PF = 1 (mid-M forms, where each workgroup streams its W panel straight from
+// HBM): the 2-slot pipeline waits for tile t+1's DMAs at tile t's half-way
+// barrier, so it covers 1-1.5 half-tiles of DMA latency (~0.25-0.75 us), under
+// a loaded HBM round trip.  Each wave also pulls its 64 W rows of tile t+4
+// into L2 (one 4-byte load per lane = one 128-B line per row, into a sink
+// register) at the end of tile t; loads retire in issue order, so the
+// half-way wait becomes vmcnt(1) (vmcnt(2) at tile 0) and each L2 fill gets
+// three half-tiles before the wait that covers it.
+template <int EPI, int BMT, bool WIDE = false, int PROBE = 0, int SPLIT = 1, int PF = 0>
 __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ X,
                                                        const bf16* __restrict__ W,
                                                        bf16* __restrict__ Y,
@@ -113,6 +122,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
                                                        const NormEpi ne, f32x4* __restrict__ ws,
                                                        int* __restrict__ cnt) {
   static_assert(SPLIT == 1 || (SPLIT == 2 && PROBE == 0 && WIDE && EPI != 3), "split forms: wide epilogue");
+  static_assert(PF == 0 || PROBE == 0, "prefetch: production forms");
   static_assert(BMT % 32 == 0 && BMT >= 128 && BMT <= 256, "tile height");
   constexpr int MTW = BMT / 32;                     // 16-row MFMA tiles per wave (4..8)
   constexpr int WROWS = BMT / 2;                    // rows per wave (64..128)
@@ -175,6 +185,16 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, offA0 + q * 16 * K, kb, 0, 0);
   };
 
+  // ---- PF: L2 fill of this wave's 64 W rows of k-tile t (clamped), one line per lane
+  [[maybe_unused]] int pf_sink = 0;
+  [[maybe_unused]] const bf16* pfw = W + (size_t)(rowB0 + lane) * K + kb0 / 2;
+  auto pf1 = [&](int t) {
+    if constexpr (PF) {
+      const bf16* p = pfw + min(t, nt - 1) * BK;
+      asm volatile("global_load_dword %0, %1, off" : "+v"(pf_sink) : "v"(p));
+    }
+  };
+
   // ---- fragment reads: wave (wm, wn) owns rows wm*WROWS.., cols wn*128..;
   //      lane (fr, fq) reads row fr of fragment i, k-chunk 4 kh + fq.  Fragment
   //      i sits i * 2 KiB after fragment 0 with the same swizzle (row & 7 = fr & 7).
@@ -219,8 +239,18 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   for (int i = 0; i < NDMA; ++i) dma1(0, 0, i);
 #pragma unroll
   for (int i = 0; i < NDMA; ++i) dma1(1, 1, i);
-  // tile 0 landed (own DMAs): the NDMA of tile 1 may still be in flight
-  if constexpr (NDMA == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if constexpr (PF) {
+    pf1(2);
+    pf1(3);
+  }
+  // tile 0 landed (own DMAs): the NDMA of tile 1 (+ 2 fills) may still be in flight
+  if constexpr (PF) {
+    if constexpr (NDMA == 16) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else if constexpr (NDMA == 15) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+    else if constexpr (NDMA == 14) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if constexpr (NDMA == 13) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  } else if constexpr (NDMA == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (NDMA == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   else if constexpr (NDMA == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   else if constexpr (NDMA == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
@@ -264,7 +294,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
     keep(F[0]);
     // tile t+1 landed (own DMAs), and this wave's reads of slot C are done
     if constexpr (PROBE != 1) {
-      __builtin_amdgcn_s_waitcnt(0x0070);            // vmcnt(0) lgkmcnt(0)
+      if constexpr (PF) {                            // the youngest fill(s) may stay in flight
+        if (C == 0 && t == 0) __builtin_amdgcn_s_waitcnt(0x0072);   // vmcnt(2) lgkmcnt(0)
+        else __builtin_amdgcn_s_waitcnt(0x0071);                    // vmcnt(1) lgkmcnt(0)
+      } else {
+        __builtin_amdgcn_s_waitcnt(0x0070);          // vmcnt(0) lgkmcnt(0)
+      }
       raw_barrier();
     }
     fence();
@@ -279,6 +314,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
       for (int d = 0; d < ops_at(j, NDMA, NP); ++d) dma1(t + 2, C, op0_at(j, NDMA, NP) + d);
       fence();
     }
+    pf1(t + 4);                                      // after this tile's DMAs (in-order retire)
     keep(F[1]);
   };
   using C0 = std::integral_constant<int, 0>;
@@ -290,6 +326,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_256d(const bf16* __restrict__ 
   // drain the trailing (unconsumed) DMAs before the workgroup's LDS is released,
   // and pad MFMA results -> VALU reads (inline asm is not padded)
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  if constexpr (PF) asm volatile("" :: "v"(pf_sink));   // the sink register stays reserved to here
   if constexpr (PROBE != 0) {
     // probes store nothing; one accumulator reaches memory under a condition
     // no launch meets, so the MFMA results stay live
@@ -812,6 +849,7 @@ int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K
 //      time (the model's stream), as for the stream-K slabs.
 namespace {
 constexpr int SPLIT_MAX_TILES = 128;                 // one wave: 2 x 128 workgroups
+int g_pf_force = -1;                                 // gemm_pf_force (tests, A/B)
 struct Split2State {
   f32x4* ws = nullptr;
   int* cnt = nullptr;
@@ -850,6 +888,16 @@ int launch_split2_height(const void* X, const void* W, void* Y, const void* R, i
   const RopeArgs ra{};
   // always the wide epilogue (it adds the other half's slab); Y < 2 GiB
   if ((size_t)M * (epi == 2 ? N / 2 : N) * 2 >= (1ull << 31)) return 8;
+  // W L2 fills ahead of the DMA (PF): MCP_GEMM_PF=1 / gemm_pf_force
+  static const int pf_env = getenv("MCP_GEMM_PF") ? atoi(getenv("MCP_GEMM_PF")) : 0;
+  if (g_pf_force >= 0 ? g_pf_force : pf_env) {
+    switch (epi) {
+      case 0: gemm_tn_256d<0, BMT, true, 0, 2, 1><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
+      case 1: gemm_tn_256d<1, BMT, true, 0, 2, 1><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
+      case 2: gemm_tn_256d<2, BMT, true, 0, 2, 1><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
+      default: return 2;
+    }
+  }
   switch (epi) {
     case 0: gemm_tn_256d<0, BMT, true, 0, 2><<<grid, 256, 0, s>>>(x, w, y, nullptr, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
     case 1: gemm_tn_256d<1, BMT, true, 0, 2><<<grid, 256, 0, s>>>(x, w, y, r, M, N, K, group, ra, norm_epi(), st.ws, st.cnt); return 0;
@@ -860,6 +908,7 @@ int launch_split2_height(const void* X, const void* W, void* Y, const void* R, i
 }  // namespace
 
 int gemm256d_split2_prealloc() { return split2_state() ? 0 : 1; }
+void gemm_pf_force(int p) { g_pf_force = p; }
 
 // Y = X W^T (+ R | SwiGLU) with every tile over two workgroups (K halves);
 // bm = a tile height 128-256.  Nonzero (nothing launched): 1-3 gemm256d_ok,

@@ -127,6 +127,7 @@ int gemm256d_code_height(int code);     // plan code 1..5 -> AGPR tile height (0
 int launch_gemm_probe(const void* X, const void* W, void* Y, int M, int N, int K, int epi,
                       int probe, hipStream_t s);
 // K-half split form (gemm256d.hip SPLIT 2): two workgroups per tile
+void gemm_pf_force(int p);                           // W L2 fills in the split form: -1 env, 0 / 1
 int launch_gemm_tn_256d_split2(const void* X, const void* W, void* Y, const void* R, int M, int N,
                                int K, int epi, int bm, hipStream_t s);
 int launch_gemm_tn_256d_bm(const void* X, const void* W, void* Y, const void* R, int M, int N,

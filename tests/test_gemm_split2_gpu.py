@@ -23,9 +23,18 @@ def rel_err(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
+@pytest.fixture(params=[0, 1], ids=["pf0", "pf1"])
+def w_prefetch(request):
+    """The split form with and without the W L2 fills ahead of the DMA (PF)."""
+    L = ops.lib()
+    L.gemm_pf_force(request.param)
+    yield request.param
+    L.gemm_pf_force(-1)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 3584, 4096), (200, 2048, 1024), (97, 4096, 14336),
                                    (300, 1024, 512)])
-def test_split2_plain_and_residual(M, N, K):
+def test_split2_plain_and_residual(M, N, K, w_prefetch):
     torch.manual_seed(11)
     L = ops.lib()
     X = torch.randn(M, K, device=DEV).bfloat16()
@@ -48,7 +57,7 @@ def test_split2_plain_and_residual(M, N, K):
 
 
 @pytest.mark.parametrize("M", [129, 192, 256, 320])
-def test_split2_swiglu_every_height(M):
+def test_split2_swiglu_every_height(M, w_prefetch):
     """gate|up + SwiGLU with the fused-norm row scale (the 'silu' plan codes
     401-405), N = 28672 as in Llama-3-8B where the tiles fit one wave."""
     torch.manual_seed(12)
@@ -73,7 +82,7 @@ def test_split2_swiglu_every_height(M):
     assert ran >= (1 if M <= 256 else 0)            # past 256 rows the tiles exceed one wave
 
 
-def test_split2_back_to_back_and_graph():
+def test_split2_back_to_back_and_graph(w_prefetch):
     """Many launches in a row and inside a hipGraph: every tile's last arriver
     re-arms its counter, so each launch sees fresh tickets (a stale counter
     would make a first arriver wait for a partner slab that never comes, and

@@ -50,6 +50,11 @@ for M in Ms:
     for code in (1, 2, 3, 4, 5, 401, 402, 403, 404, 405):
         if L.gemm_silu_algo(X, Ws[0], Y, code, None, 0.0) == 0:
             rec[f"code{code}_us"] = t_us(lambda i, c=code: L.gemm_silu_algo(X, Ws[i], Y, c, None, 0.0))
+    L.gemm_pf_force(1)                                  # the split form + W L2 fills
+    for code in (401, 402, 403, 404, 405):
+        if L.gemm_silu_algo(X, Ws[0], Y, code, None, 0.0) == 0:
+            rec[f"code{code}pf_us"] = t_us(lambda i, c=code: L.gemm_silu_algo(X, Ws[i], Y, c, None, 0.0))
+    L.gemm_pf_force(-1)
     rec["hipblaslt_gemm_us"] = t_us(lambda i: torch.matmul(X, WTs[i], out=P))
     rec["hipblaslt_gemm_silu_us"] = t_us(lambda i: (torch.matmul(X, WTs[i], out=P), L.silu_mul(P, Y)))
     ours = min(v for k, v in rec.items() if k.startswith("code") or k == "dispatch_us")
