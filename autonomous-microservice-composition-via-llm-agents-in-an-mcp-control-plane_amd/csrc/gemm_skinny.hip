@@ -243,13 +243,16 @@ void launch_mb(const void* X, const void* W, void* Y, const void* R, int M, int 
     return;
   }
   // MCP_GEMM_SKINNY_FORM (A/B after the round-4 load-order fix, M <= 16):
-  // 0 = 8 waves x 1-deep ring, 1 = 8 x 2, 2 = 4 x 2, 3 = 4 x 4
+  // 0 = 8 waves x 1-deep ring, 1 = 8 x 2, 2 = 4 x 2, 3 = 4 x 4, 4 = 8 x 4
+  // (round 6: at K = 4096 every wave's 4 steps in flight at once, 128 KiB
+  // per CU - the o projection of config 2 streams at ~2.5 TB/s with 32 KiB)
   static const int form = getenv("MCP_GEMM_SKINNY_FORM") ? atoi(getenv("MCP_GEMM_SKINNY_FORM")) : 0;
   if constexpr (MB == 1) {
     switch (form) {
       case 1: launch_form<EPI, MB, 8, 2, false>(X, W, Y, R, M, N, K, s); return;
       case 2: launch_form<EPI, MB, 4, 2, false>(X, W, Y, R, M, N, K, s); return;
       case 3: launch_form<EPI, MB, 4, 4, false>(X, W, Y, R, M, N, K, s); return;
+      case 4: launch_form<EPI, MB, 8, 4, false>(X, W, Y, R, M, N, K, s); return;
       default: break;
     }
   }

@@ -135,7 +135,12 @@ _SPIN_WAIT = os.environ.get("MCP_SPIN_WAIT", "0") == "1"
 # forward.  The host's per-decision work (read-back, grammar, schedule, pack,
 # launch) then runs while the GPU is busy with the next step instead of
 # between steps.
-_LOOKAHEAD = os.environ.get("MCP_LOOKAHEAD", "0") == "1"
+# On by default since round 6: with the hold (LLMEngine.LOOK_HOLD) an arrival
+# joins the branch step instead of queueing behind it; same box, alternated
+# (profiles/lookahead_hold_ab_r6.txt): config 2 p50 85.2-85.4 vs 85.8-86.9 ms,
+# config 5 at 20 / 40 intents/s p50 103.1-103.4 / 115.3-115.7 vs 103.7-105.0 /
+# 121.6-121.9 ms, at 80/s 144.3 vs 142.8 (one round).  MCP_LOOKAHEAD=0: off.
+_LOOKAHEAD = os.environ.get("MCP_LOOKAHEAD", "1") == "1"
 
 
 def tp_graph_safe(model) -> bool:
