@@ -1127,6 +1127,17 @@ class LLMEngine:
             time.sleep(50e-6)
         self.stats["look_hold_s"] = self.stats.get("look_hold_s", 0.0) + time.perf_counter() - held
 
+    def _look_device_errors(self) -> str:
+        """branch_select's device error word (rows whose sampled token matched
+        no outcome), read on the host's mismatch path only - a read per step
+        would add a device sync - then cleared."""
+        if self._look_err is None:
+            return ""
+        n = int(self._look_err.item())
+        self._look_err.zero_()
+        self.stats["lookahead_device_errors"] = self.stats.get("lookahead_device_errors", 0) + n
+        return f" (device error word: {n})"
+
     def _step_look(self) -> int:
         """Lookahead steady state: read the older launch's samples, resolve
         the branch launch's outcome per sequence (adopt that outcome's
@@ -1157,7 +1168,7 @@ class LLMEngine:
                     # host check is authoritative (branch_select's device
                     # error word marks the same case)
                     q.error = (f"decision lookahead: sampled token {t} is not an outcome "
-                               f"of the pending choice")
+                               f"of the pending choice{self._look_device_errors()}")
                     finished.append(q)
                     bad = True
                     continue

@@ -926,6 +926,7 @@ def test_lookahead_outcome_mismatch_fails_only_that_request(monkeypatch):
     assert state["done"], "lookahead never ran"
     errs = [q for q in seqs if q.error]
     assert len(errs) == 1 and "not an outcome" in errs[0].error
+    assert "device error word" in errs[0].error and "lookahead_device_errors" in eng.stats
     assert all(q.done for q in seqs) and sum(q.result is not None for q in seqs) == 2
     assert not eng._look and not eng.inflight
     eng.drop_prefixes()
