@@ -879,7 +879,7 @@ class LLMEngine:
         return _Launch(batch_seqs, sample_seqs, tokens, event, T, tok_dev=tok_dev)
 
     # ------------------------------------------------------ decision lookahead
-    LOOKAHEAD_MAX_SEQS = 8
+    LOOKAHEAD_MAX_SEQS = int(os.environ.get("MCP_LOOKAHEAD_MAX_SEQS", "8"))
     # queued requests join a lookahead step instead of ending lookahead (an
     # arrival would otherwise wait behind the step already queued)
     LOOKAHEAD_ADMIT = os.environ.get("MCP_LOOKAHEAD_ADMIT", "1") == "1"
