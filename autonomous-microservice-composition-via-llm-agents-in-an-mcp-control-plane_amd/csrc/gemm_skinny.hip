@@ -243,7 +243,8 @@ void launch_mb(const void* X, const void* W, void* Y, const void* R, int M, int 
     return;
   }
   // MCP_GEMM_SKINNY_FORM (A/B after the round-4 load-order fix, M <= 16):
-  // 0 = 8 waves x 1-deep ring, 1 = 8 x 2, 2 = 4 x 2, 3 = 4 x 4, 4 = 8 x 4
+  // 0 = 8 waves x 1-deep ring, 1 = 8 x 2, 2 = 4 x 2, 3 = 4 x 4, 4 = 8 x 4,
+  // 5 = 8 x 4 for EPI 0 / 1 only (form 4 on config 2: 87.7 vs 84.5-85.3 ms)
   // (round 6: at K = 4096 every wave's 4 steps in flight at once, 128 KiB
   // per CU - the o projection of config 2 streams at ~2.5 TB/s with 32 KiB)
   static const int form = getenv("MCP_GEMM_SKINNY_FORM") ? atoi(getenv("MCP_GEMM_SKINNY_FORM")) : 0;
@@ -253,6 +254,12 @@ void launch_mb(const void* X, const void* W, void* Y, const void* R, int M, int 
       case 2: launch_form<EPI, MB, 4, 2, false>(X, W, Y, R, M, N, K, s); return;
       case 3: launch_form<EPI, MB, 4, 4, false>(X, W, Y, R, M, N, K, s); return;
       case 4: launch_form<EPI, MB, 8, 4, false>(X, W, Y, R, M, N, K, s); return;
+      case 5:                                        // 8 x 4 for the plain / residual GEMMs only
+        if constexpr (EPI != 2) {
+          launch_form<EPI, MB, 8, 4, false>(X, W, Y, R, M, N, K, s);
+          return;
+        }
+        break;
       default: break;
     }
   }
