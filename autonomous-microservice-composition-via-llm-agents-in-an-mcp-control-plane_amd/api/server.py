@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import os
 from typing import Optional
 
 import httpx
@@ -325,6 +326,17 @@ def _api_worker(idx: int, n: int, host: str, port: int, access_log: bool,
     if http == "fast":
         import asyncio
         from .fasthttp import serve_fast
+        prof_dir = os.environ.get("MCP_PROFILE_DIR")   # diagnostics: cProfile each API worker
+        if prof_dir:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
+            try:
+                asyncio.run(serve_fast(app, sock=sock, ready=lambda: print(msg, flush=True)))
+            finally:
+                prof.disable()
+                prof.dump_stats(os.path.join(prof_dir, f"api-worker-{idx}.prof"))
+            return
         asyncio.run(serve_fast(app, sock=sock, ready=lambda: print(msg, flush=True)))
         return
     import uvicorn

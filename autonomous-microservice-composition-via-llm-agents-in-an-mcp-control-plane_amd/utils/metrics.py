@@ -77,6 +77,16 @@ class Metrics:
             self.windows["plan_latency_s"].add(latency_s)
             self._plan_times.append(now)
 
+    def plans_done(self, n: int, latency_s: float):
+        """``n`` plans finished now, each after ``latency_s`` (one lock for a batch)."""
+        now = time.time()
+        with self._lock:
+            self.counters["plans_total"] += n
+            w = self.windows["plan_latency_s"]
+            for _ in range(n):
+                w.add(latency_s)
+                self._plan_times.append(now)
+
     def plans_per_sec(self, window_s: float = 10.0) -> float:
         now = time.time()
         with self._lock:

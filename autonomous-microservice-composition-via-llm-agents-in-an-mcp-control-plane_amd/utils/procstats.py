@@ -148,18 +148,27 @@ async def report_forever(period: float, snap: Callable[[], dict], log: StatsLog,
     gcw = GCWatch()
     lag = LoopLag().start()
     t_start = time.time()
+
+    def report(final: bool = False):
+        rec = {"proc": proc, "pid": os.getpid(), "t": round(time.time() - t_start, 1),
+               "rss_mb": round(rss_mb(), 1)}
+        if final:
+            rec["final"] = True             # the partial window up to shutdown
+        rec.update(lag.snapshot())
+        rec.update(gcw.snapshot())
+        try:
+            rec.update(snap())
+        except Exception as e:  # noqa: BLE001 - stats must never take the server down
+            rec["snap_error"] = repr(e)
+        log.write(rec)
+
     try:
         while True:
             await asyncio.sleep(period)
-            rec = {"proc": proc, "pid": os.getpid(), "t": round(time.time() - t_start, 1),
-                   "rss_mb": round(rss_mb(), 1)}
-            rec.update(lag.snapshot())
-            rec.update(gcw.snapshot())
-            try:
-                rec.update(snap())
-            except Exception as e:  # noqa: BLE001 - stats must never take the server down
-                rec["snap_error"] = repr(e)
-            log.write(rec)
+            report()
+    except asyncio.CancelledError:
+        report(final=True)                  # every request of the run is in some line
+        raise
     finally:
         lag.stop()
         gcw.close()
