@@ -79,8 +79,9 @@ struct DecArgs {
 
 // one 16-B piece of an output row: plain, or write-through (sc1: leaves the
 // XCD's L2 at once, MI355X_MICROARCH.md "Valid forms" producer condition (2))
+template <bool SC1>
 DEV void store_out(const DecArgs& a, size_t elem, const bf16x8& v) {
-  if (a.sc1_out) {
+  if (SC1 && a.sc1_out) {
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, 0x7FFFFFFF, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (unsigned)(elem * 2), 0, 16);
   } else {
@@ -93,7 +94,9 @@ DEV void store_out(const DecArgs& a, size_t elem, const bf16x8& v) {
 // Returns (block-uniform) 1 when this block wrote its item's output rows (the
 // item's only block), 2 when it did as the last arriving block of a split
 // item, 0 when it wrote none.
-template <int G>
+// SC1: the fused form's write-through outputs are compiled in (attn_oproj_kernel
+// only; the plain kernel keeps round 5's direct stores and codegen)
+template <int G, bool SC1 = false>
 DEV int attn_decode_body(const DecArgs& a, const int b, const int kvh, const int z) {
   constexpr int TPR = 16 / G;                        // tokens per 16-row tile
   __shared__ __attribute__((aligned(16))) bf16 smem[NWV * TILE];   // per wave: V tile, then O
@@ -310,7 +313,7 @@ DEV int attn_decode_body(const DecArgs& a, const int b, const int kvh, const int
         ov[i] = (bf16)acc0[i];
         ov[4 + i] = (bf16)acc1[i];
       }
-      store_out(a, grow * D + 8 * c8, ov);
+      store_out<SC1>(a, grow * D + 8 * c8, ov);
     } else {
       // one of several blocks: its normalised partial, write-through
       const int zr = z - z_first;
@@ -380,7 +383,7 @@ DEV int attn_decode_body(const DecArgs& a, const int b, const int kvh, const int
     ov[i] = (bf16)(acc0[i] * inv);
     ov[4 + i] = (bf16)(acc1[i] * inv);
   }
-  store_out(a, grow * D + 8 * c8, ov);
+  store_out<SC1>(a, grow * D + 8 * c8, ov);
   return 2;
 }
 
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(const DecArgs a, con
     return;
   }
   const int rest = f / o.nitems;
-  const int wrote = attn_decode_body<G>(a, f - rest * o.nitems, rest % a.Hkv, rest / a.Hkv);
+  const int wrote = attn_decode_body<G, true>(a, f - rest * o.nitems, rest % a.Hkv, rest / a.Hkv);
   // hand-off of this block's rows (block-uniform: only writers signal, so the
   // padded items of a graph replay cost no atomics): sc1 stores drained by
   // every wave, a barrier, one relaxed agent-scope add; the reader's acquire
