@@ -63,7 +63,7 @@ _SPLIT_MIN_TILES = int(os.environ.get("MCP_KV_SPLIT_MIN_TILES", "4"))
 # 2 (was 1) - config 5 at 80 intents/s p50 195-196 -> 188-190 ms, p99 244 ->
 # 230, 120/s 321-333 -> 316-321 (profiles/attention_splitkv_min_tiles_ab.jsonl)
 _SPLIT_WORK_FACTOR = float(os.environ.get("MCP_KV_SPLIT_WORK_FACTOR", "2"))
-_SPLIT_SHORT = os.environ.get("MCP_KV_SPLIT_SHORT", "1") == "1"
+_SPLIT_SHORT = os.environ.get("MCP_KV_SPLIT_SHORT", "0") == "1"
 N_SIZES = 19            # packed segments of pack_host (the layout's leading entries)
 
 
@@ -110,7 +110,10 @@ def choose_kv_splits(q_lens, kv_lens, group: int, hkv: int, num_cus: int = 256,
     # (<= 8 rows each) split down to ONE tile per split - one sequence, 700
     # keys, 1-8 new tokens: 8 splits 10.6-12.0 us against 4 splits 12.3-13.2
     # (tools/bench_attention_decode.py, profiles/attention_decode_r6.jsonl);
-    # with 16-row spans 4 splits stay ahead.  MCP_KV_SPLIT_SHORT=0: off.
+    # with 16-row spans 4 splits stay ahead.  End to end it measured neutral
+    # (config 2 p50 85.3-85.7 vs 84.5-85.3 ms, config 5 at 20 / 40 intents/s
+    # +0.8 / -0.7 ms; profiles/kv_split_short_ab_r6.txt): MCP_KV_SPLIT_SHORT=1
+    # turns it on, default off.
     per = 4 if tiles >= 32 else 2
     if tiles < 16 and _SPLIT_SHORT and max(q_lens) <= 8:
         per = 1

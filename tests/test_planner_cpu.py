@@ -528,23 +528,25 @@ def test_engine_stall_recovers_after_the_step_returns():
 
 def test_kv_split_rule():
     """Split-KV only for decode-sized items that underfill the chip with own
-    key ranges of >= 4 tiles; >= 4 tiles per split from 32 tiles, >= 2 below,
-    1 below 16 tiles for spans of <= 8 rows (a single intent's ~700-key
-    context); forced / disabled by MCP_KV_SPLIT."""
+    key ranges of >= 4 tiles; >= 4 tiles per split from 32 tiles, >= 2 below
+    (a single intent's ~700-key context; 1 below 16 tiles for spans of <= 8
+    rows with MCP_KV_SPLIT_SHORT=1); forced / disabled by MCP_KV_SPLIT."""
     from mcp_amd.engine.batch import choose_kv_splits
     assert choose_kv_splits([1], [32768], 4, 8) == 64          # batch-1 decode, 32k keys
     assert choose_kv_splits([1] * 4, [32768] * 4, 4, 8) == 16
-    # short contexts with decode-sized spans: one tile per split (round 6)
-    assert choose_kv_splits([1], [700], 4, 8) == 8               # single intent: 11 tiles -> 8
-    assert choose_kv_splits([1], [400], 4, 8) == 4               # 7 tiles -> 4
-    assert choose_kv_splits([16], [700], 4, 8) == 4              # 16-row span: 11 tiles / 2 -> 4
+    assert choose_kv_splits([1], [700], 4, 8) == 4               # single intent: 11 tiles / 2 -> 5 -> power of two
+    assert choose_kv_splits([1], [400], 4, 8) == 2               # 7 tiles: 2 splits (serving-size steps)
+    # MCP_KV_SPLIT_SHORT=1 (opt-in, round 6): short contexts with decode-sized
+    # spans split down to one tile per split
     os_env = __import__("os").environ
-    os_env["MCP_KV_SPLIT_SHORT"] = "0"
+    os_env["MCP_KV_SPLIT_SHORT"] = "1"
+    import importlib
+    import mcp_amd.engine.batch as batch_mod
     try:
-        import importlib
-        import mcp_amd.engine.batch as batch_mod
         importlib.reload(batch_mod)
-        assert batch_mod.choose_kv_splits([1], [700], 4, 8) == 4  # round-5 rule: 11 tiles / 2 -> 4
+        assert batch_mod.choose_kv_splits([1], [700], 4, 8) == 8    # 11 tiles -> 8
+        assert batch_mod.choose_kv_splits([1], [400], 4, 8) == 4    # 7 tiles -> 4
+        assert batch_mod.choose_kv_splits([16], [700], 4, 8) == 4   # 16-row span: 11 / 2 -> 4
     finally:
         del os_env["MCP_KV_SPLIT_SHORT"]
         importlib.reload(batch_mod)
