@@ -331,6 +331,20 @@ void attn_kernel(const AttnArgs a) {
     const bf16* vb = a.vc + (blk * Hkv + kvh) * (size_t)TILE;
     bf16* base = smem + buf * 2 * TILE;
     const int rows_valid = kv_stop - kt * KT;              // >= 1 for a staged tile
+    if (rows_valid >= KT) {
+      // a full tile (every tile but a sequence's last): the straight DMA run
+      // - per-piece tests here cost a one-wave item walking ~11 tiles 43 %
+      // (one sequence, 700 keys: 27.0 vs 18.8 us, profiles/decode_unsplit_kernels_r6.md)
+#pragma unroll
+      for (int i = 0; i < PIECES / NW; ++i) {
+        const int p = wave * (PIECES / NW) + i;
+        const int tile = p >> 4, pr = p & 15;
+        const int row = pr * 4 + srow;
+        const int chunk = (lane & 15) ^ (row & 15);
+        glds16((tile ? vb : kb) + row * D + chunk * 8, base + tile * TILE + pr * 512);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < PIECES / NW; ++i) {
       const int p = wave * (PIECES / NW) + i;
